@@ -1,0 +1,319 @@
+"""ctypes binding of the C ABI in include/exacto_hip.h (libexacto_hip.so, built in-tree).
+
+This is the only way the Python side reaches the GPU path; there is no CPU fallback:
+if the shared library is missing, importing anything that needs it raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libexacto_hip.so")
+
+VARIANTS = ("InvalidParam", "DimensionMismatch", "ModulusMismatch", "InvalidRingDegree",
+            "DecryptionError", "DecompositionError", "LatticeError", "MissingKey", "NotImplemented")
+
+PATH_EXACT_RNS, PATH_HPS, PATH_SCHOOLBOOK = 0, 1, 2
+
+
+class ExactoError(Exception):
+    """Mirror of reference src/error.rs ExactoError: ``variant`` + Display text."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+        self.variant = VARIANTS[code - 1] if 1 <= code <= 9 else "HipError"
+
+
+class CtxInfo(C.Structure):
+    _fields_ = [("ring_degree", C.c_size_t), ("num_ct_moduli", C.c_size_t),
+                ("num_aux_moduli", C.c_size_t), ("num_internal_aux", C.c_size_t),
+                ("gadget_digits", C.c_size_t), ("gadget_base", C.c_uint64),
+                ("plain_modulus", C.c_uint64), ("mul_path", C.c_int), ("device", C.c_int)]
+
+
+_lib = None
+
+# (name, argtypes, restype)
+_P = C.c_void_p
+_SZ = C.c_size_t
+_U64 = C.c_uint64
+_SIGS = [
+    ("exacto_ctx_create", [C.POINTER(_P), _SZ, _P, _SZ, _P, _SZ, _U64, _U64, C.c_int], C.c_int),
+    ("exacto_ctx_destroy", [_P], None),
+    ("exacto_ctx_get_info", [_P, C.POINTER(CtxInfo)], C.c_int),
+    ("exacto_ctx_set_stream", [_P, _P], C.c_int),
+    ("exacto_ctx_set_chunk", [_P, _SZ], C.c_int),
+    ("exacto_synchronize", [_P], C.c_int),
+    ("exacto_ctx_load_relin_key", [_P, _P, _SZ], C.c_int),
+    ("exacto_ctx_load_relin_key_dev", [_P, _P, _SZ], C.c_int),
+    ("exacto_ctx_relin_key_buffer", [_P, _SZ], _P),
+    ("exacto_ntt_fwd", [_P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_ntt_inv", [_P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_ntt_fwd_dev", [_P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_ntt_inv_dev", [_P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_rns_fwd_dev", [_P, _P, _SZ], C.c_int),
+    ("exacto_rns_inv_dev", [_P, _P, _SZ], C.c_int),
+    ("exacto_rns_add_dev", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_rns_sub_dev", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_rns_neg_dev", [_P, _P, _P, _SZ], C.c_int),
+    ("exacto_rns_mul_dev", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_rns_scalar_mul_dev", [_P, _P, _U64, _P, _SZ], C.c_int),
+    ("exacto_bfv_add_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_bfv_sub_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_bfv_neg_dev", [_P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_bfv_mul_no_relin", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_mul_no_relin_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_relinearize", [_P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_relinearize_dev", [_P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_mul_and_relin", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_mul_and_relin_dev", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_gadget_decompose_dev", [_P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_dbfv_mul", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
+    ("exacto_dbfv_mul_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
+    ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
+    ("exacto_prof_enable", [_P, C.c_int], C.c_int),
+    ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
+                          C.POINTER(C.c_double), C.POINTER(_U64)], C.c_int),
+    ("exacto_version", [], C.c_char_p),
+]
+
+EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load() -> C.CDLL:
+    """Load libexacto_hip.so (raises if it has not been built: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError(f"{_LIB_PATH} not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = C.CDLL(_LIB_PATH)
+        for name, args, res in _SIGS:
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    lib = load()
+    buf = C.create_string_buffer(4096)
+    lib.exacto_last_error(buf, 4096)
+    return buf.value.decode("utf-8", "replace")
+
+
+def check(rc: int):
+    if rc != 0:
+        raise ExactoError(rc, last_error())
+
+
+def _ptr(a) -> int | None:
+    """Pointer of a numpy array (host) or a torch tensor (device or host)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        assert a.flags["C_CONTIGUOUS"]
+        return a.ctypes.data
+    return a.data_ptr()  # torch.Tensor
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+class HipContext:
+    """One device context = BfvParams (+ RnsBasis/NTT plans) on a GPU (exacto_ctx_create)."""
+
+    def __init__(self, ring_degree: int, ct_moduli, aux_moduli=(), plain_modulus: int = 65537,
+                 gadget_base: int = 0, device: int = 0):
+        lib = load()
+        ct = _u64(list(ct_moduli))
+        aux = _u64(list(aux_moduli)) if len(aux_moduli) else None
+        h = C.c_void_p()
+        check(lib.exacto_ctx_create(C.byref(h), ring_degree, ct.ctypes.data, len(ct),
+                                    aux.ctypes.data if aux is not None else None,
+                                    0 if aux is None else len(aux), plain_modulus, gadget_base,
+                                    device))
+        self._h = h
+        self._lib = lib
+        info = CtxInfo()
+        check(lib.exacto_ctx_get_info(h, C.byref(info)))
+        self.n = info.ring_degree
+        self.L = info.num_ct_moduli
+        self.G = info.gadget_digits
+        self.gadget_base = info.gadget_base
+        self.path = info.mul_path
+        self.num_internal_aux = info.num_internal_aux
+        self.ct_moduli = [int(q) for q in ct_moduli]
+
+    @classmethod
+    def from_params(cls, params, device=0):
+        """Build from an oracle-style / exacto_amd.params BfvParams object."""
+        aux = params.aux_basis.moduli if params.aux_basis is not None else []
+        return cls(params.ring_degree, params.ct_basis.moduli, aux, params.plain_modulus,
+                   params.gadget_base, device)
+
+    def close(self):
+        if self._h:
+            self._lib.exacto_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- configuration
+    def set_stream(self, stream_handle: int | None):
+        check(self._lib.exacto_ctx_set_stream(self._h, stream_handle))
+
+    def set_chunk(self, chunk: int):
+        check(self._lib.exacto_ctx_set_chunk(self._h, chunk))
+
+    def synchronize(self):
+        check(self._lib.exacto_synchronize(self._h))
+
+    # ---- relinearisation key
+    def load_relin_key(self, rlk: np.ndarray):
+        rlk = _u64(rlk)
+        nk = rlk.shape[0] if rlk.ndim == 4 else 0
+        check(self._lib.exacto_ctx_load_relin_key(self._h, rlk.ctypes.data if nk else None, nk))
+
+    def load_relin_key_dev(self, rlk_dev, num_keys: int):
+        check(self._lib.exacto_ctx_load_relin_key_dev(self._h, _ptr(rlk_dev), num_keys))
+
+    def relin_key_buffer(self, num_keys: int) -> int:
+        p = self._lib.exacto_ctx_relin_key_buffer(self._h, num_keys)
+        if not p:
+            raise ExactoError(100, last_error())
+        return p
+
+    # ---- host-pointer API (synchronous, numpy uint64)
+    def ntt_fwd(self, polys: np.ndarray, limb: int = 0) -> np.ndarray:
+        a = _u64(polys).copy()
+        check(self._lib.exacto_ntt_fwd(self._h, a.ctypes.data, a.size // self.n, limb))
+        return a
+
+    def ntt_inv(self, polys: np.ndarray, limb: int = 0) -> np.ndarray:
+        a = _u64(polys).copy()
+        check(self._lib.exacto_ntt_inv(self._h, a.ctypes.data, a.size // self.n, limb))
+        return a
+
+    def bfv_mul_no_relin(self, ct1: np.ndarray, ct2: np.ndarray) -> np.ndarray:
+        ct1, ct2 = _u64(ct1), _u64(ct2)
+        B = ct1.shape[0]
+        out = np.zeros((B, 3, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_bfv_mul_no_relin(self._h, ct1.ctypes.data, ct1.shape[1],
+                                                ct2.ctypes.data, ct2.shape[1], out.ctypes.data, B))
+        return out
+
+    def relinearize(self, ct: np.ndarray) -> np.ndarray:
+        ct = _u64(ct)
+        B, polys = ct.shape[0], ct.shape[1]
+        out = np.zeros((B, polys if polys < 3 else 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_relinearize(self._h, ct.ctypes.data, polys, out.ctypes.data, B))
+        return out
+
+    def bfv_mul_and_relin(self, ct1: np.ndarray, ct2: np.ndarray) -> np.ndarray:
+        ct1, ct2 = _u64(ct1), _u64(ct2)
+        B = ct1.shape[0]
+        out = np.zeros((B, 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_bfv_mul_and_relin(self._h, ct1.ctypes.data, ct2.ctypes.data,
+                                                 out.ctypes.data, B))
+        return out
+
+    def dbfv_mul(self, d, base, plain, a: np.ndarray, b: np.ndarray, depth_a=None, depth_b=None):
+        a, b = _u64(a), _u64(b)
+        B = a.shape[0]
+        out = np.zeros_like(a)
+        da = np.ascontiguousarray(depth_a, dtype=np.uint32) if depth_a is not None else None
+        db = np.ascontiguousarray(depth_b, dtype=np.uint32) if depth_b is not None else None
+        dout = np.zeros(B, dtype=np.uint32)
+        check(self._lib.exacto_dbfv_mul(self._h, d, base, plain, a.ctypes.data, b.ctypes.data,
+                                        out.ctypes.data, B, _ptr(da), _ptr(db), dout.ctypes.data))
+        return out, dout
+
+    # ---- device-pointer API (asynchronous; torch tensors or raw ints)
+    def _p(self, x):
+        return x if isinstance(x, int) else _ptr(x)
+
+    def ntt_fwd_dev(self, polys, count, limb=0):
+        check(self._lib.exacto_ntt_fwd_dev(self._h, self._p(polys), count, limb))
+
+    def ntt_inv_dev(self, polys, count, limb=0):
+        check(self._lib.exacto_ntt_inv_dev(self._h, self._p(polys), count, limb))
+
+    def rns_fwd_dev(self, polys, count):
+        check(self._lib.exacto_rns_fwd_dev(self._h, self._p(polys), count))
+
+    def rns_inv_dev(self, polys, count):
+        check(self._lib.exacto_rns_inv_dev(self._h, self._p(polys), count))
+
+    def rns_add_dev(self, a, b, out, count):
+        check(self._lib.exacto_rns_add_dev(self._h, self._p(a), self._p(b), self._p(out), count))
+
+    def rns_sub_dev(self, a, b, out, count):
+        check(self._lib.exacto_rns_sub_dev(self._h, self._p(a), self._p(b), self._p(out), count))
+
+    def rns_neg_dev(self, a, out, count):
+        check(self._lib.exacto_rns_neg_dev(self._h, self._p(a), self._p(out), count))
+
+    def rns_mul_dev(self, a, b, out, count):
+        check(self._lib.exacto_rns_mul_dev(self._h, self._p(a), self._p(b), self._p(out), count))
+
+    def rns_scalar_mul_dev(self, a, scalar, out, count):
+        check(self._lib.exacto_rns_scalar_mul_dev(self._h, self._p(a), scalar, self._p(out), count))
+
+    def bfv_add_dev(self, a, b, out, batch, polys=2):
+        check(self._lib.exacto_bfv_add_dev(self._h, self._p(a), self._p(b), self._p(out), batch, polys))
+
+    def bfv_sub_dev(self, a, b, out, batch, polys=2):
+        check(self._lib.exacto_bfv_sub_dev(self._h, self._p(a), self._p(b), self._p(out), batch, polys))
+
+    def bfv_neg_dev(self, a, out, batch, polys=2):
+        check(self._lib.exacto_bfv_neg_dev(self._h, self._p(a), self._p(out), batch, polys))
+
+    def bfv_mul_no_relin_dev(self, ct1, ct2, out, batch):
+        check(self._lib.exacto_bfv_mul_no_relin_dev(self._h, self._p(ct1), 2, self._p(ct2), 2,
+                                                    self._p(out), batch))
+
+    def relinearize_dev(self, ct, polys, out, batch):
+        check(self._lib.exacto_relinearize_dev(self._h, self._p(ct), polys, self._p(out), batch))
+
+    def bfv_mul_and_relin_dev(self, ct1, ct2, out, batch):
+        check(self._lib.exacto_bfv_mul_and_relin_dev(self._h, self._p(ct1), self._p(ct2),
+                                                     self._p(out), batch))
+
+    def gadget_decompose_dev(self, coeffs, digits, batch, num_digits):
+        check(self._lib.exacto_gadget_decompose_dev(self._h, self._p(coeffs), self._p(digits),
+                                                    batch, num_digits))
+
+    def dbfv_mul_dev(self, d, base, plain, a, b, out, batch, depth_a=None, depth_b=None):
+        da = np.ascontiguousarray(depth_a, dtype=np.uint32) if depth_a is not None else None
+        db = np.ascontiguousarray(depth_b, dtype=np.uint32) if depth_b is not None else None
+        check(self._lib.exacto_dbfv_mul_dev(self._h, d, base, plain, self._p(a), self._p(b),
+                                            self._p(out), batch, _ptr(da), _ptr(db), None))
+
+    # ---- profiling
+    def prof_enable(self, on=True):
+        check(self._lib.exacto_prof_enable(self._h, 1 if on else 0))
+
+    def prof_read(self, kind: int):
+        nl, pl = C.c_uint64(), C.c_uint64()
+        ms, by = C.c_double(), C.c_double()
+        check(self._lib.exacto_prof_read(self._h, kind, C.byref(nl), C.byref(ms), C.byref(by),
+                                         C.byref(pl)))
+        return {"launches": nl.value, "ms": ms.value, "bytes": by.value, "polys": pl.value}

@@ -1,0 +1,1024 @@
+// Host runtime and C ABI of libexacto_hip.so (see include/exacto_hip.h).
+//
+// Owns, per context: the prime set (ciphertext primes, then the auxiliary primes of
+// the selected multiplication path), per-prime NTT twiddle tables and constants in
+// HBM, the exact-CRT tables, the resident relinearisation key and a chunked
+// workspace.  Every `_dev` entry point only enqueues kernels on the context stream.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/exacto_hip.h"
+#include "exacto_internal.hpp"
+
+using namespace exacto;
+
+// ============================================================== errors
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+static int invalid_param(const std::string& s) { return fail(EXACTO_ERR_INVALID_PARAM, "invalid parameter: " + s); }
+
+#define HIP_TRY(x)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e_) +    \
+                                            " (" #x ")");                                       \
+    } while (0)
+
+#define CHECK_LAUNCH()                                                                          \
+    do {                                                                                        \
+        hipError_t e_ = hipGetLastError();                                                      \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(EXACTO_ERR_HIP, std::string("HIP launch error: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ============================================================== host integer helpers
+
+static u64 mulmod_h(u64 a, u64 b, u64 m) { return (u64)((u128)a * b % m); }
+
+static u64 powmod_h(u64 b, u64 e, u64 m) {
+    u64 r = 1 % m;
+    b %= m;
+    while (e) {
+        if (e & 1) r = mulmod_h(r, b, m);
+        b = mulmod_h(b, b, m);
+        e >>= 1;
+    }
+    return r;
+}
+
+static bool is_prime_h(u64 n) {
+    if (n < 2) return false;
+    static const u64 small[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    for (u64 p : small)
+        if (n % p == 0) return n == p;
+    u64 d = n - 1;
+    int s = 0;
+    while ((d & 1) == 0) { d >>= 1; ++s; }
+    for (u64 a : small) {
+        u64 x = powmod_h(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool comp = true;
+        for (int r = 1; r < s; ++r) {
+            x = mulmod_h(x, x, n);
+            if (x == n - 1) { comp = false; break; }
+        }
+        if (comp) return false;
+    }
+    return true;
+}
+
+// modular inverse via extended Euclid (returns 0 if not invertible)
+static u64 invmod_h(u64 a, u64 m) {
+    i128 t = 0, nt = 1, r = m, nr = a % m;
+    while (nr != 0) {
+        i128 q = r / nr;
+        i128 tmp = t - q * nt; t = nt; nt = tmp;
+        tmp = r - q * nr; r = nr; nr = tmp;
+    }
+    if (r != 1) return 0;
+    if (t < 0) t += m;
+    return (u64)t;
+}
+
+static u64 shoup_h(u64 w, u64 q) { return (u64)(((u128)w << 64) / q); }
+static int bitlen(u64 x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+static int bitrev(int x, int bits) {
+    int r = 0;
+    for (int i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
+    return r;
+}
+
+// psi: smallest x >= 2 with (x^((q-1)/2n))^n == -1 (oracle/ring.py find_psi)
+static u64 find_psi(u64 n, u64 q) {
+    const u64 e = (q - 1) / (2 * n);
+    for (u64 x = 2;; ++x) {
+        const u64 psi = powmod_h(x, e, q);
+        if (powmod_h(psi, n, q) == q - 1) return psi;
+    }
+}
+
+// --- minimal unsigned big integer (little-endian 64-bit words) ---
+struct Big {
+    std::vector<u64> w;
+    Big(u64 v = 0) { w.push_back(v); trim(); }
+    void trim() { while (w.size() > 1 && w.back() == 0) w.pop_back(); }
+    void mul(u64 m) {
+        u64 c = 0;
+        for (auto& x : w) { u128 t = (u128)x * m + c; x = (u64)t; c = (u64)(t >> 64); }
+        if (c) w.push_back(c);
+        trim();
+    }
+    void add(u64 a) {
+        for (size_t i = 0; i < w.size() && a; ++i) { u64 s = w[i] + a; a = s < a; w[i] = s; }
+        if (a) w.push_back(a);
+    }
+    void shr1() {
+        for (size_t i = 0; i < w.size(); ++i) w[i] = (w[i] >> 1) | (i + 1 < w.size() ? w[i + 1] << 63 : 0);
+        trim();
+    }
+    u64 mod(u64 m) const {
+        u128 r = 0;
+        for (size_t i = w.size(); i-- > 0;) r = ((r << 64) | w[i]) % m;
+        return (u64)r;
+    }
+    int cmp(const Big& o) const {
+        if (w.size() != o.w.size()) return w.size() < o.w.size() ? -1 : 1;
+        for (size_t i = w.size(); i-- > 0;)
+            if (w[i] != o.w[i]) return w[i] < o.w[i] ? -1 : 1;
+        return 0;
+    }
+};
+
+// mixed-radix digits of X (given as residues mod primes[0..cnt)) — host Garner
+static std::vector<u64> mixed_radix(const std::vector<u64>& res, const std::vector<u64>& pr) {
+    std::vector<u64> v(pr.size());
+    for (size_t i = 0; i < pr.size(); ++i) {
+        u64 t = res[i];
+        for (size_t k = 0; k < i; ++k) {
+            const u64 vk = v[k] % pr[i];
+            t = (t + pr[i] - vk) % pr[i];
+            t = mulmod_h(t, invmod_h(pr[k] % pr[i], pr[i]), pr[i]);
+        }
+        v[i] = t;
+    }
+    return v;
+}
+
+// ============================================================== context
+
+struct ProfRec {
+    int kind;
+    hipEvent_t a, b;
+    u64 polys;
+    double bytes;
+};
+
+struct exacto_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int n = 0, logn = 0, L = 0, K = 0;
+    std::vector<u64> ctq, user_aux, int_aux, primes;  // primes = ctq ++ (path aux)
+    u64 plain = 0, gbase = 0;
+    int G = 0;
+    int path = EXACTO_PATH_EXACT_RNS;
+    int deferred_code = 0;  // error raised at multiplication time (reference semantics)
+    std::string deferred_msg;
+    PrimeConst* d_primes = nullptr;
+    TwPair* d_tw = nullptr;
+    CrtTables* d_crt = nullptr;
+    CrtTables h_crt{};
+    u64* d_scal = nullptr;
+    u64* d_rlk = nullptr;
+    size_t rlk_keys = 0, rlk_cap = 0;
+    bool rlk_loaded = false;
+    // workspace (per chunk)
+    size_t chunk = 128;
+    size_t ws_items = 0;
+    u64 *ws_coefQ = nullptr, *ws_extP = nullptr, *ws_T = nullptr, *ws_D = nullptr;
+    // staging for host-pointer API and dBFV products
+    u64* io = nullptr;
+    size_t io_bytes = 0;
+    u64* prod = nullptr;
+    size_t prod_bytes = 0;
+    // dBFV plan cache
+    u64* d_off = nullptr;
+    size_t off_cap = 0;
+    size_t cached_B = 0, cached_d = 0;
+    u64 cached_base = 0, cached_p = 0;
+    int cached_npairs = 0;
+    int* d_term_start = nullptr;
+    CombineTerm* d_terms = nullptr;
+    size_t terms_cap = 0;
+    // profiling
+    bool prof = false;
+    std::vector<ProfRec> recs;
+};
+
+static void free_dev(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+static int grow(u64** buf, size_t* cap, size_t bytes) {
+    if (*cap >= bytes) return 0;
+    free_dev(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc((void**)buf, bytes));
+    *cap = bytes;
+    return 0;
+}
+
+static int plan_check(size_t n, u64 q) {
+    // make_plan (ntt.rs:19-29) via concrete-ntt Plan::try_new: prime q == 1 mod 2n, n >= 16.
+    // This library additionally needs q < 2^62 (lazy butterflies keep 4q < 2^64).
+    if (n < 16 || q < 2 || q >= (1ull << 62) || (q - 1) % (2 * n) != 0 || !is_prime_h(q))
+        return invalid_param("cannot create NTT plan for n=" + std::to_string(n) + ", q=" + std::to_string(q) +
+                             " (need prime q ≡ 1 mod " + std::to_string(2 * n));
+    return 0;
+}
+
+static PrimeConst make_prime_const(u64 q, int n, int logn, TwPair* h_fwd, TwPair* h_inv) {
+    PrimeConst P{};
+    P.q = q;
+    P.two_q = 2 * q;
+    P.mu64 = (u64)((((u128)1) << 64) / q);
+    P.bar_s = bitlen(q);
+    P.bar_mu = (u64)((((u128)1) << (2 * P.bar_s)) / q);
+    const u64 psi = find_psi(n, q);
+    const u64 psi_inv = invmod_h(psi, q);
+    for (int i = 0; i < n; ++i) {
+        const int e = bitrev(i, logn);
+        const u64 w = powmod_h(psi, e, q), wi = powmod_h(psi_inv, e, q);
+        h_fwd[i] = {w, shoup_h(w, q)};
+        h_inv[i] = {wi, shoup_h(wi, q)};
+    }
+    P.n_inv = invmod_h((u64)n % q, q);
+    P.n_inv_s = shoup_h(P.n_inv, q);
+    P.last_w = mulmod_h(h_inv[1].w, P.n_inv, q);
+    P.last_ws = shoup_h(P.last_w, q);
+    return P;
+}
+
+static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
+    w = v;
+    ws = shoup_h(v, q);
+}
+
+static int build_tables(exacto_ctx* c) {
+    const int NP = (int)c->primes.size();
+    std::vector<TwPair> tw((size_t)NP * 2 * c->n);
+    std::vector<PrimeConst> pc(NP);
+    for (int t = 0; t < NP; ++t)
+        pc[t] = make_prime_const(c->primes[t], c->n, c->logn, &tw[(size_t)t * 2 * c->n],
+                                 &tw[(size_t)t * 2 * c->n + c->n]);
+    HIP_TRY(hipMalloc((void**)&c->d_tw, tw.size() * sizeof(TwPair)));
+    HIP_TRY(hipMemcpy(c->d_tw, tw.data(), tw.size() * sizeof(TwPair), hipMemcpyHostToDevice));
+    for (int t = 0; t < NP; ++t) {
+        pc[t].tw_fwd = c->d_tw + (size_t)t * 2 * c->n;
+        pc[t].tw_inv = c->d_tw + (size_t)t * 2 * c->n + c->n;
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_primes, NP * sizeof(PrimeConst)));
+    HIP_TRY(hipMemcpy(c->d_primes, pc.data(), NP * sizeof(PrimeConst), hipMemcpyHostToDevice));
+
+    // ---- CRT tables
+    CrtTables& C = c->h_crt;
+    std::memset(&C, 0, sizeof(C));
+    const int L = c->L, K = c->K;
+    C.L = L;
+    C.K = K;
+    C.G = c->G;
+    C.gbase = c->gbase;
+    C.gshift = (c->gbase & (c->gbase - 1)) == 0 ? bitlen(c->gbase) - 1 : -1;
+    C.plain = c->plain;
+    const std::vector<u64> qv(c->primes.begin(), c->primes.begin() + L);
+    const std::vector<u64> pv(c->primes.begin() + L, c->primes.end());
+    for (int i = 0; i < L; ++i)
+        for (int k = 0; k < i; ++k) set_shoup(C.gq_w[i][k], C.gq_ws[i][k], invmod_h(qv[k] % qv[i], qv[i]), qv[i]);
+    Big Q(1);
+    for (u64 q : qv) Q.mul(q);
+    Big H = Q;
+    H.shr1();
+    {
+        std::vector<u64> hr(L);
+        for (int i = 0; i < L; ++i) hr[i] = H.mod(qv[i]);
+        auto mr = mixed_radix(hr, qv);
+        for (int i = 0; i < L; ++i) C.halfQ_mr[i] = mr[i];
+    }
+    for (int t = 0; t < NP; ++t) {
+        const u64 pt = c->primes[t];
+        u64 pref = 1 % pt;
+        for (int k = 0; k <= L; ++k) {
+            set_shoup(C.qpref_w[k][t], C.qpref_ws[k][t], pref, pt);
+            if (k < L) pref = mulmod_h(pref, qv[k] % pt, pt);
+        }
+        set_shoup(C.pmod_w[t], C.pmod_ws[t], c->plain % pt, pt);
+    }
+    for (int i = 0; i < L && i < (int)Q.w.size(); ++i) C.Qwords[i] = Q.w[i];
+    if (c->path == EXACTO_PATH_HPS) {
+        const u64 q = qv[0];
+        for (int a = 0; a < K && a < 2; ++a) C.hps_qinv[a] = invmod_h(q % pv[a], pv[a]);
+        if (K == 2) {
+            C.hps_p1_inv_p0 = invmod_h(pv[1] % pv[0], pv[0]);
+            C.hps_p0_inv_p1 = invmod_h(pv[0] % pv[1], pv[1]);
+        }
+    } else {
+        for (int a = 0; a < K; ++a)
+            for (int k = 0; k < a; ++k) set_shoup(C.gp_w[a][k], C.gp_ws[a][k], invmod_h(pv[k] % pv[a], pv[a]), pv[a]);
+        Big P(1);
+        for (u64 p : pv) P.mul(p);
+        Big HP = P;
+        HP.shr1();
+        std::vector<u64> hr(K);
+        for (int a = 0; a < K; ++a) hr[a] = HP.mod(pv[a]);
+        auto mr = mixed_radix(hr, pv);
+        for (int a = 0; a < K; ++a) C.halfP_mr[a] = mr[a];
+        for (int i = 0; i < L; ++i) {
+            u64 pref = 1 % qv[i];
+            for (int k = 0; k <= K; ++k) {
+                set_shoup(C.ppref_w[k][i], C.ppref_ws[k][i], pref, qv[i]);
+                if (k < K) pref = mulmod_h(pref, pv[k] % qv[i], qv[i]);
+            }
+        }
+        for (int a = 0; a < K; ++a) set_shoup(C.qinvp_w[a], C.qinvp_ws[a], invmod_h(Q.mod(pv[a]), pv[a]), pv[a]);
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
+    HIP_TRY(hipMalloc((void**)&c->d_crt, sizeof(CrtTables)));
+    HIP_TRY(hipMemcpy(c->d_crt, &C, sizeof(CrtTables), hipMemcpyHostToDevice));
+    return 0;
+}
+
+extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_moduli, size_t L,
+                                 const uint64_t* aux_moduli, size_t num_aux, uint64_t plain,
+                                 uint64_t gadget_base, int device) {
+    if (!out) return invalid_param("null context pointer");
+    *out = nullptr;
+    // BfvParamsBuilder::build order (params/mod.rs:81-98)
+    if (n < 2 || (n & (n - 1)) != 0)
+        return fail(EXACTO_ERR_INVALID_RING_DEGREE, "ring degree must be a power of 2, got " + std::to_string(n));
+    if (L == 0 || !ct_moduli) return invalid_param("must specify at least one ciphertext modulus");
+    if (plain < 2) return invalid_param("plaintext modulus must be >= 2");
+    if (n > 16384) return invalid_param("ring degree " + std::to_string(n) + " exceeds the HIP NTT limit of 16384");
+    if (L > EXACTO_MAX_L) return invalid_param("at most " + std::to_string(EXACTO_MAX_L) + " ciphertext moduli are supported");
+    for (size_t i = 0; i < L; ++i)
+        if (int e = plan_check(n, ct_moduli[i])) return e;
+    for (size_t i = 0; i < L; ++i)
+        for (size_t k = 0; k < i; ++k)
+            if (ct_moduli[i] == ct_moduli[k]) return invalid_param("RNS moduli must be coprime");
+    for (size_t i = 0; i < num_aux; ++i)
+        if (int e = plan_check(n, aux_moduli[i])) return e;
+
+    exacto_ctx* c = new exacto_ctx();
+    c->device = device;
+    c->n = (int)n;
+    c->logn = bitlen(n) - 1;
+    c->L = (int)L;
+    c->ctq.assign(ct_moduli, ct_moduli + L);
+    if (num_aux) c->user_aux.assign(aux_moduli, aux_moduli + num_aux);
+    c->plain = plain;
+    c->gbase = gadget_base == 0 ? (1ull << 16) : gadget_base;
+    if (c->gbase < 2) { delete c; return invalid_param("gadget base must be >= 2"); }
+    // compute_gadget_digits (params/mod.rs:126-140)
+    {
+        Big Q(1);
+        for (u64 q : c->ctq) Q.mul(q);
+        Big pw(1);
+        int g = 0;
+        while (pw.cmp(Q) < 0) { pw.mul(c->gbase); ++g; }
+        c->G = std::max(g, 1);
+    }
+    if (c->G > EXACTO_MAX_G) { delete c; return invalid_param("gadget digit count exceeds " + std::to_string(EXACTO_MAX_G)); }
+    // dispatcher (eval.rs:99-107)
+    if (L > 1) {
+        c->path = EXACTO_PATH_EXACT_RNS;
+    } else if (num_aux > 0) {
+        c->path = EXACTO_PATH_HPS;
+        const u64 q = c->ctq[0];
+        if (num_aux == 1) {
+            const u128 min_required = ((u128)n * q) / 2;
+            if ((u128)c->user_aux[0] <= min_required) {
+                c->deferred_code = EXACTO_ERR_INVALID_PARAM;
+                c->deferred_msg = "invalid parameter: single aux prime too small for HPS centering: P=" +
+                                  std::to_string(c->user_aux[0]) + " <= n*Q/2=" + std::to_string((u64)min_required);
+            }
+        } else if (num_aux > 2) {
+            c->deferred_code = EXACTO_ERR_INVALID_PARAM;
+            c->deferred_msg = "invalid parameter: HPS scaling supports 1 or 2 aux primes, got " + std::to_string(num_aux);
+        }
+    } else {
+        c->path = EXACTO_PATH_SCHOOLBOOK;
+        // schoolbook_overflow_risk (eval.rs:457-464), u128 saturating
+        const u128 maxc = c->ctq[0] / 2;
+        const u128 sat = ~(u128)0;
+        const u128 i128max = sat >> 1;
+        auto smul = [&](u128 a, u128 b) -> u128 { return (b != 0 && a > sat / b) ? sat : a * b; };
+        const u128 max_tensor = smul(smul((u128)n, maxc), maxc);
+        const u128 max_scaled = smul(max_tensor, (u128)plain);
+        if (max_tensor > i128max || max_scaled > i128max) {
+            c->deferred_code = EXACTO_ERR_NOT_IMPLEMENTED;
+            c->deferred_msg = "not yet implemented: schoolbook BFV multiplication can overflow i128 for these "
+                              "parameters; use HPS auxiliary basis";
+        }
+    }
+    c->primes = c->ctq;
+    if (c->path == EXACTO_PATH_HPS) {
+        if (num_aux <= 2) {
+            c->K = (int)num_aux;
+            for (u64 p : c->user_aux) c->primes.push_back(p);
+        }
+    } else {
+        // internal auxiliary basis P > 4 * p * n * Q (exact tensor and exact rounding fit)
+        Big need(4);
+        need.mul(plain);
+        need.mul(n);
+        for (u64 q : c->ctq) need.mul(q);
+        Big P(1);
+        const u64 step = 2 * n;
+        u64 cand = ((1ull << 62) - 1) / step * step + 1;
+        while (P.cmp(need) <= 0) {
+            while (cand > step) {
+                cand -= step;
+                const bool used = std::find(c->ctq.begin(), c->ctq.end(), cand) != c->ctq.end();
+                if (!used && is_prime_h(cand)) break;
+            }
+            c->int_aux.push_back(cand);
+            P.mul(cand);
+            if ((int)c->int_aux.size() > EXACTO_MAX_K) {
+                delete c;
+                return invalid_param("too many auxiliary primes required for exact multiplication");
+            }
+        }
+        c->K = (int)c->int_aux.size();
+        for (u64 p : c->int_aux) c->primes.push_back(p);
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
+    e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
+    c->own_stream = true;
+    if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
+    *out = c;
+    return 0;
+}
+
+extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+    free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk);
+    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D);
+    free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
+    if (!c || !info) return invalid_param("null argument");
+    info->ring_degree = c->n;
+    info->num_ct_moduli = c->L;
+    info->num_aux_moduli = c->user_aux.size();
+    info->num_internal_aux = c->int_aux.size();
+    info->gadget_digits = c->G;
+    info->gadget_base = c->gbase;
+    info->plain_modulus = c->plain;
+    info->mul_path = c->path;
+    info->device = c->device;
+    return 0;
+}
+
+extern "C" int exacto_ctx_set_stream(exacto_ctx* c, void* s) {
+    if (!c) return invalid_param("null context");
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->own_stream && c->stream) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipStreamDestroy(c->stream));
+    }
+    if (s) {
+        c->stream = (hipStream_t)s;
+        c->own_stream = false;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return 0;
+}
+
+extern "C" int exacto_ctx_set_chunk(exacto_ctx* c, size_t chunk) {
+    if (!c) return invalid_param("null context");
+    c->chunk = chunk == 0 ? 128 : chunk;
+    return 0;
+}
+
+extern "C" int exacto_synchronize(exacto_ctx* c) {
+    if (!c) return invalid_param("null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static size_t poly_bytes(const exacto_ctx* c) { return (size_t)c->n * sizeof(u64); }
+
+extern "C" uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* c, size_t num_keys) {
+    if (!c) return nullptr;
+    const size_t bytes = num_keys * 2 * c->L * poly_bytes(c);
+    if (hipSetDevice(c->device) != hipSuccess) return nullptr;
+    if (grow(&c->d_rlk, &c->rlk_cap, std::max<size_t>(bytes, 8))) return nullptr;
+    c->rlk_keys = num_keys;
+    c->rlk_loaded = true;
+    return c->d_rlk;
+}
+
+extern "C" int exacto_ctx_load_relin_key_dev(exacto_ctx* c, const uint64_t* rlk, size_t num_keys) {
+    if (!c) return invalid_param("null context");
+    if (num_keys && !rlk) return invalid_param("null relinearization key");
+    u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
+    if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
+    if (num_keys)
+        HIP_TRY(hipMemcpyAsync(dst, rlk, num_keys * 2 * c->L * poly_bytes(c), hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+}
+
+extern "C" int exacto_ctx_load_relin_key(exacto_ctx* c, const uint64_t* rlk, size_t num_keys) {
+    if (!c) return invalid_param("null context");
+    if (num_keys && !rlk) return invalid_param("null relinearization key");
+    u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
+    if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
+    if (num_keys) HIP_TRY(hipMemcpy(dst, rlk, num_keys * 2 * c->L * poly_bytes(c), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// ============================================================== NTT helper (+ profiling)
+
+static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) {
+    if (count <= 0) return 0;
+    ProfRec rec{};
+    if (c->prof) {
+        HIP_TRY(hipEventCreate(&rec.a));
+        HIP_TRY(hipEventCreate(&rec.b));
+        HIP_TRY(hipEventRecord(rec.a, c->stream));
+    }
+    launch_ntt(nb, (int)count, c->logn, inverse, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (c->prof) {
+        HIP_TRY(hipEventRecord(rec.b, c->stream));
+        rec.kind = inverse ? 1 : 0;
+        rec.polys = (u64)count;
+        rec.bytes = 16.0 * c->n * (double)count;
+        c->recs.push_back(rec);
+    }
+    return 0;
+}
+
+static NttBatch contiguous(u64* data, long count_items, long poly_per_item, int prime_base, int period,
+                           int n) {
+    (void)count_items;
+    NttBatch nb{};
+    nb.src = data;
+    nb.src_off = nullptr;
+    nb.src_item_stride = poly_per_item * n;
+    nb.dst = data;
+    nb.dst_item_stride = poly_per_item * n;
+    nb.ppi = (int)poly_per_item;
+    nb.prime_base = prime_base;
+    nb.period = period;
+    return nb;
+}
+
+// ============================================================== workspace
+
+static int ensure_workspace(exacto_ctx* c, size_t items) {
+    if (c->ws_items >= items) return 0;
+    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D);
+    c->ws_coefQ = c->ws_extP = c->ws_T = c->ws_D = nullptr;
+    c->ws_items = 0;
+    const size_t pb = poly_bytes(c);
+    const int NP = c->L + c->K;
+    HIP_TRY(hipMalloc((void**)&c->ws_coefQ, items * 4 * c->L * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws_extP, items * 4 * std::max(c->K, 1) * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws_T, items * 3 * NP * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws_D, items * std::max(c->G, 1) * c->L * pb));
+    c->ws_items = items;
+    return 0;
+}
+
+// ============================================================== multiplication pipeline
+
+// products [0, P): ct1 = op.a + off_a(p), ct2 = op.b + off_b(p) (each [2][L][n], NTT domain).
+// relin: out[p] = [2][L][n] = relinearize(mul_no_relin); else out[p] = [3][L][n].
+static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out_stride, bool relin) {
+    if (c->deferred_code) return fail(c->deferred_code, c->deferred_msg);
+    if (relin && !c->rlk_loaded) return fail(EXACTO_ERR_MISSING_KEY, "key not available: relinearization key not loaded");
+    if (P <= 0) return 0;
+    const int n = c->n, L = c->L, K = c->K, NP = L + K;
+    const long Ln = (long)L * n;
+    const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
+    const size_t C = std::min<size_t>(c->chunk, (size_t)P);
+    if (int e = ensure_workspace(c, C)) return e;
+    for (long s = 0; s < P; s += (long)C) {
+        const int cnt = (int)std::min<long>((long)C, P - s);
+        Operands o = op;
+        if (o.a_off) o.a_off += s; else o.a += s * o.a_stride;
+        if (o.b_off) o.b_off += s; else o.b += s * o.b_stride;
+        // 1. inputs -> coefficient domain (INTT), coefQ[item] = [c0, c1, d0, d1][L][n]
+        NttBatch nb{};
+        nb.src = o.a; nb.src_off = o.a_off; nb.src_item_stride = o.a_stride;
+        nb.dst = c->ws_coefQ; nb.dst_item_stride = 4 * Ln;
+        nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
+        if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
+        nb.src = o.b; nb.src_off = o.b_off; nb.src_item_stride = o.b_stride;
+        nb.dst = c->ws_coefQ + 2 * Ln;
+        if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
+        // 2. extension to the auxiliary primes
+        if (c->path == EXACTO_PATH_HPS)
+            launch_hps_extend(c->ws_coefQ, c->ws_extP, cnt, n, c->d_primes, K, c->stream);
+        else
+            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->stream);
+        CHECK_LAUNCH();
+        // 3. forward NTT of the extended polynomials
+        if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
+        // 4. tensor product in every prime
+        launch_tensor(o, c->ws_extP, c->ws_T, cnt, n, L, K, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+        // 5. back to coefficients
+        if (int e = run_ntt(c, contiguous(c->ws_T, cnt, 3L * NP, 0, NP, n), (long)cnt * 3 * NP, true)) return e;
+        // 6. scale-and-round (+ gadget digits of the third component)
+        u64* R = out + s * out_stride;
+        const int ncomp = relin ? 2 : 3;
+        u64* D = relin ? c->ws_D : nullptr;
+        if (c->path == EXACTO_PATH_HPS)
+            launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
+        else
+            launch_exact_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, L, K, c->stream);
+        CHECK_LAUNCH();
+        // 7. forward NTT of the results (and digits)
+        NttBatch rb{};
+        rb.src = R; rb.src_off = nullptr; rb.src_item_stride = out_stride;
+        rb.dst = R; rb.dst_item_stride = out_stride;
+        rb.ppi = ncomp * L; rb.prime_base = 0; rb.period = L;
+        if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
+        if (relin && guse > 0) {
+            if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false)) return e;
+            // 8. relinearisation MAC, in place on the output
+            launch_relin_mac(R, nullptr, out_stride, 0, c->ws_D, c->d_rlk, guse, R, out_stride, cnt, n, L,
+                             c->d_primes, c->stream);
+            CHECK_LAUNCH();
+        }
+    }
+    return 0;
+}
+
+// ============================================================== C ABI: NTT / RNS
+
+static int check_ctx(exacto_ctx* c) {
+    if (!c) return invalid_param("null context");
+    HIP_TRY(hipSetDevice(c->device));
+    return 0;
+}
+
+static int ntt_dev(exacto_ctx* c, uint64_t* polys, size_t count, size_t limb, bool inverse) {
+    if (int e = check_ctx(c)) return e;
+    if (limb >= (size_t)c->L)
+        return fail(EXACTO_ERR_DIMENSION_MISMATCH, "dimension mismatch: expected limb < " + std::to_string(c->L) + ", got " + std::to_string(limb));
+    return run_ntt(c, contiguous(polys, count, 1, (int)limb, 1, c->n), (long)count, inverse);
+}
+
+extern "C" int exacto_ntt_fwd_dev(exacto_ctx* c, uint64_t* p, size_t count, size_t limb) { return ntt_dev(c, p, count, limb, false); }
+extern "C" int exacto_ntt_inv_dev(exacto_ctx* c, uint64_t* p, size_t count, size_t limb) { return ntt_dev(c, p, count, limb, true); }
+
+extern "C" int exacto_rns_fwd_dev(exacto_ctx* c, uint64_t* p, size_t count) {
+    if (int e = check_ctx(c)) return e;
+    return run_ntt(c, contiguous(p, count, c->L, 0, c->L, c->n), (long)count * c->L, false);
+}
+extern "C" int exacto_rns_inv_dev(exacto_ctx* c, uint64_t* p, size_t count) {
+    if (int e = check_ctx(c)) return e;
+    return run_ntt(c, contiguous(p, count, c->L, 0, c->L, c->n), (long)count * c->L, true);
+}
+
+static int stage(exacto_ctx* c, size_t bytes) {
+    if (grow(&c->io, &c->io_bytes, bytes)) return EXACTO_ERR_HIP;
+    return 0;
+}
+
+static int ntt_host(exacto_ctx* c, uint64_t* polys, size_t count, size_t limb, bool inverse) {
+    if (int e = check_ctx(c)) return e;
+    const size_t bytes = count * poly_bytes(c);
+    if (int e = stage(c, std::max<size_t>(bytes, 8))) return e;
+    HIP_TRY(hipMemcpy(c->io, polys, bytes, hipMemcpyHostToDevice));
+    if (int e = ntt_dev(c, c->io, count, limb, inverse)) return e;
+    HIP_TRY(hipMemcpyAsync(polys, c->io, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+extern "C" int exacto_ntt_fwd(exacto_ctx* c, uint64_t* p, size_t count, size_t limb) { return ntt_host(c, p, count, limb, false); }
+extern "C" int exacto_ntt_inv(exacto_ctx* c, uint64_t* p, size_t count, size_t limb) { return ntt_host(c, p, count, limb, true); }
+
+static int pw(exacto_ctx* c, PwOp op, const u64* a, const u64* b, u64* out, long polys, const u64* scal) {
+    if (int e = check_ctx(c)) return e;
+    launch_pointwise(op, a, b, out, polys, c->n, c->L, scal, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_rns_add_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t n) {
+    return pw(c, PwOp::Add, a, b, o, (long)n * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_rns_sub_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t n) {
+    return pw(c, PwOp::Sub, a, b, o, (long)n * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_rns_neg_dev(exacto_ctx* c, const uint64_t* a, uint64_t* o, size_t n) {
+    return pw(c, PwOp::Neg, a, nullptr, o, (long)n * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_rns_mul_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t n) {
+    return pw(c, PwOp::Mul, a, b, o, (long)n * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_rns_scalar_mul_dev(exacto_ctx* c, const uint64_t* a, uint64_t scalar, uint64_t* o, size_t n) {
+    if (int e = check_ctx(c)) return e;
+    // s = scalar % q_i per limb (ntt.rs:136); tiny synchronous upload into the context's table
+    u64 sm[EXACTO_MAX_L];
+    for (int i = 0; i < c->L; ++i) sm[i] = scalar % c->ctq[i];
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->d_scal, sm, c->L * sizeof(u64), hipMemcpyHostToDevice));
+    return pw(c, PwOp::ScalarMul, a, nullptr, o, (long)n * c->L, c->d_scal);
+}
+
+// bfv_add / bfv_sub / bfv_neg over equal-degree ciphertexts (eval.rs:14-60)
+extern "C" int exacto_bfv_add_dev(exacto_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* o, size_t B, size_t polys) {
+    return pw(c, PwOp::Add, x, y, o, (long)B * polys * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_bfv_sub_dev(exacto_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* o, size_t B, size_t polys) {
+    return pw(c, PwOp::Sub, x, y, o, (long)B * polys * (c ? c->L : 0), nullptr);
+}
+extern "C" int exacto_bfv_neg_dev(exacto_ctx* c, const uint64_t* x, uint64_t* o, size_t B, size_t polys) {
+    return pw(c, PwOp::Neg, x, nullptr, o, (long)B * polys * (c ? c->L : 0), nullptr);
+}
+
+// ============================================================== C ABI: BFV
+
+static Operands plain_operands(const exacto_ctx* c, const u64* a, const u64* b) {
+    Operands op{};
+    op.a = a; op.a_off = nullptr; op.a_stride = 2L * c->L * c->n;
+    op.b = b; op.b_off = nullptr; op.b_stride = 2L * c->L * c->n;
+    return op;
+}
+
+extern "C" int exacto_bfv_mul_no_relin_dev(exacto_ctx* c, const uint64_t* ct1, size_t polys1,
+                                           const uint64_t* ct2, size_t polys2, uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (polys1 != 2 || polys2 != 2) return invalid_param("multiplication requires degree-1 ciphertexts");
+    return run_mul(c, plain_operands(c, ct1, ct2), (long)B, out, 3L * c->L * c->n, false);
+}
+
+extern "C" int exacto_bfv_mul_and_relin_dev(exacto_ctx* c, const uint64_t* ct1, const uint64_t* ct2,
+                                            uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    return run_mul(c, plain_operands(c, ct1, ct2), (long)B, out, 2L * c->L * c->n, true);
+}
+
+extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    const long Ln = (long)c->L * c->n;
+    if (polys < 3) {  // keyswitch.rs:63-65: already degree-1, cloned
+        for (size_t b = 0; b < B; ++b)
+            HIP_TRY(hipMemcpyAsync(out + b * 2 * Ln, ct + b * polys * Ln, polys * Ln * sizeof(u64),
+                                   hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    }
+    if (polys > 3) return invalid_param("relinearization only supports degree-2 ciphertexts");
+    if (!c->rlk_loaded) return fail(EXACTO_ERR_MISSING_KEY, "key not available: relinearization key not loaded");
+    const int guse = (int)std::min<size_t>(c->G, c->rlk_keys);
+    const size_t C = std::min<size_t>(c->chunk, std::max<size_t>(B, 1));
+    if (int e = ensure_workspace(c, C)) return e;
+    for (size_t s = 0; s < B; s += C) {
+        const int cnt = (int)std::min(C, B - s);
+        const u64* src = ct + s * 3 * Ln;
+        u64* dst = out + s * 2 * Ln;
+        // c0, c1 copied, then accumulated in place
+        HIP_TRY(hipMemcpy2DAsync(dst, 2 * Ln * sizeof(u64), src, 3 * Ln * sizeof(u64), 2 * Ln * sizeof(u64), cnt,
+                                 hipMemcpyDeviceToDevice, c->stream));
+        if (guse == 0) continue;
+        NttBatch nb{};
+        nb.src = src + 2 * Ln; nb.src_off = nullptr; nb.src_item_stride = 3 * Ln;
+        nb.dst = c->ws_coefQ; nb.dst_item_stride = Ln;
+        nb.ppi = c->L; nb.prime_base = 0; nb.period = c->L;
+        if (int e = run_ntt(c, nb, (long)cnt * c->L, true)) return e;
+        launch_decompose(c->ws_coefQ, Ln, c->ws_D, guse, cnt, c->n, c->d_crt, c->d_primes, c->L, c->stream);
+        CHECK_LAUNCH();
+        if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * c->L, 0, c->L, c->n), (long)cnt * guse * c->L, false)) return e;
+        launch_relin_mac(dst, nullptr, 2 * Ln, 0, c->ws_D, c->d_rlk, guse, dst, 2 * Ln, cnt, c->n, c->L, c->d_primes,
+                         c->stream);
+        CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+extern "C" int exacto_gadget_decompose_dev(exacto_ctx* c, const uint64_t* coeffs, uint64_t* digits, size_t B,
+                                           size_t num_digits) {
+    if (int e = check_ctx(c)) return e;
+    const int guse = (int)std::min<size_t>(c->G, num_digits);
+    launch_decompose(coeffs, (long)c->L * c->n, digits, guse, (int)B, c->n, c->d_crt, c->d_primes, c->L, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+// host-pointer wrappers: stage inputs in the context's io buffer, run the _dev entry, copy back
+static int host_call(exacto_ctx* c, const std::vector<std::pair<const void*, size_t>>& ins, size_t out_bytes,
+                     void* host_out, const std::function<int(std::vector<u64*>&, u64*)>& fn) {
+    if (int e = check_ctx(c)) return e;
+    size_t total = out_bytes;
+    for (auto& in : ins) total += (in.second + 255) / 256 * 256;
+    if (int e = stage(c, std::max<size_t>(total, 8))) return e;
+    std::vector<u64*> dins;
+    char* p = (char*)c->io;
+    for (auto& in : ins) {
+        HIP_TRY(hipMemcpy(p, in.first, in.second, hipMemcpyHostToDevice));
+        dins.push_back((u64*)p);
+        p += (in.second + 255) / 256 * 256;
+    }
+    u64* dout = (u64*)p;
+    if (int e = fn(dins, dout)) return e;
+    HIP_TRY(hipMemcpyAsync(host_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int exacto_bfv_mul_no_relin(exacto_ctx* c, const uint64_t* ct1, size_t p1, const uint64_t* ct2, size_t p2,
+                                       uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{ct1, ctb}, {ct2, ctb}}, B * 3 * c->L * poly_bytes(c), out,
+                     [&](std::vector<u64*>& d, u64* o) { return exacto_bfv_mul_no_relin_dev(c, d[0], p1, d[1], p2, o, B); });
+}
+
+extern "C" int exacto_bfv_mul_and_relin(exacto_ctx* c, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out,
+                                        size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{ct1, ctb}, {ct2, ctb}}, ctb, out,
+                     [&](std::vector<u64*>& d, u64* o) { return exacto_bfv_mul_and_relin_dev(c, d[0], d[1], o, B); });
+}
+
+extern "C" int exacto_relinearize(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t inb = B * polys * c->L * poly_bytes(c);
+    const size_t outp = polys < 3 ? polys : 2;
+    return host_call(c, {{ct, inb}}, B * outp * c->L * poly_bytes(c), out,
+                     [&](std::vector<u64*>& d, u64* o) { return exacto_relinearize_dev(c, d[0], polys, o, B); });
+}
+
+// ============================================================== C ABI: dBFV
+
+// lattice.rs:104-122 compute_simple + decomposition.rs:8-16 digit_decompose
+static std::vector<std::vector<i64>> small_reps(u64 base, size_t d, u64 p) {
+    std::vector<std::vector<i64>> reps;
+    for (size_t j = d; j + 1 < 2 * d; ++j) {
+        u64 val;
+        if (p == 0) {
+            val = 1;
+            for (size_t e = 0; e < j; ++e) val *= base;  // wrapping_pow
+        } else {
+            val = powmod_h(base, j, p);
+        }
+        std::vector<i64> dg;
+        u64 rem = val;
+        for (size_t k = 0; k < d; ++k) { dg.push_back((i64)(rem % base)); rem /= base; }
+        reps.push_back(dg);
+    }
+    return reps;
+}
+
+static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
+    if (c->cached_B == B && c->cached_d == d && c->cached_base == base && c->cached_p == plain && c->d_off) return 0;
+    const auto reps = small_reps(base, d, plain);
+    std::vector<std::pair<int, int>> pairs;
+    for (size_t i = 0; i < d; ++i)
+        for (size_t j = 0; j < d; ++j) {
+            const size_t k = i + j;
+            bool needed = k < d;
+            if (!needed)
+                for (i64 v : reps[k - d]) needed |= (v != 0);
+            if (needed) pairs.push_back({(int)i, (int)j});
+        }
+    const int npairs = (int)pairs.size();
+    // combine terms: out limb k' <- sum over pairs with i+j == k' (coef 1) and reps folding
+    std::vector<int> start(d + 1, 0);
+    std::vector<CombineTerm> terms;
+    for (size_t ko = 0; ko < d; ++ko) {
+        start[ko] = (int)terms.size();
+        for (int pi = 0; pi < npairs; ++pi) {
+            const size_t k = pairs[pi].first + pairs[pi].second;
+            i64 coef = 0;
+            if (k == ko) coef = 1;
+            else if (k >= d) coef = reps[k - d][ko];
+            if (coef != 0) terms.push_back({pi, 0, coef});
+        }
+    }
+    start[d] = (int)terms.size();
+    const long Ln2 = 2L * c->L * c->n;
+    std::vector<u64> off(2 * B * npairs);
+    for (size_t b = 0; b < B; ++b)
+        for (int pi = 0; pi < npairs; ++pi) {
+            off[b * npairs + pi] = (u64)((b * d + pairs[pi].first) * Ln2);
+            off[B * npairs + b * npairs + pi] = (u64)((b * d + pairs[pi].second) * Ln2);
+        }
+    size_t cap = c->off_cap;
+    if (grow(&c->d_off, &cap, off.size() * sizeof(u64) + 8)) return EXACTO_ERR_HIP;
+    c->off_cap = cap;
+    HIP_TRY(hipMemcpy(c->d_off, off.data(), off.size() * sizeof(u64), hipMemcpyHostToDevice));
+    free_dev(c->d_term_start);
+    free_dev(c->d_terms);
+    HIP_TRY(hipMalloc((void**)&c->d_term_start, start.size() * sizeof(int)));
+    HIP_TRY(hipMemcpy(c->d_term_start, start.data(), start.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc((void**)&c->d_terms, std::max<size_t>(terms.size(), 1) * sizeof(CombineTerm)));
+    if (!terms.empty())
+        HIP_TRY(hipMemcpy(c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm), hipMemcpyHostToDevice));
+    c->cached_B = B; c->cached_d = d; c->cached_base = base; c->cached_p = plain;
+    c->cached_npairs = npairs;
+    return 0;
+}
+
+extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                                   const uint64_t* b, uint64_t* out, size_t B, const uint32_t* depth_a,
+                                   const uint32_t* depth_b, uint32_t* depth_out) {
+    if (int e = check_ctx(c)) return e;
+    // DbfvParams::new checks (params/mod.rs:168-184)
+    if (base < 2) return invalid_param("base must be >= 2");
+    if (d < 1) return invalid_param("num_digits must be >= 1");
+    {
+        u128 bd = 1;
+        const u128 sat = ~(u128)0;
+        for (size_t i = 0; i < d; ++i) bd = (bd > sat / base) ? sat : bd * base;
+        const u128 p128 = plain == 0 ? ((u128)1 << 64) : (u128)plain;
+        if (bd < p128) {
+            auto u128s = [](u128 v) { std::string s; do { s.insert(s.begin(), char('0' + (int)(v % 10))); v /= 10; } while (v); return s; };
+            return invalid_param("base^digits = " + u128s(bd) + " < plain_modulus = " + u128s(p128));
+        }
+    }
+    // depth guard (dbfv/eval.rs:96-102)
+    for (size_t i = 0; i < B; ++i) {
+        const uint32_t da = depth_a ? depth_a[i] : 0, db = depth_b ? depth_b[i] : 0;
+        if (std::max(da, db) + 1 > 1)
+            return fail(EXACTO_ERR_NOT_IMPLEMENTED, "not yet implemented: chained dBFV multiplication requires "
+                                                    "ciphertext-level lattice reduction (paper §4.6.2)");
+    }
+    if (B == 0) return 0;
+    if (int e = dbfv_plan(c, B, d, base, plain)) return e;
+    const int npairs = c->cached_npairs;
+    const long Ln2 = 2L * c->L * c->n;
+    const long P = (long)B * npairs;
+    size_t cap = c->prod_bytes;
+    if (grow(&c->prod, &cap, (size_t)P * Ln2 * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->prod_bytes = cap;
+    Operands op{};
+    op.a = a; op.a_off = c->d_off; op.a_stride = 0;
+    op.b = b; op.b_off = c->d_off + (size_t)B * npairs; op.b_stride = 0;
+    if (int e = run_mul(c, op, P, c->prod, Ln2, true)) return e;
+    launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
+                        c->stream);
+    CHECK_LAUNCH();
+    if (depth_out)
+        for (size_t i = 0; i < B; ++i) depth_out[i] = 1;
+    return 0;
+}
+
+extern "C" int exacto_dbfv_mul(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                               const uint64_t* b, uint64_t* out, size_t B, const uint32_t* depth_a,
+                               const uint32_t* depth_b, uint32_t* depth_out) {
+    if (!c) return invalid_param("null context");
+    const size_t bytes = B * d * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{a, bytes}, {b, bytes}}, bytes, out, [&](std::vector<u64*>& dv, u64* o) {
+        return exacto_dbfv_mul_dev(c, d, base, plain, dv[0], dv[1], o, B, depth_a, depth_b, depth_out);
+    });
+}
+
+// ============================================================== diagnostics
+
+extern "C" size_t exacto_last_error(char* buf, size_t len) {
+    if (buf && len) {
+        const size_t m = std::min(len - 1, g_last_error.size());
+        std::memcpy(buf, g_last_error.data(), m);
+        buf[m] = 0;
+    }
+    return g_last_error.size();
+}
+
+extern "C" int exacto_prof_enable(exacto_ctx* c, int enable) {
+    if (!c) return invalid_param("null context");
+    c->prof = enable != 0;
+    return 0;
+}
+
+extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, double* total_ms, double* total_bytes,
+                                uint64_t* polys) {
+    if (!c) return invalid_param("null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    u64 nl = 0, np = 0;
+    double ms = 0, by = 0;
+    std::vector<ProfRec> keep;
+    for (auto& r : c->recs) {
+        if (r.kind != kind) { keep.push_back(r); continue; }
+        float t = 0;
+        HIP_TRY(hipEventElapsedTime(&t, r.a, r.b));
+        ms += t; by += r.bytes; np += r.polys; ++nl;
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    c->recs.swap(keep);
+    if (launches) *launches = nl;
+    if (total_ms) *total_ms = ms;
+    if (total_bytes) *total_bytes = by;
+    if (polys) *polys = np;
+    return 0;
+}
+
+extern "C" const char* exacto_version(void) { return "exacto-hip 0.1.0 (gfx950)"; }

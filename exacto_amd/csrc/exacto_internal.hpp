@@ -1,0 +1,101 @@
+// Internal (non-ABI) declarations shared by the HIP kernels and the host runtime.
+#pragma once
+#include "arith.hpp"
+
+namespace exacto {
+
+// A batch of independent residue polynomials for the NTT kernels.
+// Polynomial p (0 <= p < count) belongs to item p / ppi, sub-polynomial p % ppi.
+// Source: src + (src_off ? src_off[item] : item * src_item_stride) + sub * n.
+// Destination: dst + item * dst_item_stride + sub * n (may alias the source).
+// Prime: prime_base + sub % period.
+struct NttBatch {
+    const u64* src;
+    const u64* src_off;
+    long src_item_stride;
+    u64* dst;
+    long dst_item_stride;
+    int ppi;
+    int prime_base;
+    int period;
+};
+
+enum class MulPath : int { Exact = 0, Hps = 1 };
+
+// Constants for exact CRT / base conversion, HPS and gadget decomposition.
+// Mixed-radix (Garner) digits are used everywhere so that centring decisions are exact.
+struct CrtTables {
+    int L;          // ciphertext primes (prime indices 0..L-1)
+    int K;          // auxiliary primes used by the path (prime indices L..L+K-1)
+    int G;          // gadget digits  (params/mod.rs:126-140)
+    int gshift;     // log2(gadget base) if a power of two, else -1
+    u64 gbase;
+    u64 plain;      // BFV plaintext modulus p
+    // Garner over Q: gq[i][k] = q_k^-1 mod q_i (k < i)
+    u64 gq_w[EXACTO_MAX_L][EXACTO_MAX_L];
+    u64 gq_ws[EXACTO_MAX_L][EXACTO_MAX_L];
+    u64 halfQ_mr[EXACTO_MAX_L];                 // mixed-radix digits of floor(Q/2)
+    // qpref[k][t] = (q_0 ... q_{k-1}) mod prime_t, k = 0..L (k = L: Q mod prime_t)
+    u64 qpref_w[EXACTO_MAX_L + 1][EXACTO_MAX_PRIMES];
+    u64 qpref_ws[EXACTO_MAX_L + 1][EXACTO_MAX_PRIMES];
+    // Garner over P (auxiliary primes, exact path)
+    u64 gp_w[EXACTO_MAX_K][EXACTO_MAX_K];
+    u64 gp_ws[EXACTO_MAX_K][EXACTO_MAX_K];
+    u64 halfP_mr[EXACTO_MAX_K];
+    // ppref[k][i] = (p_0 ... p_{k-1}) mod q_i, k = 0..K
+    u64 ppref_w[EXACTO_MAX_K + 1][EXACTO_MAX_L];
+    u64 ppref_ws[EXACTO_MAX_K + 1][EXACTO_MAX_L];
+    u64 qinvp_w[EXACTO_MAX_K], qinvp_ws[EXACTO_MAX_K];   // Q^-1 mod p_j
+    u64 pmod_w[EXACTO_MAX_PRIMES], pmod_ws[EXACTO_MAX_PRIMES];  // plain mod prime_t
+    u64 Qwords[EXACTO_MAX_L];                   // Q as little-endian 64-bit words
+    // HPS (single q, 1 or 2 aux primes), eval.rs:257-413
+    u64 hps_qinv[2];        // q^-1 mod p_j
+    u64 hps_p1_inv_p0, hps_p0_inv_p1;
+};
+
+void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, const PrimeConst* primes,
+                hipStream_t s);
+
+// ---- kernels.hip launchers (all asynchronous on `s`) ----
+struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item
+    const u64* a;
+    const u64* a_off;        // per-item element offsets (device) or nullptr -> item * a_stride
+    long a_stride;
+    const u64* b;
+    const u64* b_off;
+    long b_stride;
+};
+
+void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
+                       const PrimeConst* primes, int L, int K, hipStream_t s);
+void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
+                       int K, hipStream_t s);
+void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
+                   const PrimeConst* primes, hipStream_t s);
+void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+                        int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
+                        int K, hipStream_t s);
+void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
+                      hipStream_t s);
+void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
+                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s);
+void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long base_poly0,
+                      const u64* D, const u64* rlk, int guse, u64* out, long out_stride, int items,
+                      int n, int L, const PrimeConst* primes, hipStream_t s);
+
+enum class PwOp : int { Add = 0, Sub = 1, Neg = 2, Mul = 3, ScalarMul = 4, Copy = 5 };
+void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys, int n, int L,
+                      const u64* scalar_mod /*[L] or null*/, const PrimeConst* primes,
+                      hipStream_t s);
+
+struct CombineTerm {
+    int pair;      // product index inside the item
+    int pad_;
+    i64 coef;      // signed small integer
+};
+void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
+                         const CombineTerm* terms, u64* out, int items, int d, int n, int L,
+                         const PrimeConst* primes, hipStream_t s);
+
+}  // namespace exacto

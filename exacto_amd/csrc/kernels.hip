@@ -1,0 +1,556 @@
+// Coefficient-wise kernels of the BFV multiplication path (gfx950).
+//
+//   exact_lift   : centred exact Q -> P base extension        (eval.rs:719-762 reconstruct_centered_bigint)
+//   hps_extend   : literal single-q centred extension         (eval.rs:217-247 base_extend_centered)
+//   tensor       : (c0d0, c0d1 + c1d0, c1d1) in every prime   (eval.rs:131-133, 186-198)
+//   exact_scale  : r = round(p*T/Q) exactly, r mod q_i        (eval.rs:816-831, 764-792)
+//   hps_scale    : literal HPS m-recovery, 1 or 2 aux primes  (eval.rs:257-413)
+//   gadget digits: balanced base-B digits of [c2]_Q           (keyswitch.rs:11-52, rns.rs:114-151)
+//   relin_mac    : c_k + sum_g d_g (.) rlk_k,g                (keyswitch.rs:86-95)
+//   dbfv_combine : per-k limb sums + degree reduction         (dbfv/eval.rs:124-132, reduction.rs:34-52)
+//
+// Every kernel is a flat 1-D grid of 256-thread blocks, one coefficient per
+// thread; the "row" (item x polynomial) is blockIdx.x / blocks_per_row so
+// consecutive lanes touch consecutive 8-byte words of one residue polynomial.
+#include "exacto_internal.hpp"
+
+namespace exacto {
+
+static constexpr int TPB = 256;
+
+static inline int blocks_per_row(int n) { return (n + TPB - 1) / TPB; }
+
+#define ROW_SETUP(n)                                        \
+    const int nblk = (n + TPB - 1) / TPB;                   \
+    const long row = blockIdx.x / nblk;                     \
+    const int j = (blockIdx.x - row * nblk) * TPB + threadIdx.x; \
+    if (j >= (n)) return;
+
+// ---------------------------------------------------------------- mixed radix helpers
+
+// Garner: residues x[i] mod q_i (i < L) -> mixed-radix digits v (x = v0 + v1 q0 + v2 q0 q1 + ...).
+__device__ __forceinline__ void garner_q(u64 (&v)[EXACTO_MAX_L], const u64 (&x)[EXACTO_MAX_L], int L,
+                                         const CrtTables* __restrict__ C,
+                                         const PrimeConst* __restrict__ primes) {
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i) {
+        if (i < L) {
+            const u64 qi = primes[i].q, mui = primes[i].mu64;
+            u64 t = x[i];
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_L; ++k) {
+                if (k < i) {
+                    t = sub_mod(t, reduce64(v[k], qi, mui), qi);
+                    t = shoup_mul_red(t, C->gq_w[i][k], C->gq_ws[i][k], qi);
+                }
+            }
+            v[i] = t;
+        }
+    }
+}
+
+template <int MAXN>
+__device__ __forceinline__ bool mr_greater(const u64 (&v)[MAXN], const u64* h, int cnt) {
+    // lexicographic compare, most significant digit first
+    int res = 0;  // 0 undecided, 1 greater, -1 smaller
+#pragma unroll
+    for (int k = MAXN - 1; k >= 0; --k) {
+        if (k < cnt && res == 0) {
+            if (v[k] > h[k]) res = 1;
+            else if (v[k] < h[k]) res = -1;
+        }
+    }
+    return res == 1;
+}
+
+// sum_k (v_k mod prime_t) * pref[k][t]  -  neg * pref[cnt][t]   (mod prime_t)
+template <int MAXN, int STRIDE>
+__device__ __forceinline__ u64 mr_eval(const u64 (&v)[MAXN], int cnt, bool neg, const u64* pw,
+                                       const u64* pws, int t, const PrimeConst& P) {
+    const u64 q = P.q, mu = P.mu64;
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) {
+        if (k < cnt) {
+            const u64 vk = reduce64(v[k], q, mu);
+            acc = add_mod(acc, shoup_mul_red(vk, pw[k * STRIDE + t], pws[k * STRIDE + t], q), q);
+        }
+    }
+    if (neg) acc = sub_mod(acc, pw[cnt * STRIDE + t], q);
+    return acc;
+}
+
+// Balanced gadget digits of the centred CRT value of residues res[0..L) (mod Q).
+// keyswitch.rs:24-44 literally (truncating %, [-B/2, B/2) adjustment, final carry dropped),
+// on the exact value (extension semantics for Q >= 2^64; identical to rns.rs:114-151 below).
+// Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j).
+__device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTables* __restrict__ C,
+                              const PrimeConst* __restrict__ primes, u64* D, int n, int guse) {
+    u64 z[EXACTO_MAX_L];
+    garner_q(z, res, L, C, primes);
+    const bool neg = mr_greater<EXACTO_MAX_L>(z, C->halfQ_mr, L);
+    // multiword value via Horner on the mixed-radix digits
+    u64 M[EXACTO_MAX_L];
+#pragma unroll
+    for (int w = 0; w < EXACTO_MAX_L; ++w) M[w] = 0;
+#pragma unroll
+    for (int k = 0; k < EXACTO_MAX_L; ++k)
+        if (k == L - 1) M[0] = z[k];
+#pragma unroll
+    for (int k = EXACTO_MAX_L - 2; k >= 0; --k) {
+        if (k <= L - 2) {
+            const u64 qk = primes[k].q;
+            u64 carry = z[k];
+#pragma unroll
+            for (int w = 0; w < EXACTO_MAX_L; ++w) {
+                if (w < L) {
+                    const u128 t = (u128)M[w] * qk + carry;
+                    M[w] = (u64)t;
+                    carry = (u64)(t >> 64);
+                }
+            }
+        }
+    }
+    if (neg) {  // magnitude Q - x
+        u64 borrow = 0;
+#pragma unroll
+        for (int w = 0; w < EXACTO_MAX_L; ++w) {
+            if (w < L) {
+                const u64 a = C->Qwords[w], b = M[w];
+                const u64 d1 = a - b;
+                const u64 b1 = a < b;
+                const u64 d2 = d1 - borrow;
+                const u64 b2 = d1 < borrow;
+                M[w] = d2;
+                borrow = b1 | b2;
+            }
+        }
+    }
+    const u64 B = C->gbase;
+    const u64 half = B >> 1;
+    const int sh = C->gshift;
+    for (int g = 0; g < guse; ++g) {
+        u64 r;
+        if (sh >= 0) {
+            r = M[0] & (B - 1);
+#pragma unroll
+            for (int w = 0; w < EXACTO_MAX_L; ++w) {
+                if (w < L) {
+                    const u64 hi = (w + 1 < L) ? M[w + 1] : 0;
+                    M[w] = (M[w] >> sh) | (sh ? (hi << (64 - sh)) : 0);
+                }
+            }
+        } else {
+            u64 rem = 0;
+#pragma unroll
+            for (int w = EXACTO_MAX_L - 1; w >= 0; --w) {
+                if (w < L) {
+                    const u128 cur = ((u128)rem << 64) | M[w];
+                    M[w] = (u64)(cur / B);
+                    rem = (u64)(cur % B);
+                }
+            }
+            r = rem;
+        }
+        // signed remainder: value = +/- M_old; Rust truncating % then balance
+        u64 mag;
+        bool dneg;
+        bool carry;
+        if (!neg) {
+            if (r >= half) { mag = B - r; dneg = true; carry = true; }
+            else { mag = r; dneg = false; carry = false; }
+        } else {
+            if (r > half) { mag = B - r; dneg = false; carry = true; }
+            else { mag = r; dneg = (r != 0); carry = false; }
+        }
+        if (carry) {
+            u64 c = 1;
+#pragma unroll
+            for (int w = 0; w < EXACTO_MAX_L; ++w) {
+                if (w < L) {
+                    const u64 s = M[w] + c;
+                    c = (s < c);
+                    M[w] = s;
+                }
+            }
+        }
+        // digit residue (rem mod Q) mod q_i == rem mod q_i
+#pragma unroll
+        for (int i = 0; i < EXACTO_MAX_L; ++i) {
+            if (i < L) {
+                const u64 qi = primes[i].q;
+                u64 m = reduce64(mag, qi, primes[i].mu64);
+                if (dneg && m != 0) m = qi - m;
+                D[((long)g * L + i) * n] = m;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- exact lift Q -> P
+
+__global__ void __launch_bounds__(TPB)
+exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L, int K,
+                  const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    u64 x[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i)
+        if (i < L) x[i] = coefQ[(row * L + i) * n + j];
+    garner_q(v, x, L, C, primes);
+    const bool neg = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+    for (int a = 0; a < K; ++a) {
+        const int t = L + a;
+        extP[(row * K + a) * n + j] =
+            mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, neg, &C->qpref_w[0][0], &C->qpref_ws[0][0],
+                                                     t, primes[t]);
+    }
+}
+
+void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
+                       const PrimeConst* primes, int L, int K, hipStream_t s) {
+    const long blocks = (long)items * 4 * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(exact_lift_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct,
+                       primes);
+}
+
+// ---------------------------------------------------------------- HPS extension
+
+__global__ void __launch_bounds__(TPB)
+hps_extend_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int K,
+                  const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const u64 q = primes[0].q;
+    const u64 c = coefQ[row * n + j];
+    for (int a = 0; a < K; ++a) {
+        const PrimeConst& P = primes[1 + a];
+        u64 r;
+        if (c > q / 2) {
+            const u64 rem = reduce64(q - c, P.q, P.mu64);
+            r = rem == 0 ? 0 : P.q - rem;
+        } else {
+            r = reduce64(c, P.q, P.mu64);
+        }
+        extP[(row * K + a) * n + j] = r;
+    }
+}
+
+void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
+                       int K, hipStream_t s) {
+    const long blocks = (long)items * 4 * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(hps_extend_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, K, primes);
+}
+
+// ---------------------------------------------------------------- tensor product
+
+__global__ void __launch_bounds__(TPB)
+tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ T, int n, int L, int K,
+              const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const int NP = L + K;
+    const long item = row / NP;
+    const int t = (int)(row - item * NP);
+    const PrimeConst& P = primes[t];
+    u64 a0, a1, b0, b1;
+    if (t < L) {
+        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
+        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
+        a0 = A[(long)t * n + j];
+        a1 = A[(long)(L + t) * n + j];
+        b0 = B[(long)t * n + j];
+        b1 = B[(long)(L + t) * n + j];
+    } else {
+        const u64* E = extP + item * 4 * K * n + (long)(t - L) * n + j;
+        a0 = E[0];
+        a1 = E[(long)K * n];
+        b0 = E[2L * K * n];
+        b1 = E[3L * K * n];
+    }
+    u64* out = T + (item * 3 * NP + t) * n + j;
+    out[0] = mul_mod(a0, b0, P);
+    out[(long)NP * n] = add_mod(mul_mod(a0, b1, P), mul_mod(a1, b0, P), P.q);
+    out[2L * NP * n] = mul_mod(a1, b1, P);
+}
+
+void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
+                   const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items * (L + K) * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(tensor_kernel, dim3(blocks), dim3(TPB), 0, s, op, extP, T, n, L, K, primes);
+}
+
+// ---------------------------------------------------------------- exact scale-and-round
+
+__global__ void __launch_bounds__(TPB)
+exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
+                   u64* __restrict__ D, int guse, int n, int L, int K,
+                   const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const int NP = L + K;
+    const long item = row / 3;
+    const int comp = (int)(row - item * 3);
+    const u64* Tin = T + row * NP * n + j;
+    // u = p * T in every prime
+    u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i)
+        if (i < L) u[i] = shoup_mul_red(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
+    // s = [u]_Q centred, via mixed radix
+    garner_q(v, u, L, C, primes);
+    const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+    // r = (u - s) / Q in every auxiliary prime
+    u64 r[EXACTO_MAX_K], w[EXACTO_MAX_K];
+#pragma unroll
+    for (int a = 0; a < EXACTO_MAX_K; ++a) {
+        if (a < K) {
+            const int t = L + a;
+            const PrimeConst& P = primes[t];
+            const u64 ut = shoup_mul_red(Tin[(long)t * n], C->pmod_w[t], C->pmod_ws[t], P.q);
+            const u64 st = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, negs, &C->qpref_w[0][0],
+                                                                    &C->qpref_ws[0][0], t, P);
+            r[a] = shoup_mul_red(sub_mod(ut, st, P.q), C->qinvp_w[a], C->qinvp_ws[a], P.q);
+        }
+    }
+    // Garner over P, centre, evaluate mod each q_i
+#pragma unroll
+    for (int a = 0; a < EXACTO_MAX_K; ++a) {
+        if (a < K) {
+            const PrimeConst& P = primes[L + a];
+            u64 t = r[a];
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_K; ++k) {
+                if (k < a) {
+                    t = sub_mod(t, reduce64(w[k], P.q, P.mu64), P.q);
+                    t = shoup_mul_red(t, C->gp_w[a][k], C->gp_ws[a][k], P.q);
+                }
+            }
+            w[a] = t;
+        }
+    }
+    const bool negr = mr_greater<EXACTO_MAX_K>(w, C->halfP_mr, K);
+    u64 res[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i)
+        if (i < L)
+            res[i] = mr_eval<EXACTO_MAX_K, EXACTO_MAX_L>(w, K, negr, &C->ppref_w[0][0],
+                                                         &C->ppref_ws[0][0], i, primes[i]);
+    if (comp < ncomp_r) {
+        u64* out = R + item * r_stride + (long)comp * L * n + j;
+#pragma unroll
+        for (int i = 0; i < EXACTO_MAX_L; ++i)
+            if (i < L) out[(long)i * n] = res[i];
+    }
+    if (comp == 2 && D != nullptr)
+        gadget_digits(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
+}
+
+void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+                        int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
+                        int K, hipStream_t s) {
+    const long blocks = (long)items * 3 * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(exact_scale_kernel, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
+                       guse, n, L, K, ct, primes);
+}
+
+// ---------------------------------------------------------------- literal HPS scale
+
+__device__ __forceinline__ u64 hps_ext(u64 a, u64 q, u64 pj) {
+    // eval.rs:307-313
+    if (a > q / 2) {
+        const u64 rem = (q - a) % pj;
+        return rem == 0 ? 0 : pj - rem;
+    }
+    return a % pj;
+}
+
+__global__ void __launch_bounds__(TPB)
+hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
+                 u64* __restrict__ D, int guse, int n, int K, const CrtTables* __restrict__ C,
+                 const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const long item = row / 3;
+    const int comp = (int)(row - item * 3);
+    const u64* Tin = T + row * (1 + K) * n + j;
+    const u64 q = primes[0].q;
+    const u64 p = C->plain;
+    const i128 q128 = (i128)q;
+    const u64 a = Tin[0];
+    const u64 half_q = q / 2;
+    const i128 a_centered = a > half_q ? (i128)a - q128 : (i128)a;
+    const i128 pa = (i128)p * a_centered;
+    const i128 round_pa_q = pa >= 0 ? (pa + q128 / 2) / q128 : -((-pa + q128 / 2) / q128);
+    u64 result;
+    if (K == 1) {
+        // eval.rs:301-332
+        const u64 big_p = primes[1].q;
+        const u64 b = Tin[n];
+        const u64 a_ext = hps_ext(a, q, big_p);
+        const u64 diff = b >= a_ext ? b - a_ext : big_p - a_ext + b;
+        const u64 m_raw = ref_mod_mul(diff, C->hps_qinv[0], big_p);
+        const i128 m_centered = m_raw > big_p / 2 ? (i128)m_raw - (i128)big_p : (i128)m_raw;
+        const i128 scaled = round_pa_q + (i128)p * m_centered;
+        result = (u64)(((scaled % q128) + q128) % q128);
+    } else {
+        // eval.rs:349-404
+        const u64 p0 = primes[1].q, p1 = primes[2].q;
+        const u64 b0 = Tin[n], b1 = Tin[2L * n];
+        const u64 a_ext0 = hps_ext(a, q, p0);
+        const u64 diff0 = b0 >= a_ext0 ? b0 - a_ext0 : p0 - a_ext0 + b0;
+        const u64 m0 = ref_mod_mul(diff0, C->hps_qinv[0], p0);
+        const u64 a_ext1 = hps_ext(a, q, p1);
+        const u64 diff1 = b1 >= a_ext1 ? b1 - a_ext1 : p1 - a_ext1 + b1;
+        const u64 m1 = ref_mod_mul(diff1, C->hps_qinv[1], p1);
+        const i128 t0 = (i128)ref_mod_mul(m0, C->hps_p1_inv_p0, p0);
+        const i128 t1 = (i128)ref_mod_mul(m1, C->hps_p0_inv_p1, p1);
+        const i128 big_p = (i128)p0 * (i128)p1;
+        const i128 half_big_p = big_p / 2;
+        const i128 crt_sum = t0 * (i128)p1 + t1 * (i128)p0;
+        const i128 m_crt = crt_sum % big_p;
+        const i128 m_centered = m_crt > half_big_p ? m_crt - big_p : m_crt;
+        const i128 m_mod_q = ((m_centered % q128) + q128) % q128;
+        const u64 round_mod_q = (u64)(((round_pa_q % q128) + q128) % q128);
+        const u64 pm_mod_q = ref_mod_mul(p, (u64)m_mod_q, q);
+        result = (u64)(((u128)round_mod_q + pm_mod_q) % q);
+    }
+    if (comp < ncomp_r) R[item * r_stride + (long)comp * n + j] = result;
+    if (comp == 2 && D != nullptr) {
+        u64 res[EXACTO_MAX_L];
+        res[0] = result;
+        gadget_digits(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
+    }
+}
+
+void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
+                      hipStream_t s) {
+    const long blocks = (long)items * 3 * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(hps_scale_kernel, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
+                       guse, n, K, ct, primes);
+}
+
+// ---------------------------------------------------------------- standalone decomposition
+
+__global__ void __launch_bounds__(TPB)
+decompose_kernel(const u64* __restrict__ C2, long c2_stride, u64* __restrict__ D, int guse, int n,
+                 int L, const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    u64 res[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i)
+        if (i < L) res[i] = C2[row * c2_stride + (long)i * n + j];
+    gadget_digits(res, L, C, primes, D + row * (long)guse * L * n + j, n, guse);
+}
+
+void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
+                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s) {
+    const long blocks = (long)items * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(decompose_kernel, dim3(blocks), dim3(TPB), 0, s, C2, c2_stride, D, guse, n, L,
+                       ct, primes);
+}
+
+// ---------------------------------------------------------------- relinearisation MAC
+
+__global__ void __launch_bounds__(TPB)
+relin_mac_kernel(const u64* __restrict__ base, const u64* __restrict__ base_off, long base_stride,
+                 const u64* __restrict__ D, const u64* __restrict__ rlk, int guse,
+                 u64* __restrict__ out, long out_stride, int n, int L,
+                 const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const long item = row / L;
+    const int i = (int)(row - item * L);
+    const PrimeConst& P = primes[i];
+    const u64* bp = base + (base_off ? (long)base_off[item] : item * base_stride);
+    u64 acc0 = bp[(long)i * n + j];
+    u64 acc1 = bp[(long)(L + i) * n + j];
+    const u64* dp = D + item * (long)guse * L * n + (long)i * n + j;
+    const u64* kp = rlk + (long)i * n + j;
+    const long Ln = (long)L * n;
+    for (int g = 0; g < guse; ++g) {
+        const u64 d = dp[g * Ln];
+        acc0 = add_mod(acc0, mul_mod(d, kp[(2L * g) * Ln], P), P.q);
+        acc1 = add_mod(acc1, mul_mod(d, kp[(2L * g + 1) * Ln], P), P.q);
+    }
+    u64* op = out + item * out_stride + (long)i * n + j;
+    op[0] = acc0;
+    op[Ln] = acc1;
+}
+
+void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long /*base_poly0*/,
+                      const u64* D, const u64* rlk, int guse, u64* out, long out_stride, int items,
+                      int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items * L * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(relin_mac_kernel, dim3(blocks), dim3(TPB), 0, s, base, base_off, base_stride, D,
+                       rlk, guse, out, out_stride, n, L, primes);
+}
+
+// ---------------------------------------------------------------- pointwise RNS ops
+
+__global__ void __launch_bounds__(TPB)
+pointwise_kernel(int op, const u64* __restrict__ a, const u64* __restrict__ b, u64* __restrict__ out,
+                 int n, int L, const u64* __restrict__ scal, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const int limb = (int)(row % L);
+    const PrimeConst& P = primes[limb];
+    const long idx = row * n + j;
+    const u64 x = a[idx];
+    u64 r;
+    switch (op) {
+        case 0: r = add_mod(x, b[idx], P.q); break;
+        case 1: r = sub_mod(x, b[idx], P.q); break;
+        case 2: r = neg_mod(x, P.q); break;
+        case 3: r = mul_mod(x, b[idx], P); break;
+        case 4: r = mul_mod(x, scal[limb], P); break;
+        default: r = x; break;
+    }
+    out[idx] = r;
+}
+
+void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys, int n, int L,
+                      const u64* scalar_mod, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = polys * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(pointwise_kernel, dim3(blocks), dim3(TPB), 0, s, (int)op, a, b, out, n, L,
+                       scalar_mod, primes);
+}
+
+// ---------------------------------------------------------------- dBFV combine
+
+__global__ void __launch_bounds__(TPB)
+dbfv_combine_kernel(const u64* __restrict__ prod, int npairs, const int* __restrict__ term_start,
+                    const CombineTerm* __restrict__ terms, u64* __restrict__ out, int d, int n, int L,
+                    const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    // row = ((item * d + k) * 2 + poly) * L + limb
+    const int limb = (int)(row % L);
+    const long r1 = row / L;
+    const int poly = (int)(r1 % 2);
+    const long r2 = r1 / 2;
+    const int k = (int)(r2 % d);
+    const long item = r2 / d;
+    const PrimeConst& P = primes[limb];
+    u64 acc = 0;
+    for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+        const CombineTerm tm = terms[t];
+        const u64 x = prod[(((item * npairs + tm.pair) * 2 + poly) * L + limb) * n + j];
+        if (tm.coef == 1) acc = add_mod(acc, x, P.q);
+        else acc = add_mod(acc, mul_mod(x, signed_mod(tm.coef, P.q, P.mu64), P), P.q);
+    }
+    out[row * n + j] = acc;
+}
+
+void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
+                         const CombineTerm* terms, u64* out, int items, int d, int n, int L,
+                         const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items * d * 2 * L * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(dbfv_combine_kernel, dim3(blocks), dim3(TPB), 0, s, prod, npairs, term_start,
+                       terms, out, d, n, L, primes);
+}
+
+}  // namespace exacto

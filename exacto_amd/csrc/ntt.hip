@@ -1,0 +1,238 @@
+// Batched negacyclic NTT / INTT for gfx950 — replaces concrete-ntt's
+// prime64::Plan::{fwd, inv, normalize} (reference call sites src/ring/ntt.rs:24,43,49,60,62).
+//
+// One residue polynomial per workgroup, n/16 threads, 16 coefficients per
+// thread held in VGPRs.  The log2(n) radix-2 stages are grouped into rounds of
+// four: inside a round every butterfly is thread-local (no LDS, no barrier);
+// between rounds the 16 values are exchanged through one n*8-byte LDS image
+// under an XOR swizzle that keeps every ds_write_b64 / ds_read_b64 of the
+// three access patterns conflict-free.  Harvey lazy butterflies (values in
+// [0, 4q) forward, [0, 2q) inverse) with Shoup twiddles; n^-1 is folded into
+// the last inverse stage.  Convention (documented in DESIGN.md, restated by
+// oracle/ring.py NttPlan): Cooley-Tukey forward, natural in / bit-reversed out;
+// Gentleman-Sande inverse, bit-reversed in / natural out.
+#include "exacto_internal.hpp"
+
+namespace exacto {
+
+__device__ __forceinline__ int swz(int j) {
+    return j ^ ((j >> 4) & 15) ^ (((j >> 8) & 1) << 4);
+}
+
+template <int LO>
+__device__ __forceinline__ int elem_index(int tid, int k) {
+    return ((tid >> LO) << (LO + 4)) | (k << LO) | (tid & ((1 << LO) - 1));
+}
+
+template <int LO>
+__device__ __forceinline__ void lds_store(u64* lds, const u64 (&x)[16], int tid) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[swz(elem_index<LO>(tid, k))] = x[k];
+}
+
+template <int LO>
+__device__ __forceinline__ void lds_load(const u64* lds, u64 (&x)[16], int tid) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = lds[swz(elem_index<LO>(tid, k))];
+}
+
+// ---------------------------------------------------------------- forward
+
+// Butterflies for stage bits BHI..BLO (descending) inside window [LO, LO+4).
+template <int LOGN, int LO, int BHI, int BLO>
+__device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* __restrict__ tw,
+                                          u64 q, u64 q2) {
+    constexpr int N = 1 << LOGN;
+    const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+#pragma unroll
+    for (int b = BHI; b >= BLO; --b) {
+        const int lb = b - LO;
+        const int half = 1 << lb;
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> lb); ++g) {
+            const TwPair t = tw[base + g];
+#pragma unroll
+            for (int m = 0; m < half; ++m) {
+                const int k0 = g * 2 * half + m;
+                const int k1 = k0 + half;
+                u64 X = x[k0];
+                X = X >= q2 ? X - q2 : X;
+                const u64 T = shoup_mul(x[k1], t.w, t.ws, q);
+                x[k0] = X + T;
+                x[k1] = X - T + q2;
+            }
+        }
+    }
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw, u64 q,
+                                           u64 q2) {
+    constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
+    constexpr int BHI = LOGN - 1 - 4 * R;
+    if constexpr (R > 0) {
+        constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
+        __syncthreads();
+        lds_store<PLO>(lds, x, tid);
+        __syncthreads();
+        lds_load<LO>(lds, x, tid);
+    }
+    fwd_round<LOGN, LO, BHI, LO>(x, tid, tw, q, q2);
+    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1>(x, lds, tid, tw, q, q2);
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    if (tid >= T) return;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64 q = P.q, q2 = P.two_q;
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+
+    u64 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+
+    fwd_rounds<LOGN, 0>(x, lds, tid, P.tw_fwd, q, q2);
+
+    // final layout: element 16*tid + k; reduce [0,4q) -> [0,q)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        u64 v = x[k];
+        v = v >= q2 ? v - q2 : v;
+        x[k] = v >= q ? v - q : v;
+    }
+    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst + 16 * tid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d2[k] = make_ulonglong2(x[2 * k], x[2 * k + 1]);
+}
+
+// ---------------------------------------------------------------- inverse
+
+template <int LOGN, int LO, int BLO, int BHI>
+__device__ __forceinline__ void inv_round(u64 (&x)[16], int tid, const TwPair* __restrict__ tw,
+                                          const PrimeConst& P) {
+    constexpr int N = 1 << LOGN;
+    const u64 q = P.q, q2 = P.two_q;
+    const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+#pragma unroll
+    for (int b = BLO; b <= BHI; ++b) {
+        const int lb = b - LO;
+        const int half = 1 << lb;
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+        if (b == LOGN - 1) {
+            // last stage: (U+V) * n^-1, (U-V) * psi_inv_rev[1] * n^-1, fully reduced
+#pragma unroll
+            for (int m = 0; m < half; ++m) {
+                const int k0 = m, k1 = m + half;
+                const u64 U = x[k0], V = x[k1];
+                x[k0] = shoup_mul_red(U + V, P.n_inv, P.n_inv_s, q);
+                x[k1] = shoup_mul_red(U - V + q2, P.last_w, P.last_ws, q);
+            }
+        } else {
+#pragma unroll
+            for (int g = 0; g < (8 >> lb); ++g) {
+                const TwPair t = tw[base + g];
+#pragma unroll
+                for (int m = 0; m < half; ++m) {
+                    const int k0 = g * 2 * half + m;
+                    const int k1 = k0 + half;
+                    const u64 U = x[k0], V = x[k1];
+                    u64 s = U + V;
+                    x[k0] = s >= q2 ? s - q2 : s;
+                    x[k1] = shoup_mul(U - V + q2, t.w, t.ws, q);
+                }
+            }
+        }
+    }
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw,
+                                           const PrimeConst& P) {
+    constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
+    constexpr int BLO = 4 * R;
+    constexpr int BHI = (4 * R + 3) < (LOGN - 1) ? 4 * R + 3 : LOGN - 1;
+    if constexpr (R > 0) {
+        constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
+        __syncthreads();
+        lds_store<PLO>(lds, x, tid);
+        __syncthreads();
+        lds_load<LO>(lds, x, tid);
+    }
+    inv_round<LOGN, LO, BLO, BHI>(x, tid, tw, P);
+    if constexpr (BHI < LOGN - 1) inv_rounds<LOGN, R + 1>(x, lds, tid, tw, P);
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    if (tid >= T) return;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+
+    u64 x[16];
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const ulonglong2 v = s2[k];
+        x[2 * k] = v.x;
+        x[2 * k + 1] = v.y;
+    }
+
+    inv_rounds<LOGN, 0>(x, lds, tid, P.tw_inv, P);
+
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
+// ---------------------------------------------------------------- launchers
+
+template <int LOGN>
+static void launch_one(const NttBatch& nb, int count, bool inverse, const PrimeConst* primes,
+                       hipStream_t s) {
+    constexpr int threads = (1 << LOGN) / 16;
+    if (inverse)
+        hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, dim3(count), dim3(threads), 0, s, nb, primes);
+    else
+        hipLaunchKernelGGL(ntt_fwd_kernel<LOGN>, dim3(count), dim3(threads), 0, s, nb, primes);
+}
+
+void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, const PrimeConst* primes,
+                hipStream_t s) {
+    if (count <= 0) return;
+    switch (logn) {
+        case 4: launch_one<4>(nb, count, inverse, primes, s); break;
+        case 5: launch_one<5>(nb, count, inverse, primes, s); break;
+        case 6: launch_one<6>(nb, count, inverse, primes, s); break;
+        case 7: launch_one<7>(nb, count, inverse, primes, s); break;
+        case 8: launch_one<8>(nb, count, inverse, primes, s); break;
+        case 9: launch_one<9>(nb, count, inverse, primes, s); break;
+        case 10: launch_one<10>(nb, count, inverse, primes, s); break;
+        case 11: launch_one<11>(nb, count, inverse, primes, s); break;
+        case 12: launch_one<12>(nb, count, inverse, primes, s); break;
+        case 13: launch_one<13>(nb, count, inverse, primes, s); break;
+        case 14: launch_one<14>(nb, count, inverse, primes, s); break;
+        default: break;  // rejected at context creation
+    }
+}
+
+}  // namespace exacto

@@ -1,0 +1,185 @@
+/* exacto_hip.h — C ABI of the MI355X (gfx950) ciphertext-multiplication path.
+ *
+ * Drop-in boundary for the hot path of RajeshRk18/exacto (Rust).  Each entry point
+ * names the reference interface it replaces (paths relative to the reference repo).
+ * A Rust caller binds these with an `extern "C"` block.
+ *
+ * Conventions
+ *   - Return value: 0 = Ok; 1..9 = ExactoError variants in declaration order
+ *     (src/error.rs:4-31): 1 InvalidParam, 2 DimensionMismatch, 3 ModulusMismatch,
+ *     4 InvalidRingDegree, 5 DecryptionError, 6 DecompositionError, 7 LatticeError,
+ *     8 MissingKey, 9 NotImplemented; 100 = HIP runtime failure.  The Display text
+ *     of the error (same wording as the reference's #[error(...)] strings) is
+ *     available from exacto_last_error() on the calling thread.
+ *   - Layout: little-endian uint64, ciphertext batches are [batch][poly][limb][coeff]
+ *     (BfvCiphertext.c: Vec<RnsPoly>, src/bfv/mod.rs:19-24; RnsPoly.components:
+ *     Vec<NttPoly>, src/ring/rns.rs:14-17).  dBFV batches are
+ *     [batch][digit][poly][limb][coeff] (DbfvCiphertext.limbs, src/dbfv/ciphertext.rs:10-22).
+ *     Relinearisation keys are [key][2][limb][coeff] (RelinKey.keys,
+ *     src/bfv/keygen.rs:39-45).  Residues are canonical, in [0, q_i).
+ *   - NTT domain: ciphertexts are stored as NttPoly evaluations (src/ring/ntt.rs:11-15)
+ *     in THIS library's documented convention (DESIGN.md "NTT convention"): negacyclic
+ *     Cooley-Tukey, evaluation k = a(psi^(2*brv(k)+1)), psi = smallest-generator
+ *     primitive 2n-th root.  concrete-ntt's own order is not observable from the
+ *     reference's tests; all parity is checked after the inverse transform.
+ *   - Functions without suffix take HOST pointers and are synchronous.  The `_dev`
+ *     variants take DEVICE pointers (hipMalloc'd on the context's device) and are
+ *     asynchronous on the context's stream (exacto_ctx_set_stream); call
+ *     exacto_synchronize() before reading results.
+ *   - Inputs are read-only (the reference borrows &BfvCiphertext); outputs never alias
+ *     inputs unless stated.
+ *   - A context is not thread-safe; use one context per host thread (the reference's
+ *     types are Send+Sync because they are immutable; here the stream is shared state).
+ */
+#ifndef EXACTO_HIP_H
+#define EXACTO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct exacto_ctx exacto_ctx;
+
+enum exacto_status {
+    EXACTO_OK = 0,
+    EXACTO_ERR_INVALID_PARAM = 1,
+    EXACTO_ERR_DIMENSION_MISMATCH = 2,
+    EXACTO_ERR_MODULUS_MISMATCH = 3,
+    EXACTO_ERR_INVALID_RING_DEGREE = 4,
+    EXACTO_ERR_DECRYPTION = 5,
+    EXACTO_ERR_DECOMPOSITION = 6,
+    EXACTO_ERR_LATTICE = 7,
+    EXACTO_ERR_MISSING_KEY = 8,
+    EXACTO_ERR_NOT_IMPLEMENTED = 9,
+    EXACTO_ERR_HIP = 100
+};
+
+/* Multiplication algorithm selected for the context (mirrors the dispatcher
+ * bfv_mul_no_relin, src/bfv/eval.rs:89-108). */
+enum exacto_mul_path {
+    EXACTO_PATH_EXACT_RNS = 0,   /* L > 1: exact CRT + exact rounding (eval.rs:113-147) */
+    EXACTO_PATH_HPS = 1,         /* L = 1 with aux basis: literal HPS (eval.rs:157-413)  */
+    EXACTO_PATH_SCHOOLBOOK = 2   /* L = 1, no aux: exact i128 semantics (eval.rs:416-454) */
+};
+
+typedef struct exacto_ctx_info {
+    size_t ring_degree;       /* n */
+    size_t num_ct_moduli;     /* L */
+    size_t num_aux_moduli;    /* user aux basis size */
+    size_t num_internal_aux;  /* primes the exact path adds internally (0 for HPS) */
+    size_t gadget_digits;     /* G (params/mod.rs:126-140) */
+    uint64_t gadget_base;
+    uint64_t plain_modulus;
+    int mul_path;             /* enum exacto_mul_path */
+    int device;
+} exacto_ctx_info;
+
+/* ---- context: replaces BfvParamsBuilder::build + RnsBasis::new + make_plan ----
+ * params/mod.rs:81-124, ring/rns.rs:35-63, ring/ntt.rs:19-29.
+ * gadget_base = 0 selects the reference default 2^16 (params/mod.rs:102-108).
+ * aux_moduli may be NULL when num_aux == 0.  Errors as the builder: InvalidRingDegree,
+ * InvalidParam ("must specify at least one ciphertext modulus", "plaintext modulus must
+ * be >= 2", "cannot create NTT plan for n=.., q=.. ..."). */
+int exacto_ctx_create(exacto_ctx** out, size_t ring_degree, const uint64_t* ct_moduli,
+                      size_t num_ct_moduli, const uint64_t* aux_moduli, size_t num_aux,
+                      uint64_t plain_modulus, uint64_t gadget_base, int device);
+void exacto_ctx_destroy(exacto_ctx* ctx);
+int exacto_ctx_get_info(const exacto_ctx* ctx, exacto_ctx_info* info);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+int exacto_ctx_set_stream(exacto_ctx* ctx, void* hip_stream);
+/* Products per pipeline chunk (workspace = chunk * ~3 MB at n=4096, L=3). 0 = default. */
+int exacto_ctx_set_chunk(exacto_ctx* ctx, size_t products_per_chunk);
+int exacto_synchronize(exacto_ctx* ctx);
+
+/* ---- relinearisation key: RelinKey (bfv/keygen.rs:39-45, made by gen_relin_key_with_rng
+ * keygen.rs:123-162).  rlk = [num_keys][2][L][n], NTT domain.  relinearize uses
+ * min(G, num_keys) digits (keyswitch.rs:86-89). */
+int exacto_ctx_load_relin_key(exacto_ctx* ctx, const uint64_t* rlk, size_t num_keys);
+int exacto_ctx_load_relin_key_dev(exacto_ctx* ctx, const uint64_t* rlk_dev, size_t num_keys);
+/* Device pointer of the resident key (for an RCCL broadcast into it), or NULL. */
+uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* ctx, size_t num_keys);
+
+/* ---- NTT engine: concrete_ntt::prime64::Plan::{fwd, inv + normalize} ----
+ * NttPoly::from_coeff_poly / to_coeff_poly (ntt.rs:42-67).  polys = [count][n], all mod
+ * ct prime `limb`, transformed in place. */
+int exacto_ntt_fwd(exacto_ctx* ctx, uint64_t* polys, size_t count, size_t limb);
+int exacto_ntt_inv(exacto_ctx* ctx, uint64_t* polys, size_t count, size_t limb);
+int exacto_ntt_fwd_dev(exacto_ctx* ctx, uint64_t* polys, size_t count, size_t limb);
+int exacto_ntt_inv_dev(exacto_ctx* ctx, uint64_t* polys, size_t count, size_t limb);
+/* RnsPoly batches [count][L][n]: RnsPoly::from_coeff_poly per limb (rns.rs:84-105,
+ * coefficients already reduced mod q_i) and the per-limb inverse. */
+int exacto_rns_fwd_dev(exacto_ctx* ctx, uint64_t* polys, size_t count);
+int exacto_rns_inv_dev(exacto_ctx* ctx, uint64_t* polys, size_t count);
+
+/* ---- RNS pointwise ops: RnsPoly::{add,sub,neg,mul,scalar_mul} (rns.rs:159-217 ->
+ * NttPoly ops ntt.rs:75-139).  a, b, out = [count][L][n]; out may alias a or b. */
+int exacto_rns_add_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
+int exacto_rns_sub_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
+int exacto_rns_neg_dev(exacto_ctx* ctx, const uint64_t* a, uint64_t* out, size_t count);
+int exacto_rns_mul_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
+int exacto_rns_scalar_mul_dev(exacto_ctx* ctx, const uint64_t* a, uint64_t scalar, uint64_t* out, size_t count);
+
+/* ---- BFV ciphertext ops (bfv/eval.rs).  Degree-1 ct batches [B][2][L][n]. ---- */
+/* bfv_add / bfv_sub / bfv_neg (eval.rs:14-60) on equal-degree ciphertexts of `polys` polys. */
+int exacto_bfv_add_dev(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, size_t batch, size_t polys);
+int exacto_bfv_sub_dev(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, size_t batch, size_t polys);
+int exacto_bfv_neg_dev(exacto_ctx* ctx, const uint64_t* ct, uint64_t* out, size_t batch, size_t polys);
+
+/* bfv_mul_no_relin (eval.rs:89-108): out = [B][3][L][n].  `polys1`/`polys2` are the
+ * input ciphertexts' component counts (must be 2: "multiplication requires degree-1
+ * ciphertexts"). */
+int exacto_bfv_mul_no_relin(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2,
+                            size_t polys2, uint64_t* out, size_t batch);
+int exacto_bfv_mul_no_relin_dev(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2,
+                                size_t polys2, uint64_t* out, size_t batch);
+
+/* relinearize (bfv/keyswitch.rs:59-101): ct = [B][polys][L][n] -> out = [B][2][L][n].
+ * polys < 3: copied; polys > 3: InvalidParam "relinearization only supports degree-2
+ * ciphertexts". */
+int exacto_relinearize(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
+int exacto_relinearize_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
+
+/* bfv_mul_and_relin (eval.rs:73-82): ct1, ct2 = [B][2][L][n] -> out = [B][2][L][n]. */
+int exacto_bfv_mul_and_relin(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out,
+                             size_t batch);
+int exacto_bfv_mul_and_relin_dev(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2,
+                                 uint64_t* out, size_t batch);
+
+/* gadget_decompose (keyswitch.rs:11-52) of coefficient-domain RNS polynomials [B][L][n]
+ * (CRT value mod Q, extension semantics when Q >= 2^64) -> digits [B][G'][L][n] as
+ * residues mod q_i, G' = min(G, num_digits). */
+int exacto_gadget_decompose_dev(exacto_ctx* ctx, const uint64_t* coeffs, uint64_t* digits,
+                                size_t batch, size_t num_digits);
+
+/* ---- dBFV: dbfv_mul (dbfv/eval.rs:82-149) + reduce (dbfv/reduction.rs:15-60) ----
+ * a, b, out = [B][d][2][L][n]; base/plain as DbfvParams (params/mod.rs:144-193,
+ * plain_modulus 0 == 2^64).  depth_a/depth_b = mul_depth of each input (NULL = 0);
+ * depth_out receives mul_depth of each output (NULL allowed).  Errors:
+ * "multiplication requires d-limb ciphertexts" is not reachable through fixed shapes;
+ * depth > 1 -> NotImplemented "chained dBFV multiplication requires ciphertext-level
+ * lattice reduction (paper §4.6.2)". */
+int exacto_dbfv_mul(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                    const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch,
+                    const uint32_t* depth_a, const uint32_t* depth_b, uint32_t* depth_out);
+int exacto_dbfv_mul_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                        const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch,
+                        const uint32_t* depth_a, const uint32_t* depth_b, uint32_t* depth_out);
+
+/* ---- diagnostics ---- */
+/* Copies the last error message of this thread (NUL-terminated); returns its length. */
+size_t exacto_last_error(char* buf, size_t len);
+/* Per-kernel-family timing of the last profiled calls: enable, then read
+ * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic
+ * bytes (16*n per polynomial). */
+int exacto_prof_enable(exacto_ctx* ctx, int enable);
+int exacto_prof_read(exacto_ctx* ctx, int kind, uint64_t* launches, double* total_ms,
+                     double* total_bytes, uint64_t* polys);
+const char* exacto_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EXACTO_HIP_H */

@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:
+    sys.path.insert(0, TESTS)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libexacto_hip.so")
+    config.addinivalue_line("markers", "slow: long-running oracle comparisons")
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return True
