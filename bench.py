@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X ciphertext-multiplication path (BASELINE.json metric).
+
+Workload (default, BASELINE configs[2]): bfv_mul_and_relin at n=4096, 3x60-bit RNS limbs,
+p=65537, gadget base 2^16 (G=12), a batch of 1024 independent ciphertext pairs per GPU
+(weak scaling).  A "step" is one pass of the whole batch through the path, with inputs
+already resident in HBM.  Synthetic data: uniform canonical residues per limb (the path
+is deterministic given (ct1, ct2, rlk), so encrypted vs uniform inputs cost the same).
+
+Multi-GPU: one process per GPU (torchrun).  The relinearisation key is generated on rank 0
+and broadcast over RCCL (xGMI); every rank then processes its own batch shard with no
+data-path collective.  value = total products over all ranks / max-over-ranks step time.
+
+Also reported on the same JSON line:
+  roofline     — the dominant kernel (forward NTT of the pipeline), algorithmic bytes
+                 16*n per residue polynomial over its summed launch time,
+                 measured with HIP events around each of its launches on the pipeline's
+                 stream, vs the 8 TB/s HBM peak;
+  cpu_baseline — the CPU restatement of the reference algorithm (oracle/, exact BigInt
+                 schoolbook tensor, eval.rs:113-147) on a bounded sample, rank 0 at N=1.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from exacto_amd._ffi import HipContext  # noqa: E402
+
+Q3 = [1152921504606830593, 1152921504606748673, 1152921504606683137]
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (n, moduli, aux, plain, gadget_base)
+    "cfg3": (4096, Q3, [], 65537, 1 << 16),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="ciphertext pairs per GPU")
+    ap.add_argument("--chunk", type=int, default=0, help="products per pipeline chunk (0 = library default)")
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="products timed for the CPU baseline (0 = auto)")
+    return ap.parse_args()
+
+
+def uniform_dev(shape_prefix, moduli, n, gen, device):
+    out = torch.empty(tuple(shape_prefix) + (len(moduli), n), dtype=torch.int64, device=device)
+    for i, q in enumerate(moduli):
+        out[..., i, :] = torch.randint(0, q, tuple(shape_prefix) + (n,), generator=gen,
+                                       dtype=torch.int64, device=device)
+    return out
+
+
+def cpu_baseline(n, moduli, plain, gbase, sample):
+    """Time the CPU restatement of the reference algorithm on `sample` products (1 thread)."""
+    from oracle import params as P
+    from oracle import bfv as obfv
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from bridge import uniform_residues, np_to_ct, np_to_rlk
+    try:
+        from oracle import cref
+        use_c = cref.available()
+    except Exception:
+        use_c = False
+    prm = P.BfvParamsBuilder().ring_degree(n).plain_modulus(plain).ct_moduli(moduli).gadget_base(gbase).build()
+    rng = np.random.default_rng(7)
+    ct1 = uniform_residues(rng, (sample, 2), moduli, n)
+    ct2 = uniform_residues(rng, (sample, 2), moduli, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), moduli, n)
+    if use_c:
+        t0 = time.perf_counter()
+        cref.bfv_mul_and_relin(prm, ct1, ct2, rlk)
+        dt = time.perf_counter() - t0
+        impl = "oracle/c (C restatement, exact multiword schoolbook tensor)"
+    else:
+        rk = np_to_rlk(rlk, prm)
+        t0 = time.perf_counter()
+        for b in range(sample):
+            obfv.bfv_mul_and_relin(np_to_ct(ct1[b], prm), np_to_ct(ct2[b], prm), rk)
+        dt = time.perf_counter() - t0
+        impl = "oracle/ (Python exact-integer restatement)"
+    return {"value": sample / dt, "unit": "bfv_mul_and_relin/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} bfv_mul_and_relin of the same workload (n={n}, L={len(moduli)}), "
+                      f"single thread, {impl}; {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    n, moduli, aux, plain, gbase = CONFIGS[args.config]
+    L = len(moduli)
+    B = args.batch
+    ctx = HipContext(n, moduli, aux, plain, gbase, device=local)
+    stream = torch.cuda.current_stream(device)
+    ctx.set_stream(stream.cuda_stream)
+    if args.chunk:
+        ctx.set_chunk(args.chunk)
+    G = ctx.G
+
+    gen = torch.Generator(device=device)
+    gen.manual_seed(0xE7AC7003 + rank)
+    ct1 = uniform_dev((B, 2), moduli, n, gen, device)
+    ct2 = uniform_dev((B, 2), moduli, n, gen, device)
+    out = torch.empty_like(ct1)
+
+    # relinearisation key: made once on rank 0, RCCL-broadcast to every GPU
+    kgen = torch.Generator(device=device)
+    kgen.manual_seed(0xE7AC7003)
+    rlk = uniform_dev((G, 2), moduli, n, kgen, device) if rank == 0 else \
+        torch.empty((G, 2, L, n), dtype=torch.int64, device=device)
+    if distributed:
+        dist.broadcast(rlk, src=0)
+    ctx.load_relin_key_dev(rlk, G)
+    torch.cuda.synchronize(device)
+
+    def step():
+        ctx.bfv_mul_and_relin_dev(ct1, ct2, out, B)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = world * B * args.steps / elapsed
+
+    # roofline of the dominant kernel: one profiled step, HIP events around every NTT launch
+    ctx.prof_enable(True)
+    step()
+    torch.cuda.synchronize(device)
+    fwd = ctx.prof_read(0)
+    inv = ctx.prof_read(1)
+    ctx.prof_enable(False)
+    dom, dom_name = (fwd, "ntt_fwd_kernel<12>") if fwd["ms"] >= inv["ms"] else (inv, "ntt_inv_kernel<12>")
+    achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9 if dom["ms"] > 0 else 0.0
+    per_launch_ms = dom["ms"] / max(dom["launches"], 1)
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": dom_name,
+        "launches_per_step": dom["launches"],
+        "avg_launch_us": round(per_launch_ms * 1000.0, 2),
+        "bytes_per_launch": dom["bytes"] / max(dom["launches"], 1),
+        "polys_per_step": dom["polys"],
+        "ntt_share_of_step": round((fwd["ms"] + inv["ms"]) / ms_per_step, 3),
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = args.cpu_sample or 3
+        try:
+            cpu = cpu_baseline(n, moduli, plain, gbase, sample)
+        except Exception as e:  # the baseline is informative; never fail the bench on it
+            cpu = {"value": None, "error": repr(e)}
+
+    if rank == 0:
+        line = {
+            "metric": "ciphertext muls/sec (bfv_mul_and_relin)",
+            "value": round(value, 1),
+            "unit": "bfv_mul_and_relin/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (uniform canonical residues per limb, seeded; rlk broadcast over RCCL)",
+            "config": {"workload": "bfv_mul_and_relin, BASELINE configs[2]", "ring_degree": n,
+                       "ct_limbs": L, "limb_bits": 60, "plain_modulus": plain, "gadget_base": gbase,
+                       "gadget_digits": G, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"batch-shard x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
