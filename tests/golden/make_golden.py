@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/.
+
+1. kats.json — the reference's own known-answer tests for this path.  Every entry cites the
+   reference test (path:line) whose assertion it transcribes; expected values are the literal
+   numbers of those assertions, or the plain-integer expression the assertion itself states
+   (e.g. modular.rs:135 asserts barrett_reduce(123456789) == 123456789 % m).  No reference code
+   is executed (it is Rust and cannot be built here).
+2. vectors.npz — seeded inputs and oracle outputs (Python restatement, cross-checked with the
+   C restatement) for every dispatch branch at small sizes, plus dBFV cases.
+3. digests.json — SHA-256 of the C-oracle output for full-size cfg3 (n=4096, 3x60-bit) on
+   seeded inputs; the GPU tests regenerate the inputs and compare digests.
+
+Run: python tests/golden/make_golden.py   (takes ~1 minute)
+"""
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle import bfv as obfv, dbfv as odbfv, params as P  # noqa: E402
+from bridge import ct_to_np, np_to_ct, np_to_rlk, uniform_residues  # noqa: E402
+
+M = 65537
+
+
+def kats():
+    k = []
+
+    def add(src, fn, args, expected):
+        k.append({"source": src, "fn": fn, "args": args, "expected": expected})
+
+    # src/ring/modular.rs tests (m = 65537)
+    add("src/ring/modular.rs:131", "barrett_reduce", [0, M], 0)
+    add("src/ring/modular.rs:132", "barrett_reduce", [1, M], 1)
+    add("src/ring/modular.rs:133", "barrett_reduce", [M, M], 0)
+    add("src/ring/modular.rs:134", "barrett_reduce", [M + 1, M], 1)
+    add("src/ring/modular.rs:135", "barrett_reduce", [123456789, M], 123456789 % M)
+    add("src/ring/modular.rs:142", "mod_mul", [1234, 5678, M], (1234 * 5678) % M)
+    add("src/ring/modular.rs:143", "mod_mul", [0, 5678, M], 0)
+    add("src/ring/modular.rs:144", "mod_mul", [1, 5678, M], 5678)
+    add("src/ring/modular.rs:150", "mod_add", [100, 200, M], 300)
+    add("src/ring/modular.rs:151", "mod_add", [M - 1, 2, M], 1)
+    add("src/ring/modular.rs:152", "mod_sub", [200, 100, M], 100)
+    add("src/ring/modular.rs:153", "mod_sub", [100, 200, M], M - 100)
+    add("src/ring/modular.rs:159", "mod_neg", [0, M], 0)
+    add("src/ring/modular.rs:160", "mod_neg", [1, M], M - 1)
+    add("src/ring/modular.rs:167", "mod_pow", [2, 10, M], 1024)
+    add("src/ring/modular.rs:168", "mod_pow", [2, 16, M], 65536 % M)
+    add("src/ring/modular.rs:169", "mod_pow", [3, 0, M], 1)
+    add("src/ring/modular.rs:178", "mod_inv_times_a", [12345, M], 1)
+    add("src/ring/modular.rs:188", "montgomery_check", [M], 0)
+    add("src/ring/modular.rs:201", "montgomery_reduce_am", [12345, M], 0)
+    # src/ring/poly.rs tests (Z_17[X]/(X^4+1))
+    add("src/ring/poly.rs:185-190", "poly_add", [[1, 2, 3, 4], [5, 6, 7, 8], 17], [6, 8, 10, 12])
+    add("src/ring/poly.rs:190", "poly_sub", [[6, 8, 10, 12], [5, 6, 7, 8], 17], [1, 2, 3, 4])
+    add("src/ring/poly.rs:194-198", "poly_neg_add_is_zero", [[1, 0, 3, 16], 17], [0, 0, 0, 0])
+    add("src/ring/poly.rs:202-207", "mul_naive", [[1, 1, 0, 0], [1, 1, 0, 0], 17], [1, 2, 1, 0])
+    add("src/ring/poly.rs:210-218", "mul_naive", [[0, 0, 0, 1], [0, 0, 0, 1], 17], [0, 0, 16, 0])
+    add("src/ring/poly.rs:221-225", "scalar_mul", [[1, 2, 3, 4], 3, 17], [3, 6, 9, 12])
+    add("src/ring/poly.rs:228-233", "centered_coeffs", [[0, 1, 16, 9], 17], [0, 1, -1, -8])
+    # src/ring/ntt.rs tests (n = 16, q = 65537)
+    add("src/ring/ntt.rs:170-178", "ntt_roundtrip", [[1, 2, 3, 4, 5, 6, 7, 8], 16, M], [1, 2, 3, 4, 5, 6, 7, 8])
+    add("src/ring/ntt.rs:181-195", "ntt_mul", [[1, 1], [1, 1], 16, M], [1, 2, 1] + [0] * 13)
+    add("src/ring/ntt.rs:198-212", "ntt_add", [[1, 2, 3], [4, 5, 6], 16, M], [5, 7, 9] + [0] * 13)
+    # src/ring/rns.rs tests (single prime 65537, n = 16)
+    add("src/ring/rns.rs:299-306", "rns_roundtrip", [[1, 2, 3, 4, 5, 6, 7, 8], 16, [M]], [1, 2, 3, 4, 5, 6, 7, 8] + [0] * 8)
+    add("src/ring/rns.rs:309-322", "rns_add", [[1, 2, 3, 4, 5, 6, 7, 8], [10, 20, 30, 40, 50, 60, 70, 80], 16, [M]],
+        [11, 22, 33, 44, 55, 66, 77, 88] + [0] * 8)
+    add("src/ring/rns.rs:325-338", "rns_mul", [[1, 1], [1, 1], 16, [M]], [1, 2, 1] + [0] * 13)
+    # src/bfv/keyswitch.rs tests
+    add("src/bfv/keyswitch.rs:111-119", "gadget_decompose", [[42], M, 16, 2], [[65531], [3]])
+    add("src/bfv/keyswitch.rs:122-144", "gadget_reconstruct", [[12345, 54321, 100, 0], M, 16, 4], [12345, 54321, 100, 0])
+    add("src/bfv/keyswitch.rs:147-152", "gadget_decompose_digit0", [[M - 1], M, 16, 4], M - 1)
+    # src/bfv/encrypt.rs:300-330 — Delta = floor(Q/p) residues for Q = q0*q1
+    q0, q1 = 1099509805057, 562949953443841
+    delta = (q0 * q1) // 257
+    add("src/bfv/encrypt.rs:300-330", "delta_residues", [[q0, q1], 257], [delta % q0, delta % q1])
+    # decrypt-level functional tests (values the reference asserts)
+    add("src/bfv/eval.rs:883-900", "bfv_mul_decrypt", ["compact_bfv", 3, 7], 21)
+    add("src/bfv/eval.rs:903-927", "bfv_mul_decrypt_multiprime", [[16, 257, [65537, 1099509805057], 8],
+                                                                  [[3, 7], [10, 20], [0, 5]]], [21, 200, 0])
+    add("src/dbfv/eval.rs:223-237", "dbfv_mul_decrypt", ["compact_dbfv", 3, 7], 21)
+    add("src/dbfv/eval.rs:272-290", "dbfv_mul_decrypt_many", ["compact_dbfv", [[15, 15], [10, 20], [12, 12]]],
+        [(15 * 15) % 256, (10 * 20) % 256, (12 * 12) % 256])
+    add("src/dbfv/eval.rs:292-313", "dbfv_depth_guard", ["compact_dbfv"],
+        "chained dBFV multiplication requires ciphertext-level lattice reduction")
+    add("src/dbfv/eval.rs:385-416", "hps_single_aux_guard", [[4096, 1040407, [18014398509506561], [36028797018972161], 256]],
+        "single aux prime too small")
+    add("src/dbfv/eval.rs:419-453", "schoolbook_guard", [[4096, 1040407, [18014398509506561], [], 256]],
+        "schoolbook BFV multiplication can overflow i128")
+    return k
+
+
+def bfv_case(name, prm, B, seed, num_keys=None):
+    rng = np.random.default_rng(seed)
+    q, n = prm.ct_basis.moduli, prm.ring_degree
+    ct1 = uniform_residues(rng, (B, 2), q, n)
+    ct2 = uniform_residues(rng, (B, 2), q, n)
+    G = prm.gadget_digits if num_keys is None else num_keys
+    rlk = uniform_residues(rng, (G, 2), q, n)
+    rk = np_to_rlk(rlk, prm)
+    out, out3 = [], []
+    for b in range(B):
+        c1, c2 = np_to_ct(ct1[b], prm), np_to_ct(ct2[b], prm)
+        m = obfv.bfv_mul_no_relin(c1, c2)
+        out3.append(ct_to_np(m))
+        out.append(ct_to_np(obfv.relinearize(m, rk)))
+    aux = prm.aux_basis.moduli if prm.aux_basis is not None else []
+    meta = {"n": n, "ct_moduli": [str(x) for x in q], "aux_moduli": [str(x) for x in aux],
+            "plain": prm.plain_modulus, "gadget_base": prm.gadget_base, "gadget_digits": prm.gadget_digits}
+    return name, meta, {"ct1": ct1, "ct2": ct2, "rlk": rlk, "out": np.stack(out), "out3": np.stack(out3)}
+
+
+def dbfv_case(name, dprm, B, seed):
+    prm = dprm.bfv_params
+    rng = np.random.default_rng(seed)
+    q, n, d = prm.ct_basis.moduli, prm.ring_degree, dprm.num_digits
+    a = uniform_residues(rng, (B, d, 2), q, n)
+    b = uniform_residues(rng, (B, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    rk = np_to_rlk(rlk, prm)
+    outs = []
+    for i in range(B):
+        A = odbfv.DbfvCiphertext([np_to_ct(a[i, k], prm) for k in range(d)], d, 0, dprm)
+        Bc = odbfv.DbfvCiphertext([np_to_ct(b[i, k], prm) for k in range(d)], d, 0, dprm)
+        r = odbfv.dbfv_mul(A, Bc, rk)
+        outs.append(np.stack([ct_to_np(l) for l in r.limbs]))
+    aux = prm.aux_basis.moduli if prm.aux_basis is not None else []
+    meta = {"n": n, "ct_moduli": [str(x) for x in q], "aux_moduli": [str(x) for x in aux],
+            "plain": prm.plain_modulus, "gadget_base": prm.gadget_base, "gadget_digits": prm.gadget_digits,
+            "d": d, "base": dprm.base, "dbfv_plain": dprm.plain_modulus}
+    return name, meta, {"a": a, "b": b, "rlk": rlk, "out": np.stack(outs)}
+
+
+def bfv_cases():
+    B = P.BfvParamsBuilder
+    yield bfv_case("multiprime16", B().ring_degree(16).plain_modulus(257).ct_moduli([65537, 1099509805057])
+                   .gadget_base(8).build(), 2, 101)
+    yield bfv_case("cfg1_compact", P.compact_bfv(), 1, 102)
+    yield bfv_case("cfg3_n64", P.cfg3_params(64), 2, 103)
+    yield bfv_case("cfg3_n64_3keys", P.cfg3_params(64), 1, 104, num_keys=3)
+    yield bfv_case("cfg5basis_n32", B().ring_degree(32).plain_modulus(1040407).ct_moduli(P.Q4)
+                   .gadget_base(256).build(), 1, 105)
+    yield bfv_case("hps2_n64", B().ring_degree(64).plain_modulus(1040407).ct_moduli([1152921504606830593])
+                   .aux_moduli([18014398509998081, 36028797018972161]).gadget_base(256).build(), 2, 106)
+    yield bfv_case("schoolbook16", B().ring_degree(16).plain_modulus(17).ct_moduli([65537]).gadget_base(4).build(),
+                   2, 107)
+    yield bfv_case("oddbase16", B().ring_degree(16).plain_modulus(17).ct_moduli([65537, 1099509805057])
+                   .gadget_base(5).build(), 2, 108)
+
+
+def dbfv_cases():
+    yield dbfv_case("dbfv_compact", P.compact_dbfv(), 1, 201)
+    yield dbfv_case("dbfv_cfg4_n32", P.cfg4_params(32), 2, 202)
+    yield dbfv_case("dbfv_cfg5basis_n16", P.cfg5_params(16), 1, 203)
+
+
+DIGEST_SPEC = {"config": "cfg3", "n": 4096, "batch": 2, "seed": 3003,
+               "generator": "numpy.random.default_rng(seed); ct1, ct2 = uniform_residues((B,2)); "
+                            "rlk = uniform_residues((G,2))  (tests/bridge.py)"}
+
+
+def digest_inputs(spec):
+    prm = P.cfg3_params(spec["n"])
+    rng = np.random.default_rng(spec["seed"])
+    q, n = prm.ct_basis.moduli, prm.ring_degree
+    ct1 = uniform_residues(rng, (spec["batch"], 2), q, n)
+    ct2 = uniform_residues(rng, (spec["batch"], 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    return prm, ct1, ct2, rlk
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint64).tobytes()).hexdigest()
+
+
+def main():
+    with open(os.path.join(HERE, "kats.json"), "w") as f:
+        json.dump(kats(), f, indent=1)
+    arrays, meta = {}, {}
+    for name, m, arr in list(bfv_cases()) + list(dbfv_cases()):
+        meta[name] = m
+        for k, v in arr.items():
+            arrays[f"{name}__{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "vectors.npz"), **arrays)
+    with open(os.path.join(HERE, "vectors_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    from oracle import cref
+    prm, ct1, ct2, rlk = digest_inputs(DIGEST_SPEC)
+    out = cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=2)
+    spec = dict(DIGEST_SPEC)
+    spec["sha256_inputs"] = sha(np.concatenate([ct1.ravel(), ct2.ravel(), rlk.ravel()]))
+    spec["sha256_out"] = sha(out)
+    with open(os.path.join(HERE, "digests.json"), "w") as f:
+        json.dump({"cfg3_full": spec}, f, indent=1)
+    print("wrote kats.json, vectors.npz, vectors_meta.json, digests.json")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,54 @@
+"""CPU: the C-ABI library loads, exports every symbol include/exacto_hip.h declares, and
+validates parameters with the reference's error variants/messages before touching a GPU."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from exacto_amd import _ffi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "exacto_hip.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(exacto_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(_ffi.lib_path())
+    syms = header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the Python binding declares the same set
+    assert sorted(_ffi.EXPORTED_SYMBOLS) == syms
+
+
+def test_version():
+    assert b"gfx950" in _ffi.load().exacto_version()
+
+
+@pytest.mark.parametrize("n,moduli,plain,variant,text", [
+    (12, [65537], 257, "InvalidRingDegree", "ring degree must be a power of 2, got 12"),
+    (16, [], 257, "InvalidParam", "must specify at least one ciphertext modulus"),
+    (16, [65537], 1, "InvalidParam", "plaintext modulus must be >= 2"),
+    (16, [65539], 257, "InvalidParam", "cannot create NTT plan for n=16, q=65539"),
+    (8, [65537], 257, "InvalidParam", "cannot create NTT plan for n=8"),
+    (16, [(1 << 62) + 1], 257, "InvalidParam", "cannot create NTT plan"),
+])
+def test_ctx_create_validation(n, moduli, plain, variant, text):
+    with pytest.raises(_ffi.ExactoError) as e:
+        _ffi.HipContext(n, moduli, plain_modulus=plain)
+    assert e.value.variant == variant
+    assert text in str(e.value)
+
+
+def test_no_silent_fallback(monkeypatch, tmp_path):
+    monkeypatch.setattr(_ffi, "_LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_ffi, "_lib", None)
+    with pytest.raises(RuntimeError):
+        _ffi.load()
