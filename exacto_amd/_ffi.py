@@ -178,7 +178,8 @@ class HipContext:
 
     # ---- configuration
     def set_stream(self, stream_handle: int | None):
-        check(self._lib.exacto_ctx_set_stream(self._h, stream_handle))
+        """Enqueue on this hipStream_t handle (0/None = the default stream)."""
+        check(self._lib.exacto_ctx_set_stream(self._h, stream_handle or None))
 
     def set_chunk(self, chunk: int):
         check(self._lib.exacto_ctx_set_chunk(self._h, chunk))

@@ -43,10 +43,33 @@ struct PrimeConst {
     const TwPair* tw_inv;      // [n] psi^-brv(i)
 };
 
+// hi64(y * s) from 32-bit halves.  u = y1*s0 + hi(y0*s0) fits 64 bits; v = y0*s1 + u is
+// a 65-bit sum, and y*s = lo(y0*s0) + 2^32*v + 2^64*y1*s1, so hi64 = y1*s1 + (v >> 32).
+// Written this way hipcc keeps every v_mad_u64_u32 addend a natural 64-bit value
+// (no zero-extension moves) and the carry in v_addc.
+__device__ __forceinline__ u64 mulhi64(u64 y, u64 s) {
+    const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)(y >> 32);
+    const uint32_t s0 = (uint32_t)s, s1 = (uint32_t)(s >> 32);
+    const u64 u = (u64)y1 * s0 + __umulhi(y0, s0);
+    const u128 v = (u128)((u64)y0 * s1) + u;
+    return (u64)y1 * s1 + (u64)(v >> 32);
+}
+
+// Shoup: x < 2^64, w < q, ws = floor(w * 2^64 / q), nq = 2^64 - q.  Returns x*w mod q in
+// [0, 2q) as lo64(x*w + qhat*nq): -q is folded into a chained mad instead of a 64-bit sub.
+__device__ __forceinline__ u64 shoup_mul_nq(u64 x, u64 w, u64 ws, u64 nq) {
+    const u64 qh = mulhi64(x, ws);
+    const uint32_t x0 = (uint32_t)x, x1 = (uint32_t)(x >> 32);
+    const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+    const uint32_t h0 = (uint32_t)qh, h1 = (uint32_t)(qh >> 32);
+    const uint32_t n0 = (uint32_t)nq, n1 = (uint32_t)(nq >> 32);
+    const u64 t = (u64)h0 * n0 + (u64)x0 * w0;
+    const uint32_t cross = x0 * w1 + x1 * w0 + h0 * n1 + h1 * n0;
+    return t + ((u64)cross << 32);
+}
+
 __device__ __forceinline__ u64 shoup_mul(u64 x, u64 w, u64 ws, u64 q) {
-    // x < 2^64, w < q: returns x*w mod q in [0, 2q)
-    u64 qh = __umul64hi(x, ws);
-    return x * w - qh * q;
+    return shoup_mul_nq(x, w, ws, (u64)0 - q);
 }
 
 __device__ __forceinline__ u64 shoup_mul_red(u64 x, u64 w, u64 ws, u64 q) {

@@ -425,7 +425,8 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
         for (u64 q : c->ctq) need.mul(q);
         Big P(1);
         const u64 step = 2 * n;
-        u64 cand = ((1ull << 62) - 1) / step * step + 1;
+        // below 2^60 so every prime of the exact path takes the lazy forward NTT (16q <= 2^64)
+        u64 cand = ((1ull << 60) - 1) / step * step + 1;
         while (P.cmp(need) <= 0) {
             while (cand > step) {
                 cand -= step;
@@ -479,19 +480,14 @@ extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
 }
 
 extern "C" int exacto_ctx_set_stream(exacto_ctx* c, void* s) {
+    // The handle is used as given; NULL is the device's default (null) stream, which is what
+    // torch.cuda.current_stream().cuda_stream returns for the default torch stream.
     if (!c) return invalid_param("null context");
     HIP_TRY(hipSetDevice(c->device));
-    if (c->own_stream && c->stream) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(hipStreamDestroy(c->stream));
-    }
-    if (s) {
-        c->stream = (hipStream_t)s;
-        c->own_stream = false;
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        c->own_stream = true;
-    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->own_stream && c->stream) HIP_TRY(hipStreamDestroy(c->stream));
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
     return 0;
 }
 
@@ -548,7 +544,9 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
         HIP_TRY(hipEventCreate(&rec.b));
         HIP_TRY(hipEventRecord(rec.a, c->stream));
     }
-    launch_ntt(nb, (int)count, c->logn, inverse, c->d_primes, c->stream);
+    bool lazy = true;
+    for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) lazy &= c->primes[t] < (1ull << 60);
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));

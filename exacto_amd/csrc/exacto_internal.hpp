@@ -53,7 +53,8 @@ struct CrtTables {
     u64 hps_p1_inv_p0, hps_p0_inv_p1;
 };
 
-void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, const PrimeConst* primes,
+// lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)
+void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
                 hipStream_t s);
 
 // ---- kernels.hip launchers (all asynchronous on `s`) ----

@@ -19,6 +19,12 @@ __device__ __forceinline__ int swz(int j) {
     return j ^ ((j >> 4) & 15) ^ (((j >> 8) & 1) << 4);
 }
 
+// LDS-only workgroup barrier: waits for this wave's LDS traffic only (__syncthreads() would
+// also add vmcnt(0), serialising the tail of the output stores of the previous round).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int LO>
 __device__ __forceinline__ int elem_index(int tid, int k) {
     return ((tid >> LO) << (LO + 4)) | (k << LO) | (tid & ((1 << LO) - 1));
@@ -39,9 +45,9 @@ __device__ __forceinline__ void lds_load(const u64* lds, u64 (&x)[16], int tid) 
 // ---------------------------------------------------------------- forward
 
 // Butterflies for stage bits BHI..BLO (descending) inside window [LO, LO+4).
-template <int LOGN, int LO, int BHI, int BLO>
+template <int LOGN, int LO, int BHI, int BLO, bool LAZY>
 __device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* __restrict__ tw,
-                                          u64 q, u64 q2) {
+                                          u64 nq, u64 q2) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
 #pragma unroll
@@ -57,8 +63,8 @@ __device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* _
                 const int k0 = g * 2 * half + m;
                 const int k1 = k0 + half;
                 u64 X = x[k0];
-                X = X >= q2 ? X - q2 : X;
-                const u64 T = shoup_mul(x[k1], t.w, t.ws, q);
+                if (!LAZY) X = X >= q2 ? X - q2 : X;
+                const u64 T = shoup_mul_nq(x[k1], t.w, t.ws, nq);
                 x[k0] = X + T;
                 x[k1] = X - T + q2;
             }
@@ -66,23 +72,30 @@ __device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* _
     }
 }
 
-template <int LOGN, int R>
-__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw, u64 q,
-                                           u64 q2) {
+// LAZY (all q < 2^60, so 16q <= 2^64): no per-butterfly reduction.  A round of <= 4 stages
+// adds < 2q per stage to the bound, so values < 8q at a round start stay < 16q; one
+// conditional subtraction of 8q per value at each round start restores the invariant.
+template <int LOGN, int R, bool LAZY>
+__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw, u64 nq,
+                                           u64 q2, u64 q8) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
     if constexpr (R > 0) {
         constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
-        __syncthreads();
+        lds_barrier();
         lds_store<PLO>(lds, x, tid);
-        __syncthreads();
+        lds_barrier();
         lds_load<LO>(lds, x, tid);
+        if constexpr (LAZY) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = x[k] >= q8 ? x[k] - q8 : x[k];
+        }
     }
-    fwd_round<LOGN, LO, BHI, LO>(x, tid, tw, q, q2);
-    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1>(x, lds, tid, tw, q, q2);
+    fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tid, tw, nq, q2);
+    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY>(x, lds, tid, tw, nq, q2, q8);
 }
 
-template <int LOGN>
+template <int LOGN, bool LAZY>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
@@ -102,12 +115,17 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
 
-    fwd_rounds<LOGN, 0>(x, lds, tid, P.tw_fwd, q, q2);
+    const u64 q8 = 8 * q;
+    fwd_rounds<LOGN, 0, LAZY>(x, lds, tid, P.tw_fwd, (u64)0 - q, q2, q8);
 
-    // final layout: element 16*tid + k; reduce [0,4q) -> [0,q)
+    // final layout: element 16*tid + k; reduce [0,16q) (LAZY) or [0,4q) -> [0,q)
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         u64 v = x[k];
+        if (LAZY) {
+            v = v >= q8 ? v - q8 : v;
+            v = v >= 4 * q ? v - 4 * q : v;
+        }
         v = v >= q2 ? v - q2 : v;
         x[k] = v >= q ? v - q : v;
     }
@@ -164,9 +182,9 @@ __device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, cons
     constexpr int BHI = (4 * R + 3) < (LOGN - 1) ? 4 * R + 3 : LOGN - 1;
     if constexpr (R > 0) {
         constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
-        __syncthreads();
+        lds_barrier();
         lds_store<PLO>(lds, x, tid);
-        __syncthreads();
+        lds_barrier();
         lds_load<LO>(lds, x, tid);
     }
     inv_round<LOGN, LO, BLO, BHI>(x, tid, tw, P);
@@ -207,30 +225,32 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // ---------------------------------------------------------------- launchers
 
 template <int LOGN>
-static void launch_one(const NttBatch& nb, int count, bool inverse, const PrimeConst* primes,
+static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, const PrimeConst* primes,
                        hipStream_t s) {
     constexpr int threads = (1 << LOGN) / 16;
     if (inverse)
         hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, dim3(count), dim3(threads), 0, s, nb, primes);
+    else if (lazy)
+        hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
     else
-        hipLaunchKernelGGL(ntt_fwd_kernel<LOGN>, dim3(count), dim3(threads), 0, s, nb, primes);
+        hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
 }
 
-void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, const PrimeConst* primes,
+void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
                 hipStream_t s) {
     if (count <= 0) return;
     switch (logn) {
-        case 4: launch_one<4>(nb, count, inverse, primes, s); break;
-        case 5: launch_one<5>(nb, count, inverse, primes, s); break;
-        case 6: launch_one<6>(nb, count, inverse, primes, s); break;
-        case 7: launch_one<7>(nb, count, inverse, primes, s); break;
-        case 8: launch_one<8>(nb, count, inverse, primes, s); break;
-        case 9: launch_one<9>(nb, count, inverse, primes, s); break;
-        case 10: launch_one<10>(nb, count, inverse, primes, s); break;
-        case 11: launch_one<11>(nb, count, inverse, primes, s); break;
-        case 12: launch_one<12>(nb, count, inverse, primes, s); break;
-        case 13: launch_one<13>(nb, count, inverse, primes, s); break;
-        case 14: launch_one<14>(nb, count, inverse, primes, s); break;
+        case 4: launch_one<4>(nb, count, inverse, lazy, primes, s); break;
+        case 5: launch_one<5>(nb, count, inverse, lazy, primes, s); break;
+        case 6: launch_one<6>(nb, count, inverse, lazy, primes, s); break;
+        case 7: launch_one<7>(nb, count, inverse, lazy, primes, s); break;
+        case 8: launch_one<8>(nb, count, inverse, lazy, primes, s); break;
+        case 9: launch_one<9>(nb, count, inverse, lazy, primes, s); break;
+        case 10: launch_one<10>(nb, count, inverse, lazy, primes, s); break;
+        case 11: launch_one<11>(nb, count, inverse, lazy, primes, s); break;
+        case 12: launch_one<12>(nb, count, inverse, lazy, primes, s); break;
+        case 13: launch_one<13>(nb, count, inverse, lazy, primes, s); break;
+        case 14: launch_one<14>(nb, count, inverse, lazy, primes, s); break;
         default: break;  // rejected at context creation
     }
 }

@@ -88,7 +88,8 @@ int exacto_ctx_create(exacto_ctx** out, size_t ring_degree, const uint64_t* ct_m
                       uint64_t plain_modulus, uint64_t gadget_base, int device);
 void exacto_ctx_destroy(exacto_ctx* ctx);
 int exacto_ctx_get_info(const exacto_ctx* ctx, exacto_ctx_info* info);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+/* Enqueue on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream), used as
+ * given: NULL is the device's default stream.  A new context starts on a stream of its own. */
 int exacto_ctx_set_stream(exacto_ctx* ctx, void* hip_stream);
 /* Products per pipeline chunk (workspace = chunk * ~3 MB at n=4096, L=3). 0 = default. */
 int exacto_ctx_set_chunk(exacto_ctx* ctx, size_t products_per_chunk);

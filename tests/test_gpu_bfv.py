@@ -185,3 +185,10 @@ def test_decrypt_level(gpu_available, which):
         assert np.array_equal(got, ct_to_np(obfv.bfv_mul_and_relin(c1, c2, rlk)))
         dec = obfv.decrypt(np_to_ct(got, prm), sk)
         assert obfv.decode_scalar(dec) == (a * b) % prm.plain_modulus
+
+
+def test_exact_path_with_62bit_primes(gpu_available):
+    """Primes >= 2^60 take the non-lazy forward NTT; results must not change."""
+    prm = (P.BfvParamsBuilder().ring_degree(64).plain_modulus(65537)
+           .ct_moduli([4611686018427322369, 2305843009213554689]).build())
+    run_case(prm, 2, 91)

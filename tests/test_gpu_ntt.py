@@ -23,7 +23,9 @@ def oracle_fwd(coeffs, n, q):
 @pytest.mark.parametrize("n,q", [(16, 65537), (32, 65537), (64, 65537), (256, 65537),
                                  (1024, 1099509805057), (1024, 562949953443841),
                                  (2048, CFG2_Q), (4096, CFG2_Q), (8192, CFG2_Q),
-                                 (16384, 1152921504606748673), (4096, 1152921504606748673)])
+                                 (16384, 1152921504606748673), (4096, 1152921504606748673),
+                                 (4096, 2305843009213554689), (4096, 4611686018427322369),
+                                 (1024, 4611686018427322369)])
 def test_ntt_fwd_matches_oracle(gpu_available, n, q):
     rng = np.random.default_rng(n + q % 1000)
     ctx = HipContext(n, [q], plain_modulus=257)
