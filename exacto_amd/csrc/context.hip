@@ -331,7 +331,20 @@ static int build_tables(exacto_ctx* c) {
                 if (k < K) pref = mulmod_h(pref, pv[k] % qv[i], qv[i]);
             }
         }
-        for (int a = 0; a < K; ++a) set_shoup(C.qinvp_w[a], C.qinvp_ws[a], invmod_h(Q.mod(pv[a]), pv[a]), pv[a]);
+        for (int a = 0; a < K; ++a) {
+            const u64 pa = pv[a];
+            const u64 qinv = invmod_h(Q.mod(pa), pa);
+            set_shoup(C.qinvp_w[a], C.qinvp_ws[a], qinv, pa);
+            set_shoup(C.pq_w[a], C.pq_ws[a], mulmod_h(c->plain % pa, qinv, pa), pa);
+            for (int k = 0; k <= L; ++k)
+                set_shoup(C.qpq_w[k][a], C.qpq_ws[k][a], mulmod_h(C.qpref_w[k][L + a], qinv, pa), pa);
+        }
+    }
+    {
+        const u64 mx = *std::max_element(c->primes.begin(), c->primes.end());
+        const u64 mn = *std::min_element(c->primes.begin(), c->primes.end());
+        C.near = (u128)mx < 2 * (u128)mn;
+        C.digit_small = c->gbase <= *std::min_element(qv.begin(), qv.end());
     }
     HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
     HIP_TRY(hipMalloc((void**)&c->d_crt, sizeof(CrtTables)));
@@ -621,7 +634,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_extend(c->ws_coefQ, c->ws_extP, cnt, n, c->d_primes, K, c->stream);
         else
-            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->stream);
+            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.near != 0,
+                              c->stream);
         CHECK_LAUNCH();
         // 3. forward NTT of the extended polynomials
         if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
@@ -637,7 +651,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
-            launch_exact_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, L, K, c->stream);
+            launch_exact_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, L, K,
+                               c->h_crt.near != 0, c->stream);
         CHECK_LAUNCH();
         // 7. forward NTT of the results (and digits)
         NttBatch rb{};

@@ -46,6 +46,11 @@ struct CrtTables {
     u64 ppref_w[EXACTO_MAX_K + 1][EXACTO_MAX_L];
     u64 ppref_ws[EXACTO_MAX_K + 1][EXACTO_MAX_L];
     u64 qinvp_w[EXACTO_MAX_K], qinvp_ws[EXACTO_MAX_K];   // Q^-1 mod p_j
+    // folded scale constants: pq[t] = p * Q^-1 mod p_t (aux t), qpq[k][a] = qpref[k][L+a] * Q^-1 mod p_a
+    u64 pq_w[EXACTO_MAX_K], pq_ws[EXACTO_MAX_K];
+    u64 qpq_w[EXACTO_MAX_L + 1][EXACTO_MAX_K], qpq_ws[EXACTO_MAX_L + 1][EXACTO_MAX_K];
+    int near;       // max prime < 2 * min prime: residues move between primes by one conditional subtraction
+    int digit_small;  // gadget base <= every ciphertext prime: digit magnitudes are already reduced
     u64 pmod_w[EXACTO_MAX_PRIMES], pmod_ws[EXACTO_MAX_PRIMES];  // plain mod prime_t
     u64 Qwords[EXACTO_MAX_L];                   // Q as little-endian 64-bit words
     // HPS (single q, 1 or 2 aux primes), eval.rs:257-413
@@ -68,14 +73,14 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 };
 
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
-                       const PrimeConst* primes, int L, int K, hipStream_t s);
+                       const PrimeConst* primes, int L, int K, bool near, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
 void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
                    const PrimeConst* primes, hipStream_t s);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, hipStream_t s);
+                        int K, bool near, hipStream_t s);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);

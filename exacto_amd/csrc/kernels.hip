@@ -28,7 +28,16 @@ static inline int blocks_per_row(int n) { return (n + TPB - 1) / TPB; }
 
 // ---------------------------------------------------------------- mixed radix helpers
 
+// A residue of one prime moved to another: with NEAR (max prime < 2 * min prime) a value
+// below any prime needs one conditional subtraction, otherwise a full reduce64.
+template <bool NEAR>
+__device__ __forceinline__ u64 xfer(u64 v, u64 q, u64 mu) {
+    if (NEAR) return v >= q ? v - q : v;
+    return reduce64(v, q, mu);
+}
+
 // Garner: residues x[i] mod q_i (i < L) -> mixed-radix digits v (x = v0 + v1 q0 + v2 q0 q1 + ...).
+template <bool NEAR>
 __device__ __forceinline__ void garner_q(u64 (&v)[EXACTO_MAX_L], const u64 (&x)[EXACTO_MAX_L], int L,
                                          const CrtTables* __restrict__ C,
                                          const PrimeConst* __restrict__ primes) {
@@ -40,7 +49,7 @@ __device__ __forceinline__ void garner_q(u64 (&v)[EXACTO_MAX_L], const u64 (&x)[
 #pragma unroll
             for (int k = 0; k < EXACTO_MAX_L; ++k) {
                 if (k < i) {
-                    t = sub_mod(t, reduce64(v[k], qi, mui), qi);
+                    t = sub_mod(t, xfer<NEAR>(v[k], qi, mui), qi);
                     t = shoup_mul_red(t, C->gq_w[i][k], C->gq_ws[i][k], qi);
                 }
             }
@@ -64,7 +73,7 @@ __device__ __forceinline__ bool mr_greater(const u64 (&v)[MAXN], const u64* h, i
 }
 
 // sum_k (v_k mod prime_t) * pref[k][t]  -  neg * pref[cnt][t]   (mod prime_t)
-template <int MAXN, int STRIDE>
+template <int MAXN, int STRIDE, bool NEAR>
 __device__ __forceinline__ u64 mr_eval(const u64 (&v)[MAXN], int cnt, bool neg, const u64* pw,
                                        const u64* pws, int t, const PrimeConst& P) {
     const u64 q = P.q, mu = P.mu64;
@@ -72,7 +81,7 @@ __device__ __forceinline__ u64 mr_eval(const u64 (&v)[MAXN], int cnt, bool neg, 
 #pragma unroll
     for (int k = 0; k < MAXN; ++k) {
         if (k < cnt) {
-            const u64 vk = reduce64(v[k], q, mu);
+            const u64 vk = xfer<NEAR>(v[k], q, mu);
             acc = add_mod(acc, shoup_mul_red(vk, pw[k * STRIDE + t], pws[k * STRIDE + t], q), q);
         }
     }
@@ -84,10 +93,11 @@ __device__ __forceinline__ u64 mr_eval(const u64 (&v)[MAXN], int cnt, bool neg, 
 // keyswitch.rs:24-44 literally (truncating %, [-B/2, B/2) adjustment, final carry dropped),
 // on the exact value (extension semantics for Q >= 2^64; identical to rns.rs:114-151 below).
 // Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j).
+template <bool NEAR>
 __device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTables* __restrict__ C,
                               const PrimeConst* __restrict__ primes, u64* D, int n, int guse) {
     u64 z[EXACTO_MAX_L];
-    garner_q(z, res, L, C, primes);
+    garner_q<NEAR>(z, res, L, C, primes);
     const bool neg = mr_greater<EXACTO_MAX_L>(z, C->halfQ_mr, L);
     // multiword value via Horner on the mixed-radix digits
     u64 M[EXACTO_MAX_L];
@@ -174,12 +184,13 @@ __device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTa
                 }
             }
         }
-        // digit residue (rem mod Q) mod q_i == rem mod q_i
+        // digit residue (rem mod Q) mod q_i == rem mod q_i; |rem| < B <= q_i when digit_small
+        const bool small = C->digit_small != 0;
 #pragma unroll
         for (int i = 0; i < EXACTO_MAX_L; ++i) {
             if (i < L) {
                 const u64 qi = primes[i].q;
-                u64 m = reduce64(mag, qi, primes[i].mu64);
+                u64 m = small ? mag : reduce64(mag, qi, primes[i].mu64);
                 if (dneg && m != 0) m = qi - m;
                 D[((long)g * L + i) * n] = m;
             }
@@ -189,6 +200,7 @@ __device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTa
 
 // ---------------------------------------------------------------- exact lift Q -> P
 
+template <bool NEAR>
 __global__ void __launch_bounds__(TPB)
 exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L, int K,
                   const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
@@ -197,22 +209,23 @@ exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L) x[i] = coefQ[(row * L + i) * n + j];
-    garner_q(v, x, L, C, primes);
+    garner_q<NEAR>(v, x, L, C, primes);
     const bool neg = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
     for (int a = 0; a < K; ++a) {
         const int t = L + a;
-        extP[(row * K + a) * n + j] =
-            mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, neg, &C->qpref_w[0][0], &C->qpref_ws[0][0],
-                                                     t, primes[t]);
+        extP[(row * K + a) * n + j] = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, NEAR>(
+            v, L, neg, &C->qpref_w[0][0], &C->qpref_ws[0][0], t, primes[t]);
     }
 }
 
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
-                       const PrimeConst* primes, int L, int K, hipStream_t s) {
+                       const PrimeConst* primes, int L, int K, bool near, hipStream_t s) {
     const long blocks = (long)items * 4 * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(exact_lift_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct,
-                       primes);
+    if (near)
+        hipLaunchKernelGGL(exact_lift_kernel<true>, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, primes);
+    else
+        hipLaunchKernelGGL(exact_lift_kernel<false>, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, primes);
 }
 
 // ---------------------------------------------------------------- HPS extension
@@ -283,6 +296,7 @@ void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n
 
 // ---------------------------------------------------------------- exact scale-and-round
 
+template <bool NEAR>
 __global__ void __launch_bounds__(TPB)
 exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
                    u64* __restrict__ D, int guse, int n, int L, int K,
@@ -292,41 +306,36 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
     const long item = row / 3;
     const int comp = (int)(row - item * 3);
     const u64* Tin = T + row * NP * n + j;
-    // u = p * T in every prime
+    // u = p * T mod q_i; s = [u]_Q centred, as mixed-radix digits v + sign
     u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L) u[i] = shoup_mul_red(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
-    // s = [u]_Q centred, via mixed radix
-    garner_q(v, u, L, C, primes);
+    garner_q<NEAR>(v, u, L, C, primes);
     const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
-    // r = (u - s) / Q in every auxiliary prime
-    u64 r[EXACTO_MAX_K], w[EXACTO_MAX_K];
-#pragma unroll
-    for (int a = 0; a < EXACTO_MAX_K; ++a) {
-        if (a < K) {
-            const int t = L + a;
-            const PrimeConst& P = primes[t];
-            const u64 ut = shoup_mul_red(Tin[(long)t * n], C->pmod_w[t], C->pmod_ws[t], P.q);
-            const u64 st = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, negs, &C->qpref_w[0][0],
-                                                                    &C->qpref_ws[0][0], t, P);
-            r[a] = shoup_mul_red(sub_mod(ut, st, P.q), C->qinvp_w[a], C->qinvp_ws[a], P.q);
-        }
-    }
-    // Garner over P, centre, evaluate mod each q_i
+    // r = (p*T - s) / Q in every auxiliary prime, with Q^-1 folded into the constants:
+    // r = T*(p Q^-1) - sum_k v_k*(qpref_k Q^-1) + negs   (Q * Q^-1 == 1)
+    u64 w[EXACTO_MAX_K];
 #pragma unroll
     for (int a = 0; a < EXACTO_MAX_K; ++a) {
         if (a < K) {
             const PrimeConst& P = primes[L + a];
-            u64 t = r[a];
+            const u64 pa = P.q;
+            u64 acc = shoup_mul_red(Tin[(long)(L + a) * n], C->pq_w[a], C->pq_ws[a], pa);
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_L; ++k)
+                if (k < L)
+                    acc = sub_mod(acc, shoup_mul_red(xfer<NEAR>(v[k], pa, P.mu64), C->qpq_w[k][a], C->qpq_ws[k][a], pa), pa);
+            if (negs) acc = add_mod(acc, 1, pa);
+            // Garner over P on the fly (w_a depends on w_0..w_{a-1})
 #pragma unroll
             for (int k = 0; k < EXACTO_MAX_K; ++k) {
                 if (k < a) {
-                    t = sub_mod(t, reduce64(w[k], P.q, P.mu64), P.q);
-                    t = shoup_mul_red(t, C->gp_w[a][k], C->gp_ws[a][k], P.q);
+                    acc = sub_mod(acc, xfer<NEAR>(w[k], pa, P.mu64), pa);
+                    acc = shoup_mul_red(acc, C->gp_w[a][k], C->gp_ws[a][k], pa);
                 }
             }
-            w[a] = t;
+            w[a] = acc;
         }
     }
     const bool negr = mr_greater<EXACTO_MAX_K>(w, C->halfP_mr, K);
@@ -334,8 +343,8 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L)
-            res[i] = mr_eval<EXACTO_MAX_K, EXACTO_MAX_L>(w, K, negr, &C->ppref_w[0][0],
-                                                         &C->ppref_ws[0][0], i, primes[i]);
+            res[i] = mr_eval<EXACTO_MAX_K, EXACTO_MAX_L, NEAR>(w, K, negr, &C->ppref_w[0][0],
+                                                               &C->ppref_ws[0][0], i, primes[i]);
     if (comp < ncomp_r) {
         u64* out = R + item * r_stride + (long)comp * L * n + j;
 #pragma unroll
@@ -343,16 +352,20 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
             if (i < L) out[(long)i * n] = res[i];
     }
     if (comp == 2 && D != nullptr)
-        gadget_digits(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
+        gadget_digits<NEAR>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
 }
 
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, hipStream_t s) {
+                        int K, bool near, hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(exact_scale_kernel, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
-                       guse, n, L, K, ct, primes);
+    if (near)
+        hipLaunchKernelGGL(exact_scale_kernel<true>, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
+                           guse, n, L, K, ct, primes);
+    else
+        hipLaunchKernelGGL(exact_scale_kernel<false>, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
+                           guse, n, L, K, ct, primes);
 }
 
 // ---------------------------------------------------------------- literal HPS scale
@@ -419,7 +432,7 @@ hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, 
     if (comp == 2 && D != nullptr) {
         u64 res[EXACTO_MAX_L];
         res[0] = result;
-        gadget_digits(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
+        gadget_digits<false>(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
     }
 }
 
@@ -442,7 +455,7 @@ decompose_kernel(const u64* __restrict__ C2, long c2_stride, u64* __restrict__ D
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L) res[i] = C2[row * c2_stride + (long)i * n + j];
-    gadget_digits(res, L, C, primes, D + row * (long)guse * L * n + j, n, guse);
+    gadget_digits<false>(res, L, C, primes, D + row * (long)guse * L * n + j, n, guse);
 }
 
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,

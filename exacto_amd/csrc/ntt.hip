@@ -44,20 +44,32 @@ __device__ __forceinline__ void lds_load(const u64* lds, u64 (&x)[16], int tid) 
 
 // ---------------------------------------------------------------- forward
 
-// Butterflies for stage bits BHI..BLO (descending) inside window [LO, LO+4).
-template <int LOGN, int LO, int BHI, int BLO, bool LAZY>
-__device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* __restrict__ tw,
-                                          u64 nq, u64 q2) {
+// Twiddles of one round: stage bit b uses (8 >> (b - LO)) groups; at most 1+2+4+8 = 15 pairs.
+// Index of group g at bit b: (N >> (b+1)) + (thigh << (LO+3-b)) + g.
+template <int LOGN, int LO, int BHI, int BLO>
+__device__ __forceinline__ void load_round_tw(TwPair (&tw)[15], int tid, const TwPair* __restrict__ tab) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+    int slot = 0;
+#pragma unroll
+    for (int b = BHI; b >= BLO; --b) {
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = tab[base + g];
+    }
+}
+
+// Butterflies for stage bits BHI..BLO (descending) inside window [LO, LO+4).
+template <int LOGN, int LO, int BHI, int BLO, bool LAZY>
+__device__ __forceinline__ void fwd_round(u64 (&x)[16], const TwPair (&tw)[15], u64 nq, u64 q2) {
+    int slot = 0;
 #pragma unroll
     for (int b = BHI; b >= BLO; --b) {
         const int lb = b - LO;
         const int half = 1 << lb;
-        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
         for (int g = 0; g < (8 >> lb); ++g) {
-            const TwPair t = tw[base + g];
+            const TwPair t = tw[slot++];
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m;
@@ -76,10 +88,12 @@ __device__ __forceinline__ void fwd_round(u64 (&x)[16], int tid, const TwPair* _
 // adds < 2q per stage to the bound, so values < 8q at a round start stay < 16q; one
 // conditional subtraction of 8q per value at each round start restores the invariant.
 template <int LOGN, int R, bool LAZY>
-__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw, u64 nq,
+__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tab, u64 nq,
                                            u64 q2, u64 q8) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
+    TwPair tw[15];
+    load_round_tw<LOGN, LO, BHI, LO>(tw, tid, tab);  // in flight across the exchange below
     if constexpr (R > 0) {
         constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
         lds_barrier();
@@ -91,8 +105,8 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, cons
             for (int k = 0; k < 16; ++k) x[k] = x[k] >= q8 ? x[k] - q8 : x[k];
         }
     }
-    fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tid, tw, nq, q2);
-    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY>(x, lds, tid, tw, nq, q2, q8);
+    fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tw, nq, q2);
+    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY>(x, lds, tid, tab, nq, q2, q8);
 }
 
 template <int LOGN, bool LAZY>
@@ -137,29 +151,42 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // ---------------------------------------------------------------- inverse
 
 template <int LOGN, int LO, int BLO, int BHI>
-__device__ __forceinline__ void inv_round(u64 (&x)[16], int tid, const TwPair* __restrict__ tw,
-                                          const PrimeConst& P) {
+__device__ __forceinline__ void load_round_tw_inv(TwPair (&tw)[15], int tid, const TwPair* __restrict__ tab) {
     constexpr int N = 1 << LOGN;
-    const u64 q = P.q, q2 = P.two_q;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+    int slot = 0;
+#pragma unroll
+    for (int b = BLO; b <= BHI; ++b) {
+        if (b == LOGN - 1) continue;  // last stage uses the n^-1-folded constants
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = tab[base + g];
+    }
+}
+
+template <int LOGN, int LO, int BLO, int BHI>
+__device__ __forceinline__ void inv_round(u64 (&x)[16], const TwPair (&tw)[15], const PrimeConst& P) {
+    const u64 q = P.q, q2 = P.two_q, nq = (u64)0 - q;
+    int slot = 0;
 #pragma unroll
     for (int b = BLO; b <= BHI; ++b) {
         const int lb = b - LO;
         const int half = 1 << lb;
-        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
         if (b == LOGN - 1) {
             // last stage: (U+V) * n^-1, (U-V) * psi_inv_rev[1] * n^-1, fully reduced
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = m, k1 = m + half;
                 const u64 U = x[k0], V = x[k1];
-                x[k0] = shoup_mul_red(U + V, P.n_inv, P.n_inv_s, q);
-                x[k1] = shoup_mul_red(U - V + q2, P.last_w, P.last_ws, q);
+                u64 a = shoup_mul_nq(U + V, P.n_inv, P.n_inv_s, nq);
+                u64 c = shoup_mul_nq(U - V + q2, P.last_w, P.last_ws, nq);
+                x[k0] = a >= q ? a - q : a;
+                x[k1] = c >= q ? c - q : c;
             }
         } else {
 #pragma unroll
             for (int g = 0; g < (8 >> lb); ++g) {
-                const TwPair t = tw[base + g];
+                const TwPair t = tw[slot++];
 #pragma unroll
                 for (int m = 0; m < half; ++m) {
                     const int k0 = g * 2 * half + m;
@@ -167,7 +194,7 @@ __device__ __forceinline__ void inv_round(u64 (&x)[16], int tid, const TwPair* _
                     const u64 U = x[k0], V = x[k1];
                     u64 s = U + V;
                     x[k0] = s >= q2 ? s - q2 : s;
-                    x[k1] = shoup_mul(U - V + q2, t.w, t.ws, q);
+                    x[k1] = shoup_mul_nq(U - V + q2, t.w, t.ws, nq);
                 }
             }
         }
@@ -175,11 +202,13 @@ __device__ __forceinline__ void inv_round(u64 (&x)[16], int tid, const TwPair* _
 }
 
 template <int LOGN, int R>
-__device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tw,
+__device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tab,
                                            const PrimeConst& P) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
     constexpr int BHI = (4 * R + 3) < (LOGN - 1) ? 4 * R + 3 : LOGN - 1;
+    TwPair tw[15];
+    load_round_tw_inv<LOGN, LO, BLO, BHI>(tw, tid, tab);
     if constexpr (R > 0) {
         constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
         lds_barrier();
@@ -187,8 +216,8 @@ __device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, cons
         lds_barrier();
         lds_load<LO>(lds, x, tid);
     }
-    inv_round<LOGN, LO, BLO, BHI>(x, tid, tw, P);
-    if constexpr (BHI < LOGN - 1) inv_rounds<LOGN, R + 1>(x, lds, tid, tw, P);
+    inv_round<LOGN, LO, BLO, BHI>(x, tw, P);
+    if constexpr (BHI < LOGN - 1) inv_rounds<LOGN, R + 1>(x, lds, tid, tab, P);
 }
 
 template <int LOGN>
