@@ -6,6 +6,7 @@
 // workspace.  Every `_dev` entry point only enqueues kernels on the context stream.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <string>
@@ -181,7 +182,10 @@ struct exacto_ctx {
     CrtTables h_crt{};
     u64* d_scal = nullptr;
     u64* d_rlk = nullptr;
-    size_t rlk_keys = 0, rlk_cap = 0;
+    u64* d_rlk_s = nullptr;  // Shoup companions of the key (fused key switching)
+    size_t rlk_keys = 0, rlk_cap = 0, rlk_s_cap = 0;
+    bool rlk_s_valid = false;
+    bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 128;
@@ -461,6 +465,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
     c->own_stream = true;
+    if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
@@ -471,7 +476,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
-    free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk);
+    free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -525,6 +530,7 @@ extern "C" uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* c, size_t num_keys)
     if (grow(&c->d_rlk, &c->rlk_cap, std::max<size_t>(bytes, 8))) return nullptr;
     c->rlk_keys = num_keys;
     c->rlk_loaded = true;
+    c->rlk_s_valid = false;  // contents change: companions recomputed before first use
     return c->d_rlk;
 }
 
@@ -603,6 +609,22 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     return 0;
 }
 
+static int ensure_rlk_companions(exacto_ctx* c) {
+    if (c->rlk_s_valid) return 0;
+    const size_t count = c->rlk_keys * 2 * c->L * (size_t)c->n;
+    if (grow(&c->d_rlk_s, &c->rlk_s_cap, std::max<size_t>(count * sizeof(u64), 8))) return EXACTO_ERR_HIP;
+    launch_shoup_companions(c->d_rlk, c->d_rlk_s, (long)count, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    c->rlk_s_valid = true;
+    return 0;
+}
+
+static bool lazy_ok(const exacto_ctx* c, int base, int period) {
+    bool lazy = true;
+    for (int t = base; t < base + period; ++t) lazy &= c->primes[t] < (1ull << 60);
+    return lazy;
+}
+
 // ============================================================== multiplication pipeline
 
 // products [0, P): ct1 = op.a + off_a(p), ct2 = op.b + off_b(p) (each [2][L][n], NTT domain).
@@ -659,6 +681,17 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         rb.src = R; rb.src_off = nullptr; rb.src_item_stride = out_stride;
         rb.dst = R; rb.dst_item_stride = out_stride;
         rb.ppi = ncomp * L; rb.prime_base = 0; rb.period = L;
+        if (relin && guse > 0 && c->fused_ks) {
+            // 7+8 fused: NTT(r0, r1) + sum_g NTT(d_g) (.) rlk_g, one launch, digits never stored in NTT form
+            if (int e = ensure_rlk_companions(c)) return e;
+            KsArgs ka{};
+            ka.R = R; ka.r_off = nullptr; ka.r_stride = out_stride; ka.r_ntt = 0; ka.L = L;
+            ka.D = c->ws_D; ka.guse = guse; ka.rlk = c->d_rlk; ka.rlk_s = c->d_rlk_s;
+            ka.out = R; ka.out_stride = out_stride;
+            launch_keyswitch(ka, cnt, c->logn, lazy_ok(c, 0, L), c->d_primes, c->stream);
+            CHECK_LAUNCH();
+            continue;
+        }
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
         if (relin && guse > 0) {
             if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false)) return e;

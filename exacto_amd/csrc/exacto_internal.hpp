@@ -62,6 +62,24 @@ struct CrtTables {
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
                 hipStream_t s);
 
+// Fused relinearisation: see keyswitch_kernel in ntt.hip.
+struct KsArgs {
+    const u64* R;        // c0', c1' sources: [2][L][n] per item (coefficient or NTT domain)
+    const u64* r_off;    // per-item element offsets or nullptr -> item * r_stride
+    long r_stride;
+    int r_ntt;           // R already in the NTT domain
+    int L;
+    const u64* D;        // gadget digits, coefficient domain, [guse][L][n] per item (contiguous)
+    int guse;
+    const u64* rlk;      // [keys][2][L][n]
+    const u64* rlk_s;    // Shoup companions of rlk
+    u64* out;            // [2][L][n] per item (may alias R)
+    long out_stride;
+};
+void launch_keyswitch(const KsArgs& a, int items, int logn, bool lazy, const PrimeConst* primes, hipStream_t s);
+void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
+                             hipStream_t s);
+
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item
     const u64* a;

@@ -87,13 +87,42 @@ __device__ __forceinline__ void fwd_round(u64 (&x)[16], const TwPair (&tw)[15], 
 // LAZY (all q < 2^60, so 16q <= 2^64): no per-butterfly reduction.  A round of <= 4 stages
 // adds < 2q per stage to the bound, so values < 8q at a round start stay < 16q; one
 // conditional subtraction of 8q per value at each round start restores the invariant.
-template <int LOGN, int R, bool LAZY>
+// Butterflies of one round with each twiddle loaded right before its group (low register
+// pressure; used where the accumulators of the fused key switch need the VGPRs).
+template <int LOGN, int LO, int BHI, int BLO, bool LAZY>
+__device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, const TwPair* __restrict__ tab,
+                                                 u64 nq, u64 q2) {
+    constexpr int N = 1 << LOGN;
+    const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+#pragma unroll
+    for (int b = BHI; b >= BLO; --b) {
+        const int lb = b - LO;
+        const int half = 1 << lb;
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> lb); ++g) {
+            const TwPair t = tab[base + g];
+#pragma unroll
+            for (int m = 0; m < half; ++m) {
+                const int k0 = g * 2 * half + m;
+                const int k1 = k0 + half;
+                u64 X = x[k0];
+                if (!LAZY) X = X >= q2 ? X - q2 : X;
+                const u64 T = shoup_mul_nq(x[k1], t.w, t.ws, nq);
+                x[k0] = X + T;
+                x[k1] = X - T + q2;
+            }
+        }
+    }
+}
+
+template <int LOGN, int R, bool LAZY, bool PRELOAD = true>
 __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tab, u64 nq,
                                            u64 q2, u64 q8) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
     TwPair tw[15];
-    load_round_tw<LOGN, LO, BHI, LO>(tw, tid, tab);  // in flight across the exchange below
+    if constexpr (PRELOAD) load_round_tw<LOGN, LO, BHI, LO>(tw, tid, tab);  // in flight across the exchange
     if constexpr (R > 0) {
         constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
         lds_barrier();
@@ -105,8 +134,9 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, cons
             for (int k = 0; k < 16; ++k) x[k] = x[k] >= q8 ? x[k] - q8 : x[k];
         }
     }
-    fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tw, nq, q2);
-    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY>(x, lds, tid, tab, nq, q2, q8);
+    if constexpr (PRELOAD) fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tw, nq, q2);
+    else fwd_round_direct<LOGN, LO, BHI, LO, LAZY>(x, tid, tab, nq, q2);
+    if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY, PRELOAD>(x, lds, tid, tab, nq, q2, q8);
 }
 
 template <int LOGN, bool LAZY>
@@ -251,6 +281,113 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
+// ---------------------------------------------------------------- fused key switching
+
+// One workgroup per (product, limb i) of relinearize (keyswitch.rs:86-95):
+//   out_c[i] = NTT(R_c[i]) + sum_{g < guse} NTT(D_g[i]) (.) rlk_g,c[i]     (c = 0, 1)
+// The G forward transforms of the gadget digits never leave the chip: each digit is
+// transformed in registers/LDS and immediately multiply-accumulated (Shoup, with the
+// key's precomputed companions) into two register accumulators kept in [0, 2q).
+// R_c may already be in the NTT domain (r_ntt = 1, standalone relinearize).
+template <int LOGN, bool LAZY>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16, 3)
+keyswitch_kernel(KsArgs a, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int L = a.L;
+    const long item = blockIdx.x / L;
+    const int i = (int)(blockIdx.x - item * L);
+    const PrimeConst& P = primes[i];
+    const u64 q = P.q, q2 = P.two_q, q8 = 8 * q, nq = (u64)0 - q;
+    const long Ln = (long)L * N;
+
+    auto ntt_canon = [&](u64 (&x)[16]) {
+        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, P.tw_fwd, nq, q2, q8);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            u64 v = x[k];
+            if (LAZY) {
+                v = v >= q8 ? v - q8 : v;
+                v = v >= 4 * q ? v - 4 * q : v;
+            }
+            v = v >= q2 ? v - q2 : v;
+            x[k] = v >= q ? v - q : v;
+        }
+    };
+    auto load_coeff = [&](u64 (&x)[16], const u64* src) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+    };
+    auto load_ntt = [&](u64 (&x)[16], const u64* src) {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 v = s2[k];
+            x[2 * k] = v.x;
+            x[2 * k + 1] = v.y;
+        }
+    };
+
+    const u64* rbase = a.R + (a.r_off ? (long)a.r_off[item] : item * a.r_stride);
+    u64 acc0[16], acc1[16];
+    if (a.r_ntt) {
+        load_ntt(acc0, rbase + (long)i * N);
+        load_ntt(acc1, rbase + Ln + (long)i * N);
+    } else {
+        load_coeff(acc0, rbase + (long)i * N);
+        ntt_canon(acc0);
+        load_coeff(acc1, rbase + Ln + (long)i * N);
+        ntt_canon(acc1);
+    }
+    const u64* dbase = a.D + item * (long)a.guse * Ln + (long)i * N;
+    for (int g = 0; g < a.guse; ++g) {
+        u64 x[16];
+        load_coeff(x, dbase + g * Ln);
+        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, P.tw_fwd, nq, q2, q8);  // any value < 2^64 is a valid Shoup input
+        const long ko = ((long)(2 * g) * L + i) * N + 16 * tid;
+        const ulonglong2* k0 = reinterpret_cast<const ulonglong2*>(a.rlk + ko);
+        const ulonglong2* k0s = reinterpret_cast<const ulonglong2*>(a.rlk_s + ko);
+        const ulonglong2* k1 = reinterpret_cast<const ulonglong2*>(a.rlk + ko + Ln);
+        const ulonglong2* k1s = reinterpret_cast<const ulonglong2*>(a.rlk_s + ko + Ln);
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            // keep at most two groups of key loads in flight (register pressure: the two
+            // accumulators already hold 64 VGPRs)
+            if (h % 2 == 0) asm volatile("" ::: "memory");
+            const ulonglong2 w0 = k0[h], w0s = k0s[h], w1 = k1[h], w1s = k1s[h];
+            u64 t;
+            t = acc0[2 * h] + shoup_mul_nq(x[2 * h], w0.x, w0s.x, nq);
+            acc0[2 * h] = t >= q2 ? t - q2 : t;
+            t = acc0[2 * h + 1] + shoup_mul_nq(x[2 * h + 1], w0.y, w0s.y, nq);
+            acc0[2 * h + 1] = t >= q2 ? t - q2 : t;
+            t = acc1[2 * h] + shoup_mul_nq(x[2 * h], w1.x, w1s.x, nq);
+            acc1[2 * h] = t >= q2 ? t - q2 : t;
+            t = acc1[2 * h + 1] + shoup_mul_nq(x[2 * h + 1], w1.y, w1s.y, nq);
+            acc1[2 * h + 1] = t >= q2 ? t - q2 : t;
+        }
+    }
+    u64* obase = a.out + item * a.out_stride + (long)i * N + 16 * tid;
+    ulonglong2* o0 = reinterpret_cast<ulonglong2*>(obase);
+    ulonglong2* o1 = reinterpret_cast<ulonglong2*>(obase + Ln);
+#pragma unroll
+    for (int h = 0; h < 8; ++h) {
+        u64 a0 = acc0[2 * h], a1 = acc0[2 * h + 1], b0 = acc1[2 * h], b1 = acc1[2 * h + 1];
+        o0[h] = make_ulonglong2(a0 >= q ? a0 - q : a0, a1 >= q ? a1 - q : a1);
+        o1[h] = make_ulonglong2(b0 >= q ? b0 - q : b0, b1 >= q ? b1 - q : b1);
+    }
+}
+
+// rlk_s = floor(rlk * 2^64 / q_limb) (Shoup companions of the resident key, computed once)
+__global__ void shoup_companion_kernel(const u64* __restrict__ w, u64* __restrict__ ws, long count, int n,
+                                       int L, const PrimeConst* __restrict__ primes) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= count) return;
+    const int limb = (int)((idx / n) % L);
+    ws[idx] = (u64)(((u128)w[idx] << 64) / primes[limb].q);
+}
+
 // ---------------------------------------------------------------- launchers
 
 template <int LOGN>
@@ -282,6 +419,41 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         case 14: launch_one<14>(nb, count, inverse, lazy, primes, s); break;
         default: break;  // rejected at context creation
     }
+}
+
+template <int LOGN>
+static void launch_ks(const KsArgs& a, int blocks, bool lazy, const PrimeConst* primes, hipStream_t s) {
+    constexpr int threads = (1 << LOGN) / 16;
+    if (lazy)
+        hipLaunchKernelGGL((keyswitch_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, a, primes);
+    else
+        hipLaunchKernelGGL((keyswitch_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, a, primes);
+}
+
+void launch_keyswitch(const KsArgs& a, int items, int logn, bool lazy, const PrimeConst* primes, hipStream_t s) {
+    const int blocks = items * a.L;
+    if (blocks <= 0) return;
+    switch (logn) {
+        case 4: launch_ks<4>(a, blocks, lazy, primes, s); break;
+        case 5: launch_ks<5>(a, blocks, lazy, primes, s); break;
+        case 6: launch_ks<6>(a, blocks, lazy, primes, s); break;
+        case 7: launch_ks<7>(a, blocks, lazy, primes, s); break;
+        case 8: launch_ks<8>(a, blocks, lazy, primes, s); break;
+        case 9: launch_ks<9>(a, blocks, lazy, primes, s); break;
+        case 10: launch_ks<10>(a, blocks, lazy, primes, s); break;
+        case 11: launch_ks<11>(a, blocks, lazy, primes, s); break;
+        case 12: launch_ks<12>(a, blocks, lazy, primes, s); break;
+        case 13: launch_ks<13>(a, blocks, lazy, primes, s); break;
+        case 14: launch_ks<14>(a, blocks, lazy, primes, s); break;
+        default: break;
+    }
+}
+
+void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
+                             hipStream_t s) {
+    if (count <= 0) return;
+    hipLaunchKernelGGL(shoup_companion_kernel, dim3((count + 255) / 256), dim3(256), 0, s, w, ws, count, n, L,
+                       primes);
 }
 
 }  // namespace exacto
