@@ -38,12 +38,17 @@ sys.path.insert(0, ROOT)
 from exacto_amd._ffi import HipContext  # noqa: E402
 
 Q3 = [1152921504606830593, 1152921504606748673, 1152921504606683137]
+Q4 = Q3 + [1152921504606601217]
 HBM_PEAK_GBS = 8000.0
 
+# name: (n, moduli, aux, BFV plain modulus, gadget base, dBFV (d, base, p) or None, chain depth)
 CONFIGS = {
-    # name: (n, moduli, aux, plain, gadget_base)
-    "cfg3": (4096, Q3, [], 65537, 1 << 16),
+    "cfg2": (4096, [1152921504606830593], [], 65537, 1 << 16, None, 0),   # NTT fwd + mul + inv
+    "cfg3": (4096, Q3, [], 65537, 1 << 16, None, 0),                      # bfv_mul_and_relin
+    "cfg4": (4096, Q3, [], 260111, 1 << 16, (2, 256, 65536), 1),          # dbfv_mul
+    "cfg5": (8192, Q4, [], 1040407, 256, (8, 256, 0), 4),                 # dbfv_mul chain depth 4
 }
+DEFAULT_BATCH = {"cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8}
 
 
 def parse():
@@ -51,7 +56,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="ciphertext pairs per GPU")
+    ap.add_argument("--batch", type=int, default=0, help="work items per GPU (0 = config default)")
     ap.add_argument("--chunk", type=int, default=0, help="products per pipeline chunk (0 = library default)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -112,9 +117,9 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    n, moduli, aux, plain, gbase = CONFIGS[args.config]
+    n, moduli, aux, plain, gbase, dbfv, depth = CONFIGS[args.config]
     L = len(moduli)
-    B = args.batch
+    B = args.batch or DEFAULT_BATCH[args.config]
     ctx = HipContext(n, moduli, aux, plain, gbase, device=local)
     stream = torch.cuda.current_stream(device)
     ctx.set_stream(stream.cuda_stream)
@@ -124,22 +129,57 @@ def main():
 
     gen = torch.Generator(device=device)
     gen.manual_seed(0xE7AC7003 + rank)
-    ct1 = uniform_dev((B, 2), moduli, n, gen, device)
-    ct2 = uniform_dev((B, 2), moduli, n, gen, device)
-    out = torch.empty_like(ct1)
-
-    # relinearisation key: made once on rank 0, RCCL-broadcast to every GPU
     kgen = torch.Generator(device=device)
     kgen.manual_seed(0xE7AC7003)
-    rlk = uniform_dev((G, 2), moduli, n, kgen, device) if rank == 0 else \
-        torch.empty((G, 2, L, n), dtype=torch.int64, device=device)
-    if distributed:
-        dist.broadcast(rlk, src=0)
-    ctx.load_relin_key_dev(rlk, G)
-    torch.cuda.synchronize(device)
+    if args.config == "cfg2":
+        a = uniform_dev((B,), moduli, n, gen, device)
+        b = uniform_dev((B,), moduli, n, gen, device)
 
-    def step():
-        ctx.bfv_mul_and_relin_dev(ct1, ct2, out, B)
+        def step():  # fwd NTT of both operands, pointwise product, inverse NTT
+            ctx.rns_fwd_dev(a, B)
+            ctx.rns_fwd_dev(b, B)
+            ctx.rns_mul_dev(a, b, a, B)
+            ctx.rns_inv_dev(a, B)
+        units_per_step = B
+        unit = "poly_mul/s"
+        metric = "NTT-based negacyclic poly muls/sec (fwd NTT x2 + pointwise + inv NTT)"
+    else:
+        # relinearisation key: made once on rank 0, RCCL-broadcast to every GPU
+        rlk = uniform_dev((G, 2), moduli, n, kgen, device) if rank == 0 else \
+            torch.empty((G, 2, L, n), dtype=torch.int64, device=device)
+        if distributed:
+            dist.broadcast(rlk, src=0)
+        torch.cuda.synchronize(device)
+        ctx.load_relin_key_dev(rlk, G)
+        if dbfv is None:
+            ct1 = uniform_dev((B, 2), moduli, n, gen, device)
+            ct2 = uniform_dev((B, 2), moduli, n, gen, device)
+            out = torch.empty_like(ct1)
+
+            def step():
+                ctx.bfv_mul_and_relin_dev(ct1, ct2, out, B)
+            units_per_step = B
+            unit = "bfv_mul_and_relin/s"
+            metric = "ciphertext muls/sec (bfv_mul_and_relin)"
+        else:
+            d, base, dplain = dbfv
+            x = uniform_dev((B, d, 2), moduli, n, gen, device)
+            y = uniform_dev((B, d, 2), moduli, n, gen, device)
+            bufs = [torch.empty_like(x), torch.empty_like(x)]
+
+            def step():
+                # depth-`depth` chain: acc <- dbfv_mul(acc, y), mul_depth reset before every step
+                # (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220)
+                src = x
+                for k in range(depth):
+                    dst = bufs[k % 2]
+                    ctx.dbfv_mul_dev(d, base, dplain, src, y, dst, B)
+                    src = dst
+            units_per_step = B
+            unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
+            metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else \
+                f"dbfv_mul chains/sec (depth {depth})"
+    torch.cuda.synchronize(device)
 
     for _ in range(args.warmup):
         step()
@@ -160,7 +200,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * B * args.steps / elapsed
+    value = world * units_per_step * args.steps / elapsed
 
     # roofline of the dominant kernel: one profiled step, HIP events around every NTT launch
     ctx.prof_enable(True)
@@ -169,7 +209,8 @@ def main():
     fwd = ctx.prof_read(0)
     inv = ctx.prof_read(1)
     ctx.prof_enable(False)
-    dom, dom_name = (fwd, "ntt_fwd_kernel<12>") if fwd["ms"] >= inv["ms"] else (inv, "ntt_inv_kernel<12>")
+    logn = n.bit_length() - 1
+    dom, dom_name = (fwd, f"ntt_fwd_kernel<{logn}>") if fwd["ms"] >= inv["ms"] else (inv, f"ntt_inv_kernel<{logn}>")
     achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9 if dom["ms"] > 0 else 0.0
     per_launch_ms = dom["ms"] / max(dom["launches"], 1)
     roofline = {
@@ -188,7 +229,7 @@ def main():
     }
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cfg3":
         sample = args.cpu_sample or 3
         try:
             cpu = cpu_baseline(n, moduli, plain, gbase, sample)
@@ -196,10 +237,14 @@ def main():
             cpu = {"value": None, "error": repr(e)}
 
     if rank == 0:
+        workload = {"cfg2": "batched fwd NTT + pointwise mul + inv NTT, BASELINE configs[1]",
+                    "cfg3": "bfv_mul_and_relin, BASELINE configs[2]",
+                    "cfg4": "dbfv_mul d=2 b=256 p=2^16, BASELINE configs[3]",
+                    "cfg5": "dbfv_mul chain depth 4, d=8 b=256 p=2^64, BASELINE configs[4]"}[args.config]
         line = {
-            "metric": "ciphertext muls/sec (bfv_mul_and_relin)",
+            "metric": metric,
             "value": round(value, 1),
-            "unit": "bfv_mul_and_relin/s",
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -209,13 +254,16 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (uniform canonical residues per limb, seeded; rlk broadcast over RCCL)",
-            "config": {"workload": "bfv_mul_and_relin, BASELINE configs[2]", "ring_degree": n,
-                       "ct_limbs": L, "limb_bits": 60, "plain_modulus": plain, "gadget_base": gbase,
-                       "gadget_digits": G, "batch_per_gpu": B, "global_batch": B * world,
+            "config": {"workload": workload, "ring_degree": n, "ct_limbs": L, "limb_bits": 60,
+                       "plain_modulus": plain, "gadget_base": gbase, "gadget_digits": G,
+                       "batch_per_gpu": B, "global_batch": B * world,
                        "parallelism": f"batch-shard x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if dbfv is not None:
+            line["config"].update({"dbfv_digits": dbfv[0], "dbfv_base": dbfv[1],
+                                   "dbfv_plain_modulus": dbfv[2] or "2^64", "chain_depth": depth})
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()

@@ -1,0 +1,264 @@
+// exacto.hpp — C++ host API mirroring the reference's Rust API on the multiplication path,
+// layered on the C ABI (exacto_hip.h).  Same names and argument meaning as
+//   exacto::params::{BfvParams, BfvParamsBuilder, DbfvParams}   (src/params/mod.rs:12-193)
+//   exacto::bfv::{BfvCiphertext, RelinKey}                       (src/bfv/mod.rs:19-24, keygen.rs:39-45)
+//   exacto::bfv::eval::{bfv_mul_and_relin, bfv_mul_no_relin, bfv_add, bfv_sub, bfv_neg}
+//   exacto::bfv::keyswitch::relinearize
+//   exacto::dbfv::{DbfvCiphertext, eval::dbfv_mul}
+// Errors: Rust's Result<T, ExactoError> becomes a thrown exacto::ExactoError carrying the
+// variant (src/error.rs:4-31) and the reference's Display text.
+// Ciphertexts are host-resident here (one H2D/D2H per call); the batched overloads amortise it.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "exacto_hip.h"
+
+namespace exacto {
+
+class ExactoError : public std::runtime_error {
+  public:
+    ExactoError(int code, const std::string& msg) : std::runtime_error(msg), code_(code) {}
+    int code() const { return code_; }
+    const char* variant() const {
+        static const char* names[] = {"InvalidParam", "DimensionMismatch", "ModulusMismatch",
+                                      "InvalidRingDegree", "DecryptionError", "DecompositionError",
+                                      "LatticeError", "MissingKey", "NotImplemented"};
+        return (code_ >= 1 && code_ <= 9) ? names[code_ - 1] : "HipError";
+    }
+
+  private:
+    int code_;
+};
+
+namespace detail {
+inline void check(int rc) {
+    if (rc == 0) return;
+    char buf[1024];
+    exacto_last_error(buf, sizeof buf);
+    throw ExactoError(rc, buf);
+}
+}  // namespace detail
+
+// RnsPoly (src/ring/rns.rs:14-17): L limbs of n NTT-domain evaluations, stored [L][n].
+struct RnsPoly {
+    size_t ring_degree = 0;
+    size_t num_limbs = 0;
+    std::vector<uint64_t> data;  // [limb][n]
+    uint64_t* limb(size_t i) { return data.data() + i * ring_degree; }
+    const uint64_t* limb(size_t i) const { return data.data() + i * ring_degree; }
+};
+
+class BfvParams {
+  public:
+    size_t ring_degree;
+    uint64_t plain_modulus;
+    std::vector<uint64_t> ct_moduli, aux_moduli;
+    double sigma;
+    uint64_t gadget_base;
+    size_t gadget_digits;
+    ~BfvParams() { exacto_ctx_destroy(ctx_); }
+    exacto_ctx* ctx() const { return ctx_; }
+    size_t num_limbs() const { return ct_moduli.size(); }
+    // the key last uploaded to the context (identity, not contents)
+    mutable const void* loaded_key = nullptr;
+
+  private:
+    friend class BfvParamsBuilder;
+    exacto_ctx* ctx_ = nullptr;
+};
+using BfvParamsPtr = std::shared_ptr<const BfvParams>;
+
+// BfvParamsBuilder (src/params/mod.rs:30-124); build() also creates the device context.
+class BfvParamsBuilder {
+  public:
+    BfvParamsBuilder& ring_degree(size_t n) { n_ = n; return *this; }
+    BfvParamsBuilder& plain_modulus(uint64_t p) { p_ = p; return *this; }
+    BfvParamsBuilder& ct_moduli(std::vector<uint64_t> m) { ct_ = std::move(m); return *this; }
+    BfvParamsBuilder& aux_moduli(std::vector<uint64_t> m) { aux_ = std::move(m); return *this; }
+    BfvParamsBuilder& sigma(double s) { sigma_ = s; return *this; }
+    BfvParamsBuilder& gadget_base(uint64_t b) { base_ = b; return *this; }
+    BfvParamsBuilder& device(int d) { device_ = d; return *this; }
+    BfvParamsPtr build() const {
+        auto p = std::shared_ptr<BfvParams>(new BfvParams());
+        detail::check(exacto_ctx_create(&p->ctx_, n_, ct_.data(), ct_.size(),
+                                        aux_.empty() ? nullptr : aux_.data(), aux_.size(), p_, base_,
+                                        device_));
+        exacto_ctx_info info{};
+        detail::check(exacto_ctx_get_info(p->ctx_, &info));
+        p->ring_degree = n_;
+        p->plain_modulus = p_;
+        p->ct_moduli = ct_;
+        p->aux_moduli = aux_;
+        p->sigma = sigma_;
+        p->gadget_base = info.gadget_base;
+        p->gadget_digits = info.gadget_digits;
+        return p;
+    }
+
+  private:
+    size_t n_ = 4096;        // params/mod.rs:42
+    uint64_t p_ = 65537;     // params/mod.rs:43
+    std::vector<uint64_t> ct_, aux_;
+    double sigma_ = 3.2;
+    uint64_t base_ = 0;      // auto: 2^16 (params/mod.rs:102-108)
+    int device_ = 0;
+};
+
+struct BfvCiphertext {
+    std::vector<RnsPoly> c;
+    BfvParamsPtr params;
+    size_t degree() const { return c.size() - 1; }
+};
+
+struct RelinKey {
+    std::vector<std::pair<RnsPoly, RnsPoly>> keys;
+    BfvParamsPtr params;
+};
+
+namespace detail {
+inline std::vector<uint64_t> flatten(const std::vector<BfvCiphertext>& cts, size_t polys) {
+    std::vector<uint64_t> out;
+    for (auto& ct : cts) {
+        if (ct.c.size() != polys) throw ExactoError(1, "invalid parameter: mixed ciphertext degrees in a batch");
+        for (auto& p : ct.c) out.insert(out.end(), p.data.begin(), p.data.end());
+    }
+    return out;
+}
+inline std::vector<BfvCiphertext> unflatten(const std::vector<uint64_t>& flat, size_t batch, size_t polys,
+                                            const BfvParamsPtr& prm) {
+    const size_t L = prm->num_limbs(), n = prm->ring_degree;
+    std::vector<BfvCiphertext> out(batch);
+    for (size_t b = 0; b < batch; ++b) {
+        out[b].params = prm;
+        out[b].c.resize(polys);
+        for (size_t k = 0; k < polys; ++k) {
+            RnsPoly& p = out[b].c[k];
+            p.ring_degree = n;
+            p.num_limbs = L;
+            auto it = flat.begin() + (long)((b * polys + k) * L * n);
+            p.data.assign(it, it + (long)(L * n));
+        }
+    }
+    return out;
+}
+inline void load_key(const RelinKey& rlk) {
+    const BfvParams& prm = *rlk.params;
+    if (prm.loaded_key == &rlk) return;
+    std::vector<uint64_t> flat;
+    for (auto& kp : rlk.keys) {
+        flat.insert(flat.end(), kp.first.data.begin(), kp.first.data.end());
+        flat.insert(flat.end(), kp.second.data.begin(), kp.second.data.end());
+    }
+    check(exacto_ctx_load_relin_key(prm.ctx(), flat.empty() ? nullptr : flat.data(), rlk.keys.size()));
+    prm.loaded_key = &rlk;
+}
+}  // namespace detail
+
+// ---- exacto::bfv::eval (batched forms; the single-ciphertext forms below wrap them)
+inline std::vector<BfvCiphertext> bfv_mul_no_relin(const std::vector<BfvCiphertext>& a,
+                                                   const std::vector<BfvCiphertext>& b) {
+    if (a.empty()) return {};
+    const BfvParamsPtr& prm = a[0].params;
+    const size_t p1 = a[0].c.size(), p2 = b[0].c.size();
+    auto fa = detail::flatten(a, p1), fb = detail::flatten(b, p2);
+    std::vector<uint64_t> out(a.size() * 3 * prm->num_limbs() * prm->ring_degree);
+    detail::check(exacto_bfv_mul_no_relin(prm->ctx(), fa.data(), p1, fb.data(), p2, out.data(), a.size()));
+    return detail::unflatten(out, a.size(), 3, prm);
+}
+
+inline std::vector<BfvCiphertext> relinearize(const std::vector<BfvCiphertext>& cts, const RelinKey& rlk) {
+    if (cts.empty()) return {};
+    const BfvParamsPtr& prm = cts[0].params;
+    const size_t polys = cts[0].c.size();
+    detail::load_key(rlk);
+    auto f = detail::flatten(cts, polys);
+    const size_t outp = polys < 3 ? polys : 2;
+    std::vector<uint64_t> out(cts.size() * outp * prm->num_limbs() * prm->ring_degree);
+    detail::check(exacto_relinearize(prm->ctx(), f.data(), polys, out.data(), cts.size()));
+    return detail::unflatten(out, cts.size(), outp, prm);
+}
+
+inline std::vector<BfvCiphertext> bfv_mul_and_relin(const std::vector<BfvCiphertext>& a,
+                                                    const std::vector<BfvCiphertext>& b, const RelinKey& rlk) {
+    if (a.empty()) return {};
+    const BfvParamsPtr& prm = a[0].params;
+    if (a[0].c.size() != 2 || b[0].c.size() != 2)
+        throw ExactoError(1, "invalid parameter: multiplication requires degree-1 ciphertexts");
+    detail::load_key(rlk);
+    auto fa = detail::flatten(a, 2), fb = detail::flatten(b, 2);
+    std::vector<uint64_t> out(fa.size());
+    detail::check(exacto_bfv_mul_and_relin(prm->ctx(), fa.data(), fb.data(), out.data(), a.size()));
+    return detail::unflatten(out, a.size(), 2, prm);
+}
+
+inline BfvCiphertext bfv_mul_no_relin(const BfvCiphertext& a, const BfvCiphertext& b) {
+    return bfv_mul_no_relin(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b})[0];
+}
+inline BfvCiphertext relinearize(const BfvCiphertext& ct, const RelinKey& rlk) {
+    return relinearize(std::vector<BfvCiphertext>{ct}, rlk)[0];
+}
+inline BfvCiphertext bfv_mul_and_relin(const BfvCiphertext& a, const BfvCiphertext& b, const RelinKey& rlk) {
+    return bfv_mul_and_relin(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b}, rlk)[0];
+}
+
+// ---- exacto::dbfv
+struct DbfvParams {
+    BfvParamsPtr bfv_params;
+    uint64_t base;
+    size_t num_digits;
+    uint64_t plain_modulus;  // 0 == 2^64
+};
+
+struct DbfvCiphertext {
+    std::vector<BfvCiphertext> limbs;
+    size_t degree = 0;
+    size_t mul_depth = 0;
+    std::shared_ptr<const DbfvParams> params;
+    size_t num_limbs() const { return limbs.size(); }
+};
+
+// dbfv_mul (src/dbfv/eval.rs:82-149), batched over independent products.
+inline std::vector<DbfvCiphertext> dbfv_mul(const std::vector<DbfvCiphertext>& a,
+                                            const std::vector<DbfvCiphertext>& b, const RelinKey& rlk) {
+    if (a.empty()) return {};
+    const auto& dp = *a[0].params;
+    const size_t d = dp.num_digits;
+    for (size_t i = 0; i < a.size(); ++i)
+        if (a[i].num_limbs() != d || b[i].num_limbs() != d)
+            throw ExactoError(1, "invalid parameter: multiplication requires d-limb ciphertexts");
+    detail::load_key(rlk);
+    std::vector<uint64_t> fa, fb;
+    std::vector<uint32_t> da, db, dout(a.size());
+    for (size_t i = 0; i < a.size(); ++i) {
+        auto x = detail::flatten(a[i].limbs, 2), y = detail::flatten(b[i].limbs, 2);
+        fa.insert(fa.end(), x.begin(), x.end());
+        fb.insert(fb.end(), y.begin(), y.end());
+        da.push_back((uint32_t)a[i].mul_depth);
+        db.push_back((uint32_t)b[i].mul_depth);
+    }
+    std::vector<uint64_t> out(fa.size());
+    detail::check(exacto_dbfv_mul(dp.bfv_params->ctx(), d, dp.base, dp.plain_modulus, fa.data(), fb.data(),
+                                  out.data(), a.size(), da.data(), db.data(), dout.data()));
+    std::vector<DbfvCiphertext> res(a.size());
+    const size_t per = d * 2 * dp.bfv_params->num_limbs() * dp.bfv_params->ring_degree;
+    for (size_t i = 0; i < a.size(); ++i) {
+        std::vector<uint64_t> slice(out.begin() + (long)(i * per), out.begin() + (long)((i + 1) * per));
+        res[i].limbs = detail::unflatten(slice, d, 2, dp.bfv_params);
+        res[i].degree = d;
+        res[i].mul_depth = dout[i];
+        res[i].params = a[0].params;
+    }
+    return res;
+}
+
+inline DbfvCiphertext dbfv_mul(const DbfvCiphertext& a, const DbfvCiphertext& b, const RelinKey& rlk) {
+    return dbfv_mul(std::vector<DbfvCiphertext>{a}, std::vector<DbfvCiphertext>{b}, rlk)[0];
+}
+
+}  // namespace exacto

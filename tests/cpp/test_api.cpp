@@ -1,0 +1,180 @@
+// C++ host-API tests (include/exacto.hpp), mirroring the reference's Rust tests of the path.
+// Usage: test_api <fixture-dir> <case>...   (fixtures written by tests/test_cpp_api.py from
+// tests/golden/vectors.npz).  Prints "PASS <name>" per case and "ALL OK" at the end.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "exacto.hpp"
+
+using namespace exacto;
+
+static std::vector<uint64_t> read_u64(const std::string& path) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) throw std::runtime_error("missing " + path);
+    const auto bytes = (size_t)f.tellg();
+    std::vector<uint64_t> v(bytes / 8);
+    f.seekg(0);
+    f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)bytes);
+    return v;
+}
+
+struct Meta {
+    size_t n, L, K;
+    uint64_t plain, gbase;
+    std::vector<uint64_t> q, aux;
+    size_t d = 0;
+    uint64_t base = 0, dplain = 0;
+};
+
+static Meta read_meta(const std::string& path) {
+    std::ifstream f(path);
+    Meta m{};
+    f >> m.n >> m.L >> m.K >> m.plain >> m.gbase;
+    m.q.resize(m.L);
+    for (auto& x : m.q) f >> x;
+    m.aux.resize(m.K);
+    for (auto& x : m.aux) f >> x;
+    f >> m.d >> m.base >> m.dplain;
+    return m;
+}
+
+static std::vector<BfvCiphertext> to_cts(const std::vector<uint64_t>& flat, size_t batch, size_t polys,
+                                         const BfvParamsPtr& prm) {
+    return detail::unflatten(flat, batch, polys, prm);
+}
+
+static RelinKey to_rlk(const std::vector<uint64_t>& flat, const BfvParamsPtr& prm) {
+    const size_t Ln = prm->num_limbs() * prm->ring_degree;
+    RelinKey k;
+    k.params = prm;
+    for (size_t g = 0; g * 2 * Ln < flat.size(); ++g) {
+        RnsPoly a{prm->ring_degree, prm->num_limbs(), {}}, b = a;
+        a.data.assign(flat.begin() + (long)(2 * g * Ln), flat.begin() + (long)((2 * g + 1) * Ln));
+        b.data.assign(flat.begin() + (long)((2 * g + 1) * Ln), flat.begin() + (long)((2 * g + 2) * Ln));
+        k.keys.push_back({a, b});
+    }
+    return k;
+}
+
+static bool same(const std::vector<BfvCiphertext>& got, const std::vector<uint64_t>& want) {
+    std::vector<uint64_t> flat;
+    for (auto& ct : got)
+        for (auto& p : ct.c) flat.insert(flat.end(), p.data.begin(), p.data.end());
+    return flat == want;
+}
+
+static int run_case(const std::string& dir, const std::string& name) {
+    const Meta m = read_meta(dir + "/" + name + ".meta");
+    auto prm = BfvParamsBuilder().ring_degree(m.n).plain_modulus(m.plain).ct_moduli(m.q).aux_moduli(m.aux)
+                   .gadget_base(m.gbase).sigma(3.2).build();
+    const size_t Ln = m.L * m.n;
+    const RelinKey rlk = to_rlk(read_u64(dir + "/" + name + ".rlk.u64"), prm);
+    if (m.d == 0) {
+        const auto c1 = read_u64(dir + "/" + name + ".ct1.u64");
+        const size_t B = c1.size() / (2 * Ln);
+        auto a = to_cts(c1, B, 2, prm);
+        auto b = to_cts(read_u64(dir + "/" + name + ".ct2.u64"), B, 2, prm);
+        // eval.rs:73 bfv_mul_and_relin, batched and single
+        const auto want = read_u64(dir + "/" + name + ".out.u64");
+        if (!same(bfv_mul_and_relin(a, b, rlk), want)) return 1;
+        auto one = bfv_mul_and_relin(a[0], b[0], rlk);
+        if (!same({one}, std::vector<uint64_t>(want.begin(), want.begin() + (long)(2 * Ln)))) return 2;
+        // eval.rs:89 bfv_mul_no_relin + keyswitch.rs:59 relinearize
+        auto three = bfv_mul_no_relin(a, b);
+        if (!same(three, read_u64(dir + "/" + name + ".out3.u64"))) return 3;
+        if (!same(relinearize(three, rlk), read_u64(dir + "/" + name + ".out.u64"))) return 4;
+    } else {
+        auto dp = std::make_shared<DbfvParams>(DbfvParams{prm, m.base, m.d, m.dplain});
+        const auto fa = read_u64(dir + "/" + name + ".a.u64");
+        const auto fb = read_u64(dir + "/" + name + ".b.u64");
+        const size_t per = m.d * 2 * Ln, B = fa.size() / per;
+        std::vector<DbfvCiphertext> A(B), Bc(B);
+        for (size_t i = 0; i < B; ++i) {
+            A[i].limbs = to_cts(std::vector<uint64_t>(fa.begin() + (long)(i * per), fa.begin() + (long)((i + 1) * per)), m.d, 2, prm);
+            Bc[i].limbs = to_cts(std::vector<uint64_t>(fb.begin() + (long)(i * per), fb.begin() + (long)((i + 1) * per)), m.d, 2, prm);
+            A[i].degree = Bc[i].degree = m.d;
+            A[i].params = Bc[i].params = dp;
+        }
+        auto r = dbfv_mul(A, Bc, rlk);
+        std::vector<BfvCiphertext> limbs;
+        for (auto& x : r) {
+            if (x.mul_depth != 1 || x.degree != m.d) return 5;
+            limbs.insert(limbs.end(), x.limbs.begin(), x.limbs.end());
+        }
+        if (!same(limbs, read_u64(dir + "/" + name + ".out.u64"))) return 6;
+        // dbfv/eval.rs:292-313: chained multiplication is rejected
+        try {
+            dbfv_mul(r[0], Bc[0], rlk);
+            return 7;
+        } catch (const ExactoError& e) {
+            if (std::string(e.variant()) != "NotImplemented" ||
+                std::string(e.what()).find("chained dBFV multiplication requires ciphertext-level lattice reduction") ==
+                    std::string::npos)
+                return 8;
+        }
+    }
+    return 0;
+}
+
+static int error_cases() {
+    // eval.rs:93-97 and keyswitch.rs:66-70 messages; params/mod.rs:82-90 builder errors
+    try {
+        BfvParamsBuilder().ring_degree(12).ct_moduli({65537}).build();
+        return 10;
+    } catch (const ExactoError& e) {
+        if (std::string(e.variant()) != "InvalidRingDegree") return 11;
+    }
+    try {
+        BfvParamsBuilder().ring_degree(16).build();
+        return 12;
+    } catch (const ExactoError& e) {
+        if (std::string(e.what()) != "invalid parameter: must specify at least one ciphertext modulus") return 13;
+    }
+    auto prm = BfvParamsBuilder().ring_degree(16).plain_modulus(257).ct_moduli({65537, 1099509805057}).gadget_base(8).build();
+    RnsPoly z{16, 2, std::vector<uint64_t>(32, 0)};
+    BfvCiphertext c3{{z, z, z}, prm};
+    RelinKey rlk{{}, prm};
+    try {
+        bfv_mul_and_relin(c3, c3, rlk);
+        return 14;
+    } catch (const ExactoError& e) {
+        if (std::string(e.what()).find("multiplication requires degree-1 ciphertexts") == std::string::npos) return 15;
+    }
+    BfvCiphertext c4{{z, z, z, z}, prm};
+    try {
+        relinearize(c4, rlk);
+        return 16;
+    } catch (const ExactoError& e) {
+        if (std::string(e.what()).find("relinearization only supports degree-2 ciphertexts") == std::string::npos) return 17;
+    }
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <fixture-dir> <case>...\n", argv[0]);
+        return 2;
+    }
+    int bad = 0;
+    for (int i = 2; i < argc; ++i) {
+        int rc;
+        try {
+            rc = run_case(argv[1], argv[i]);
+        } catch (const std::exception& e) {
+            std::printf("ERROR %s: %s\n", argv[i], e.what());
+            rc = 99;
+        }
+        std::printf("%s %s (%d)\n", rc ? "FAIL" : "PASS", argv[i], rc);
+        bad |= rc != 0;
+    }
+    const int e = error_cases();
+    std::printf("%s error_cases (%d)\n", e ? "FAIL" : "PASS", e);
+    bad |= e != 0;
+    if (!bad) std::printf("ALL OK\n");
+    return bad;
+}
