@@ -188,7 +188,7 @@ struct exacto_ctx {
     bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool rlk_loaded = false;
     // workspace (per chunk)
-    size_t chunk = 128;
+    size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
     size_t ws_items = 0;
     u64 *ws_coefQ = nullptr, *ws_extP = nullptr, *ws_T = nullptr, *ws_D = nullptr;
     // staging for host-pointer API and dBFV products
@@ -696,8 +696,9 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         if (relin && guse > 0) {
             if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false)) return e;
             // 8. relinearisation MAC, in place on the output
-            launch_relin_mac(R, nullptr, out_stride, 0, c->ws_D, c->d_rlk, guse, R, out_stride, cnt, n, L,
-                             c->d_primes, c->stream);
+            if (int e = ensure_rlk_companions(c)) return e;
+            launch_relin_mac(R, nullptr, out_stride, 0, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n,
+                             L, c->d_primes, c->stream);
             CHECK_LAUNCH();
         }
     }
@@ -841,8 +842,9 @@ extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t 
         launch_decompose(c->ws_coefQ, Ln, c->ws_D, guse, cnt, c->n, c->d_crt, c->d_primes, c->L, c->stream);
         CHECK_LAUNCH();
         if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * c->L, 0, c->L, c->n), (long)cnt * guse * c->L, false)) return e;
-        launch_relin_mac(dst, nullptr, 2 * Ln, 0, c->ws_D, c->d_rlk, guse, dst, 2 * Ln, cnt, c->n, c->L, c->d_primes,
-                         c->stream);
+        if (int e = ensure_rlk_companions(c)) return e;
+        launch_relin_mac(dst, nullptr, 2 * Ln, 0, c->ws_D, c->d_rlk, c->d_rlk_s, guse, dst, 2 * Ln, cnt, c->n, c->L,
+                         c->d_primes, c->stream);
         CHECK_LAUNCH();
     }
     return 0;

@@ -105,8 +105,8 @@ void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, 
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
                       const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s);
 void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long base_poly0,
-                      const u64* D, const u64* rlk, int guse, u64* out, long out_stride, int items,
-                      int n, int L, const PrimeConst* primes, hipStream_t s);
+                      const u64* D, const u64* rlk, const u64* rlk_s, int guse, u64* out, long out_stride,
+                      int items, int n, int L, const PrimeConst* primes, hipStream_t s);
 
 enum class PwOp : int { Add = 0, Sub = 1, Neg = 2, Mul = 3, ScalarMul = 4, Copy = 5 };
 void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys, int n, int L,

@@ -470,36 +470,41 @@ void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items
 
 __global__ void __launch_bounds__(TPB)
 relin_mac_kernel(const u64* __restrict__ base, const u64* __restrict__ base_off, long base_stride,
-                 const u64* __restrict__ D, const u64* __restrict__ rlk, int guse,
-                 u64* __restrict__ out, long out_stride, int n, int L,
+                 const u64* __restrict__ D, const u64* __restrict__ rlk, const u64* __restrict__ rlk_s,
+                 int guse, u64* __restrict__ out, long out_stride, int n, int L,
                  const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
     const long item = row / L;
     const int i = (int)(row - item * L);
     const PrimeConst& P = primes[i];
+    const u64 q = P.q, q2 = P.two_q, nq = (u64)0 - q;
     const u64* bp = base + (base_off ? (long)base_off[item] : item * base_stride);
+    // accumulators kept in [0, 2q): key is constant, so Shoup with precomputed companions
     u64 acc0 = bp[(long)i * n + j];
     u64 acc1 = bp[(long)(L + i) * n + j];
     const u64* dp = D + item * (long)guse * L * n + (long)i * n + j;
-    const u64* kp = rlk + (long)i * n + j;
     const long Ln = (long)L * n;
+    const long ko = (long)i * n + j;
     for (int g = 0; g < guse; ++g) {
         const u64 d = dp[g * Ln];
-        acc0 = add_mod(acc0, mul_mod(d, kp[(2L * g) * Ln], P), P.q);
-        acc1 = add_mod(acc1, mul_mod(d, kp[(2L * g + 1) * Ln], P), P.q);
+        const long k0 = (2L * g) * Ln + ko, k1 = k0 + Ln;
+        u64 t = acc0 + shoup_mul_nq(d, rlk[k0], rlk_s[k0], nq);
+        acc0 = t >= q2 ? t - q2 : t;
+        t = acc1 + shoup_mul_nq(d, rlk[k1], rlk_s[k1], nq);
+        acc1 = t >= q2 ? t - q2 : t;
     }
     u64* op = out + item * out_stride + (long)i * n + j;
-    op[0] = acc0;
-    op[Ln] = acc1;
+    op[0] = acc0 >= q ? acc0 - q : acc0;
+    op[Ln] = acc1 >= q ? acc1 - q : acc1;
 }
 
 void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long /*base_poly0*/,
-                      const u64* D, const u64* rlk, int guse, u64* out, long out_stride, int items,
-                      int n, int L, const PrimeConst* primes, hipStream_t s) {
+                      const u64* D, const u64* rlk, const u64* rlk_s, int guse, u64* out, long out_stride,
+                      int items, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = (long)items * L * blocks_per_row(n);
     if (blocks == 0) return;
     hipLaunchKernelGGL(relin_mac_kernel, dim3(blocks), dim3(TPB), 0, s, base, base_off, base_stride, D,
-                       rlk, guse, out, out_stride, n, L, primes);
+                       rlk, rlk_s, guse, out, out_stride, n, L, primes);
 }
 
 // ---------------------------------------------------------------- pointwise RNS ops
