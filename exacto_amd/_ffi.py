@@ -11,7 +11,8 @@ import os
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libexacto_hip.so")
+_LIB_PATH = os.environ.get("EXACTO_HIP_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libexacto_hip.so")  # env: kernel-variant builds (tools/)
 
 VARIANTS = ("InvalidParam", "DimensionMismatch", "ModulusMismatch", "InvalidRingDegree",
             "DecryptionError", "DecompositionError", "LatticeError", "MissingKey", "NotImplemented")

@@ -15,6 +15,28 @@
 
 namespace exacto {
 
+// Twiddle tables are read-only for a kernel's lifetime: addressing them through the
+// constant address space turns block-uniform loads into s_load and the rest into
+// global_load (a generic pointer read from PrimeConst would give flat_load, which
+// counts against lgkmcnt, so every LDS barrier would also wait on the twiddle preload).
+#ifndef EXACTO_TW_AS
+#define EXACTO_TW_AS 1
+#endif
+#if EXACTO_TW_AS == 0
+typedef const TwPair* TwTab;
+#else
+typedef const TwPair __attribute__((address_space(EXACTO_TW_AS)))* TwTab;
+#endif
+
+__device__ __forceinline__ TwTab tw_table(const TwPair* p) { return (TwTab)p; }
+
+__device__ __forceinline__ TwPair ld_tw(TwTab tab, int i) {
+    TwPair t;
+    t.w = tab[i].w;
+    t.ws = tab[i].ws;
+    return t;
+}
+
 __device__ __forceinline__ int swz(int j) {
     return j ^ ((j >> 4) & 15) ^ (((j >> 8) & 1) << 4);
 }
@@ -47,7 +69,7 @@ __device__ __forceinline__ void lds_load(const u64* lds, u64 (&x)[16], int tid) 
 // Twiddles of one round: stage bit b uses (8 >> (b - LO)) groups; at most 1+2+4+8 = 15 pairs.
 // Index of group g at bit b: (N >> (b+1)) + (thigh << (LO+3-b)) + g.
 template <int LOGN, int LO, int BHI, int BLO>
-__device__ __forceinline__ void load_round_tw(TwPair (&tw)[15], int tid, const TwPair* __restrict__ tab) {
+__device__ __forceinline__ void load_round_tw(TwPair (&tw)[15], int tid, TwTab tab) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
     int slot = 0;
@@ -55,7 +77,7 @@ __device__ __forceinline__ void load_round_tw(TwPair (&tw)[15], int tid, const T
     for (int b = BHI; b >= BLO; --b) {
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
-        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = tab[base + g];
+        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = ld_tw(tab, base + g);
     }
 }
 
@@ -90,7 +112,7 @@ __device__ __forceinline__ void fwd_round(u64 (&x)[16], const TwPair (&tw)[15], 
 // Butterflies of one round with each twiddle loaded right before its group (low register
 // pressure; used where the accumulators of the fused key switch need the VGPRs).
 template <int LOGN, int LO, int BHI, int BLO, bool LAZY>
-__device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, const TwPair* __restrict__ tab,
+__device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, TwTab tab,
                                                  u64 nq, u64 q2) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
@@ -101,7 +123,7 @@ __device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, const Tw
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
         for (int g = 0; g < (8 >> lb); ++g) {
-            const TwPair t = tab[base + g];
+            const TwPair t = ld_tw(tab, base + g);
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m;
@@ -117,7 +139,7 @@ __device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, const Tw
 }
 
 template <int LOGN, int R, bool LAZY, bool PRELOAD = true>
-__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tab, u64 nq,
+__device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTab tab, u64 nq,
                                            u64 q2, u64 q8) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
@@ -139,8 +161,24 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, cons
     if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY, PRELOAD>(x, lds, tid, tab, nq, q2, q8);
 }
 
+// Build-time tuning knobs (tools/build_variants.sh measures them).
+#ifndef EXACTO_NTT_PRELOAD
+#define EXACTO_NTT_PRELOAD 1
+#endif
+#ifndef EXACTO_NTT_TOUT
+#define EXACTO_NTT_TOUT 1  // forward: transpose through LDS so the output stores coalesce
+#endif
+#ifndef EXACTO_NTT_TIN
+#define EXACTO_NTT_TIN 0   // inverse: coalesced loads, transposed through LDS (measured slower)
+#endif
+#ifdef EXACTO_NTT_WAVES
+#define NTT_OCC __attribute__((amdgpu_waves_per_eu(EXACTO_NTT_WAVES)))
+#else
+#define NTT_OCC
+#endif
+
 template <int LOGN, bool LAZY>
-__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16) NTT_OCC
 ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
@@ -160,7 +198,7 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
 
     const u64 q8 = 8 * q;
-    fwd_rounds<LOGN, 0, LAZY>(x, lds, tid, P.tw_fwd, (u64)0 - q, q2, q8);
+    fwd_rounds<LOGN, 0, LAZY, EXACTO_NTT_PRELOAD>(x, lds, tid, tw_table(P.tw_fwd), (u64)0 - q, q2, q8);
 
     // final layout: element 16*tid + k; reduce [0,16q) (LAZY) or [0,4q) -> [0,q)
 #pragma unroll
@@ -173,15 +211,26 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         v = v >= q2 ? v - q2 : v;
         x[k] = v >= q ? v - q : v;
     }
-    ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst + 16 * tid);
+    if constexpr (EXACTO_NTT_TOUT) {
+        // element 16*tid+k -> element tid+k*T: every store instruction then writes 512
+        // contiguous bytes per wave instead of touching 64 cache lines
+        lds_barrier();
+        lds_store<0>(lds, x, tid);
+        lds_barrier();
+        lds_load<LOGN - 4>(lds, x, tid);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d2[k] = make_ulonglong2(x[2 * k], x[2 * k + 1]);
+        for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+    } else {
+        ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d2[k] = make_ulonglong2(x[2 * k], x[2 * k + 1]);
+    }
 }
 
 // ---------------------------------------------------------------- inverse
 
 template <int LOGN, int LO, int BLO, int BHI>
-__device__ __forceinline__ void load_round_tw_inv(TwPair (&tw)[15], int tid, const TwPair* __restrict__ tab) {
+__device__ __forceinline__ void load_round_tw_inv(TwPair (&tw)[15], int tid, TwTab tab) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
     int slot = 0;
@@ -190,49 +239,77 @@ __device__ __forceinline__ void load_round_tw_inv(TwPair (&tw)[15], int tid, con
         if (b == LOGN - 1) continue;  // last stage uses the n^-1-folded constants
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
-        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = tab[base + g];
+        for (int g = 0; g < (8 >> (b - LO)); ++g) tw[slot++] = ld_tw(tab, base + g);
     }
 }
 
-template <int LOGN, int LO, int BLO, int BHI>
+// Gentleman-Sande stages with per-register bound tracking.  m[k] is a compile-time bound
+// (x[k] < m[k]*q; the array folds away after unrolling).  Sums are left unreduced while
+// the pair's sum stays < 16q (< 2^64 since q < 2^60); otherwise the larger operand is
+// halved with one conditional subtraction.  Differences enter Shoup as U - V + m[V]*q
+// (any value < 2^64 is a valid Shoup input) and leave in [0, 2q).  Rounds start and end
+// with every value < 4q: 12 conditional subtractions per 4-stage round instead of 32.
+__device__ __forceinline__ void halve(u64& v, int& m, u64 q) {
+    const u64 t = q * (u64)(m / 2);
+    v = v >= t ? v - t : v;
+    m /= 2;
+}
+
+template <int LOGN, int LO, int BLO, int BHI, bool LAZY>
 __device__ __forceinline__ void inv_round(u64 (&x)[16], const TwPair (&tw)[15], const PrimeConst& P) {
-    const u64 q = P.q, q2 = P.two_q, nq = (u64)0 - q;
+    // LAZY: all q < 2^60, sums may reach 16q; otherwise (q < 2^62) only 4q, round invariant 2q
+    constexpr int CAP = LAZY ? 16 : 4, INV = LAZY ? 4 : 2;
+    const u64 q = P.q, nq = (u64)0 - q;
+    int m[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = INV;
     int slot = 0;
 #pragma unroll
     for (int b = BLO; b <= BHI; ++b) {
         const int lb = b - LO;
         const int half = 1 << lb;
-        if (b == LOGN - 1) {
-            // last stage: (U+V) * n^-1, (U-V) * psi_inv_rev[1] * n^-1, fully reduced
 #pragma unroll
-            for (int m = 0; m < half; ++m) {
-                const int k0 = m, k1 = m + half;
+        for (int g = 0; g < (8 >> lb); ++g) {
+            TwPair t{0, 0};
+            if (b != LOGN - 1) t = tw[slot++];
+#pragma unroll
+            for (int mm = 0; mm < half; ++mm) {
+                const int k0 = g * 2 * half + mm, k1 = k0 + half;
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+                    if (m[k0] + m[k1] > CAP) {
+                        if (m[k0] >= m[k1]) halve(x[k0], m[k0], q);
+                        else halve(x[k1], m[k1], q);
+                    }
                 const u64 U = x[k0], V = x[k1];
-                u64 a = shoup_mul_nq(U + V, P.n_inv, P.n_inv_s, nq);
-                u64 c = shoup_mul_nq(U - V + q2, P.last_w, P.last_ws, nq);
-                x[k0] = a >= q ? a - q : a;
-                x[k1] = c >= q ? c - q : c;
-            }
-        } else {
-#pragma unroll
-            for (int g = 0; g < (8 >> lb); ++g) {
-                const TwPair t = tw[slot++];
-#pragma unroll
-                for (int m = 0; m < half; ++m) {
-                    const int k0 = g * 2 * half + m;
-                    const int k1 = k0 + half;
-                    const u64 U = x[k0], V = x[k1];
-                    u64 s = U + V;
-                    x[k0] = s >= q2 ? s - q2 : s;
-                    x[k1] = shoup_mul_nq(U - V + q2, t.w, t.ws, nq);
+                const u64 D = U - V + q * (u64)m[k1];
+                if (b == LOGN - 1) {
+                    // last stage: (U+V) * n^-1, (U-V) * psi_inv_rev[1] * n^-1, fully reduced
+                    const u64 a = shoup_mul_nq(U + V, P.n_inv, P.n_inv_s, nq);
+                    const u64 c = shoup_mul_nq(D, P.last_w, P.last_ws, nq);
+                    x[k0] = a >= q ? a - q : a;
+                    x[k1] = c >= q ? c - q : c;
+                    m[k0] = m[k1] = 1;
+                } else {
+                    x[k0] = U + V;
+                    x[k1] = shoup_mul_nq(D, t.w, t.ws, nq);
+                    m[k0] += m[k1];
+                    m[k1] = 2;
                 }
             }
         }
     }
+    if (BHI < LOGN - 1) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+                if (m[k] > INV) halve(x[k], m[k], q);
+    }
 }
 
-template <int LOGN, int R>
-__device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, const TwPair* tab,
+template <int LOGN, int R, bool LAZY>
+__device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, TwTab tab,
                                            const PrimeConst& P) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -246,12 +323,12 @@ __device__ __forceinline__ void inv_rounds(u64 (&x)[16], u64* lds, int tid, cons
         lds_barrier();
         lds_load<LO>(lds, x, tid);
     }
-    inv_round<LOGN, LO, BLO, BHI>(x, tw, P);
-    if constexpr (BHI < LOGN - 1) inv_rounds<LOGN, R + 1>(x, lds, tid, tab, P);
+    inv_round<LOGN, LO, BLO, BHI, LAZY>(x, tw, P);
+    if constexpr (BHI < LOGN - 1) inv_rounds<LOGN, R + 1, LAZY>(x, lds, tid, tab, P);
 }
 
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+template <int LOGN, bool LAZY>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16) NTT_OCC
 ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
@@ -267,15 +344,24 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
 
     u64 x[16];
-    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+    if constexpr (EXACTO_NTT_TIN) {
+        // coalesced loads (element tid+k*T), then transpose to 16*tid+k through LDS
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const ulonglong2 v = s2[k];
-        x[2 * k] = v.x;
-        x[2 * k + 1] = v.y;
+        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+        lds_store<LOGN - 4>(lds, x, tid);
+        lds_barrier();
+        lds_load<0>(lds, x, tid);
+    } else {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 v = s2[k];
+            x[2 * k] = v.x;
+            x[2 * k + 1] = v.y;
+        }
     }
 
-    inv_rounds<LOGN, 0>(x, lds, tid, P.tw_inv, P);
+    inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
 
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
@@ -304,7 +390,7 @@ keyswitch_kernel(KsArgs a, const PrimeConst* __restrict__ primes) {
     const long Ln = (long)L * N;
 
     auto ntt_canon = [&](u64 (&x)[16]) {
-        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, P.tw_fwd, nq, q2, q8);
+        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, tw_table(P.tw_fwd), nq, q2, q8);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             u64 v = x[k];
@@ -345,7 +431,7 @@ keyswitch_kernel(KsArgs a, const PrimeConst* __restrict__ primes) {
     for (int g = 0; g < a.guse; ++g) {
         u64 x[16];
         load_coeff(x, dbase + g * Ln);
-        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, P.tw_fwd, nq, q2, q8);  // any value < 2^64 is a valid Shoup input
+        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, tw_table(P.tw_fwd), nq, q2, q8);  // any value < 2^64 is a valid Shoup input
         const long ko = ((long)(2 * g) * L + i) * N + 16 * tid;
         const ulonglong2* k0 = reinterpret_cast<const ulonglong2*>(a.rlk + ko);
         const ulonglong2* k0s = reinterpret_cast<const ulonglong2*>(a.rlk_s + ko);
@@ -395,7 +481,8 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
                        hipStream_t s) {
     constexpr int threads = (1 << LOGN) / 16;
     if (inverse)
-        hipLaunchKernelGGL(ntt_inv_kernel<LOGN>, dim3(count), dim3(threads), 0, s, nb, primes);
+        hipLaunchKernelGGL((lazy ? ntt_inv_kernel<LOGN, true> : ntt_inv_kernel<LOGN, false>), dim3(count),
+                           dim3(threads), 0, s, nb, primes);
     else if (lazy)
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
     else

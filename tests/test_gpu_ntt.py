@@ -125,3 +125,20 @@ def test_limb_out_of_range(gpu_available):
     with pytest.raises(ExactoError) as e:
         ctx.ntt_fwd(np.zeros((1, 16), dtype=np.uint64), limb=3)
     assert e.value.variant == "DimensionMismatch"
+
+
+@pytest.mark.parametrize("n,q", [(16, 65537), (4096, CFG2_Q), (8192, 1152921504606748673),
+                                 (4096, 4611686018427322369), (2048, 2305843009213554689)])
+def test_ntt_extreme_inputs(gpu_available, n, q):
+    # worst-case magnitudes for the lazy bounds: all q-1, alternating 0/q-1, and the inverse
+    # applied to all-(q-1) evaluations
+    ctx = HipContext(n, [q], plain_modulus=257)
+    top = np.full(n, q - 1, dtype=np.uint64)
+    alt = np.where(np.arange(n) % 2 == 0, q - 1, 0).astype(np.uint64)
+    a = np.stack([top, alt, top[::-1].copy()])
+    got = ctx.ntt_fwd(a)
+    for r in range(2):
+        assert [int(x) for x in got[r]] == oracle_fwd(a[r], n, q)
+    assert np.array_equal(ctx.ntt_inv(got), a)
+    inv_top = ctx.ntt_inv(top[None, :])
+    assert np.array_equal(ctx.ntt_fwd(inv_top), top[None, :])

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Builds libexacto_hip.so variants that differ only in ntt.hip compile flags, for A/B runs of
+# tools/ntt_bench.py / bench.py with EXACTO_HIP_LIB=build/variants/<name>.so.
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+make -C $R/exacto_amd/csrc -s
+OUT=$R/build/variants; mkdir -p $OUT
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC"
+build() {  # name, flags...
+  local name=$1; shift
+  $H "$@" -c $R/exacto_amd/csrc/ntt.hip -o $OUT/ntt_$name.o
+  $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o $OUT/ntt_$name.o
+}
+for v in "$@"; do
+  case $v in
+    base) build base ;;
+    as0) build as0 -DEXACTO_TW_AS=0 ;;
+    as1) build as1 -DEXACTO_TW_AS=1 ;;
+    as1_w4) build as1_w4 -DEXACTO_TW_AS=1 -DEXACTO_NTT_WAVES=4 ;;
+    as4_w4) build as4_w4 -DEXACTO_NTT_WAVES=4 ;;
+    old) build old -DEXACTO_NTT_TOUT=0 -DEXACTO_NTT_TIN=0 ;;
+    tout) build tout -DEXACTO_NTT_TIN=0 ;;
+    tin) build tin -DEXACTO_NTT_TOUT=0 ;;
+    nopre) build nopre -DEXACTO_NTT_PRELOAD=0 ;;
+    nopre_w5) build nopre_w5 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=5 ;;
+    nopre_w6) build nopre_w6 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=6 ;;
+    w5) build w5 -DEXACTO_NTT_WAVES=5 ;;
+    ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
+    ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
+    *) echo "unknown variant $v"; exit 1 ;;
+  esac
+done
