@@ -348,6 +348,7 @@ static int build_tables(exacto_ctx* c) {
         const u64 mx = *std::max_element(c->primes.begin(), c->primes.end());
         const u64 mn = *std::min_element(c->primes.begin(), c->primes.end());
         C.near = (u128)mx < 2 * (u128)mn;
+        C.fast = C.near && mx < (1ull << 60);
         C.digit_small = c->gbase <= *std::min_element(qv.begin(), qv.end());
     }
     HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
@@ -656,7 +657,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_extend(c->ws_coefQ, c->ws_extP, cnt, n, c->d_primes, K, c->stream);
         else
-            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.near != 0,
+            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0),
                               c->stream);
         CHECK_LAUNCH();
         // 3. forward NTT of the extended polynomials
@@ -674,7 +675,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, L, K,
-                               c->h_crt.near != 0, c->stream);
+                               c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
         CHECK_LAUNCH();
         // 7. forward NTT of the results (and digits)
         NttBatch rb{};
@@ -697,8 +698,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false)) return e;
             // 8. relinearisation MAC, in place on the output
             if (int e = ensure_rlk_companions(c)) return e;
-            launch_relin_mac(R, nullptr, out_stride, 0, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n,
-                             L, c->d_primes, c->stream);
+            launch_relin_mac(R, out_stride, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n, L,
+                             c->d_primes, c->stream);
             CHECK_LAUNCH();
         }
     }
@@ -843,7 +844,7 @@ extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t 
         CHECK_LAUNCH();
         if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * c->L, 0, c->L, c->n), (long)cnt * guse * c->L, false)) return e;
         if (int e = ensure_rlk_companions(c)) return e;
-        launch_relin_mac(dst, nullptr, 2 * Ln, 0, c->ws_D, c->d_rlk, c->d_rlk_s, guse, dst, 2 * Ln, cnt, c->n, c->L,
+        launch_relin_mac(dst, 2 * Ln, c->ws_D, c->d_rlk, c->d_rlk_s, guse, dst, 2 * Ln, cnt, c->n, c->L,
                          c->d_primes, c->stream);
         CHECK_LAUNCH();
     }

@@ -50,6 +50,7 @@ struct CrtTables {
     u64 pq_w[EXACTO_MAX_K], pq_ws[EXACTO_MAX_K];
     u64 qpq_w[EXACTO_MAX_L + 1][EXACTO_MAX_K], qpq_ws[EXACTO_MAX_L + 1][EXACTO_MAX_K];
     int near;       // max prime < 2 * min prime: residues move between primes by one conditional subtraction
+    int fast;       // near and every prime < 2^60: lazy CRT kernels (unreduced Shoup sums)
     int digit_small;  // gadget base <= every ciphertext prime: digit magnitudes are already reduced
     u64 pmod_w[EXACTO_MAX_PRIMES], pmod_ws[EXACTO_MAX_PRIMES];  // plain mod prime_t
     u64 Qwords[EXACTO_MAX_L];                   // Q as little-endian 64-bit words
@@ -91,22 +92,22 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 };
 
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
-                       const PrimeConst* primes, int L, int K, bool near, hipStream_t s);
+                       const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
 void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
                    const PrimeConst* primes, hipStream_t s);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, bool near, hipStream_t s);
+                        int K, int mode, hipStream_t s);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
                       const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s);
-void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long base_poly0,
-                      const u64* D, const u64* rlk, const u64* rlk_s, int guse, u64* out, long out_stride,
-                      int items, int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
+                      int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
+                      hipStream_t s);
 
 enum class PwOp : int { Add = 0, Sub = 1, Neg = 2, Mul = 3, ScalarMul = 4, Copy = 5 };
 void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys, int n, int L,

@@ -89,13 +89,58 @@ __device__ __forceinline__ u64 mr_eval(const u64 (&v)[MAXN], int cnt, bool neg, 
     return acc;
 }
 
+// ---- lazy CRT helpers (FAST: primes near each other and all < 2^60) ----
+// A Shoup product accepts any 64-bit input and returns [0, 2q), so differences are formed as
+// t + 2q - v (v < 2q by nearness) and fed to it unreduced; sums of Shoup outputs are reduced
+// once with reduce64.  Only the mixed-radix digits themselves are made canonical.
+
+// Garner over Q; x[i] < 2 q_i.
+template <int LT>
+__device__ __forceinline__ void garner_q_fast(u64 (&v)[EXACTO_MAX_L], const u64 (&x)[EXACTO_MAX_L], int L_arg,
+                                              const CrtTables* __restrict__ C,
+                                              const PrimeConst* __restrict__ primes) {
+    const int L = LT ? LT : L_arg;
+#pragma unroll
+    for (int i = 0; i < EXACTO_MAX_L; ++i) {
+        if (i < L) {
+            const u64 qi = primes[i].q, nq = (u64)0 - qi;
+            u64 t = x[i];
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_L; ++k)
+                if (k < i) t = shoup_mul_nq(t + 2 * qi - v[k], C->gq_w[i][k], C->gq_ws[i][k], nq);
+            v[i] = t >= qi ? t - qi : t;
+        }
+    }
+}
+
+// sum_k v_k * pref[k][t] - neg * pref[cnt][t]  (mod prime_t), canonical; 14q < 2^64 bounds
+// the unreduced run to 7 terms.
+template <int MAXN, int STRIDE>
+__device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool neg, const u64* pw,
+                                            const u64* pws, int t, const PrimeConst& P) {
+    const u64 q = P.q, nq = (u64)0 - q;
+    u64 acc = 0;
+#pragma unroll
+    for (int k = 0; k < MAXN; ++k) {
+        if (k < cnt) {
+            acc += shoup_mul_nq(v[k], pw[k * STRIDE + t], pws[k * STRIDE + t], nq);
+            if (k % 7 == 6) acc = reduce64(acc, q, P.mu64);
+        }
+    }
+    acc = reduce64(acc, q, P.mu64);
+    if (neg) acc = sub_mod(acc, pw[cnt * STRIDE + t], q);
+    return acc;
+}
+
 // Balanced gadget digits of the centred CRT value of residues res[0..L) (mod Q).
 // keyswitch.rs:24-44 literally (truncating %, [-B/2, B/2) adjustment, final carry dropped),
 // on the exact value (extension semantics for Q >= 2^64; identical to rns.rs:114-151 below).
 // Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j).
-template <bool NEAR>
-__device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTables* __restrict__ C,
-                              const PrimeConst* __restrict__ primes, u64* D, int n, int guse) {
+template <bool NEAR, int LT = 0>
+__device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L_arg,
+                                              const CrtTables* __restrict__ C,
+                                              const PrimeConst* __restrict__ primes, u64* D, int n, int guse) {
+    const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
     u64 z[EXACTO_MAX_L];
     garner_q<NEAR>(z, res, L, C, primes);
     const bool neg = mr_greater<EXACTO_MAX_L>(z, C->halfQ_mr, L);
@@ -200,32 +245,52 @@ __device__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L, const CrtTa
 
 // ---------------------------------------------------------------- exact lift Q -> P
 
-template <bool NEAR>
+template <bool NEAR, bool FAST, int LT>
 __global__ void __launch_bounds__(TPB)
-exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L, int K,
+exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L_arg, int K,
                   const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
+    const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
     u64 x[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L) x[i] = coefQ[(row * L + i) * n + j];
-    garner_q<NEAR>(v, x, L, C, primes);
+    if (FAST) garner_q_fast<LT>(v, x, L, C, primes);
+    else garner_q<NEAR>(v, x, L, C, primes);
     const bool neg = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
     for (int a = 0; a < K; ++a) {
         const int t = L + a;
-        extP[(row * K + a) * n + j] = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, NEAR>(
-            v, L, neg, &C->qpref_w[0][0], &C->qpref_ws[0][0], t, primes[t]);
+        extP[(row * K + a) * n + j] =
+            FAST ? mr_eval_fast<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, neg, &C->qpref_w[0][0],
+                                                               &C->qpref_ws[0][0], t, primes[t])
+                 : mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, NEAR>(v, L, neg, &C->qpref_w[0][0],
+                                                                 &C->qpref_ws[0][0], t, primes[t]);
     }
 }
 
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
-                       const PrimeConst* primes, int L, int K, bool near, hipStream_t s) {
+                       const PrimeConst* primes, int L, int K, int mode, hipStream_t s) {
     const long blocks = (long)items * 4 * blocks_per_row(n);
     if (blocks == 0) return;
-    if (near)
-        hipLaunchKernelGGL(exact_lift_kernel<true>, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, primes);
-    else
-        hipLaunchKernelGGL(exact_lift_kernel<false>, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, primes);
+#define LIFT(NR, FS, LT)                                                                                      \
+    hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
+                       primes)
+    if (mode == 2) {
+        switch (L) {
+            case 1: LIFT(true, true, 1); break;
+            case 2: LIFT(true, true, 2); break;
+            case 3: LIFT(true, true, 3); break;
+            case 4: LIFT(true, true, 4); break;
+            case 5: LIFT(true, true, 5); break;
+            case 6: LIFT(true, true, 6); break;
+            default: LIFT(true, true, 0); break;
+        }
+    } else if (mode == 1) {
+        LIFT(true, false, 0);
+    } else {
+        LIFT(false, false, 0);
+    }
+#undef LIFT
 }
 
 // ---------------------------------------------------------------- HPS extension
@@ -296,12 +361,13 @@ void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n
 
 // ---------------------------------------------------------------- exact scale-and-round
 
-template <bool NEAR>
+template <bool NEAR, bool FAST, int LT>
 __global__ void __launch_bounds__(TPB)
 exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                   u64* __restrict__ D, int guse, int n, int L, int K,
+                   u64* __restrict__ D, int guse, int n, int L_arg, int K,
                    const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
+    const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
     const int NP = L + K;
     const long item = row / 3;
     const int comp = (int)(row - item * 3);
@@ -310,15 +376,36 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
     u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
-        if (i < L) u[i] = shoup_mul_red(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
-    garner_q<NEAR>(v, u, L, C, primes);
+        if (i < L)
+            u[i] = FAST ? shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q)
+                        : shoup_mul_red(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
+    if (FAST) garner_q_fast<LT>(v, u, L, C, primes);
+    else garner_q<NEAR>(v, u, L, C, primes);
     const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
     // r = (p*T - s) / Q in every auxiliary prime, with Q^-1 folded into the constants:
     // r = T*(p Q^-1) - sum_k v_k*(qpref_k Q^-1) + negs   (Q * Q^-1 == 1)
     u64 w[EXACTO_MAX_K];
 #pragma unroll
     for (int a = 0; a < EXACTO_MAX_K; ++a) {
-        if (a < K) {
+        if (a < K && FAST) {
+            const PrimeConst& P = primes[L + a];
+            const u64 pa = P.q, np = (u64)0 - pa;
+            // terms in (0, 2p]: 2p - x*c instead of a modular subtraction; <= 7 before a reduce
+            u64 acc = shoup_mul_nq(Tin[(long)(L + a) * n], C->pq_w[a], C->pq_ws[a], np) + (negs ? 1 : 0);
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_L; ++k) {
+                if (k < L) {
+                    acc += 2 * pa - shoup_mul_nq(v[k], C->qpq_w[k][a], C->qpq_ws[k][a], np);
+                    if (k % 6 == 5) acc = reduce64(acc, pa, P.mu64);
+                }
+            }
+            acc = reduce64(acc, pa, P.mu64);
+            // Garner over P on the fly; w_k < p_k < 2 p_a
+#pragma unroll
+            for (int k = 0; k < EXACTO_MAX_K; ++k)
+                if (k < a) acc = shoup_mul_nq(acc + 2 * pa - w[k], C->gp_w[a][k], C->gp_ws[a][k], np);
+            w[a] = acc >= pa ? acc - pa : acc;
+        } else if (a < K) {
             const PrimeConst& P = primes[L + a];
             const u64 pa = P.q;
             u64 acc = shoup_mul_red(Tin[(long)(L + a) * n], C->pq_w[a], C->pq_ws[a], pa);
@@ -343,8 +430,10 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L)
-            res[i] = mr_eval<EXACTO_MAX_K, EXACTO_MAX_L, NEAR>(w, K, negr, &C->ppref_w[0][0],
-                                                               &C->ppref_ws[0][0], i, primes[i]);
+            res[i] = FAST ? mr_eval_fast<EXACTO_MAX_K, EXACTO_MAX_L>(w, K, negr, &C->ppref_w[0][0],
+                                                                      &C->ppref_ws[0][0], i, primes[i])
+                          : mr_eval<EXACTO_MAX_K, EXACTO_MAX_L, NEAR>(w, K, negr, &C->ppref_w[0][0],
+                                                                      &C->ppref_ws[0][0], i, primes[i]);
     if (comp < ncomp_r) {
         u64* out = R + item * r_stride + (long)comp * L * n + j;
 #pragma unroll
@@ -352,20 +441,33 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
             if (i < L) out[(long)i * n] = res[i];
     }
     if (comp == 2 && D != nullptr)
-        gadget_digits<NEAR>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
+        gadget_digits<NEAR, LT>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
 }
 
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, bool near, hipStream_t s) {
+                        int K, int mode, hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-    if (near)
-        hipLaunchKernelGGL(exact_scale_kernel<true>, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
-                           guse, n, L, K, ct, primes);
-    else
-        hipLaunchKernelGGL(exact_scale_kernel<false>, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
-                           guse, n, L, K, ct, primes);
+#define SCALE(NR, FS, LT)                                                                                     \
+    hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
+                       D, guse, n, L, K, ct, primes)
+    if (mode == 2) {
+        switch (L) {
+            case 1: SCALE(true, true, 1); break;
+            case 2: SCALE(true, true, 2); break;
+            case 3: SCALE(true, true, 3); break;
+            case 4: SCALE(true, true, 4); break;
+            case 5: SCALE(true, true, 5); break;
+            case 6: SCALE(true, true, 6); break;
+            default: SCALE(true, true, 0); break;
+        }
+    } else if (mode == 1) {
+        SCALE(true, false, 0);
+    } else {
+        SCALE(false, false, 0);
+    }
+#undef SCALE
 }
 
 // ---------------------------------------------------------------- literal HPS scale
@@ -468,43 +570,68 @@ void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items
 
 // ---------------------------------------------------------------- relinearisation MAC
 
+// out_c = base_c + sum_g D_g (.) rlk_g,c  (keyswitch.rs:86-95), NTT domain.  One thread per
+// (item, limb i, coefficient j).  Blocks are numbered item-fastest, so the blocks resident at
+// any time share a few 256-coefficient key slices: the key and its Shoup companions
+// (G*2*L*n words each, more than one XCD's L2 at cfg3) come from HBM about once per XCD
+// instead of once per item.  Accumulators stay in [0, 2q); D is canonical.
 __global__ void __launch_bounds__(TPB)
-relin_mac_kernel(const u64* __restrict__ base, const u64* __restrict__ base_off, long base_stride,
-                 const u64* __restrict__ D, const u64* __restrict__ rlk, const u64* __restrict__ rlk_s,
-                 int guse, u64* __restrict__ out, long out_stride, int n, int L,
-                 const PrimeConst* __restrict__ primes) {
-    ROW_SETUP(n)
-    const long item = row / L;
-    const int i = (int)(row - item * L);
+relin_mac_kernel(const u64* __restrict__ base, long base_stride, const u64* __restrict__ D,
+                 const u64* __restrict__ rlk, const u64* __restrict__ rlk_s, int guse, u64* out,
+                 long out_stride, int items, int n, int L, const PrimeConst* __restrict__ primes) {
+    // two consecutive coefficients per thread: 16-byte loads/stores (n is even)
+    const long Ln = (long)L * n;
+    const int it = (int)(blockIdx.x % (unsigned)items);
+    const long coef = ((long)(blockIdx.x / (unsigned)items) * TPB + threadIdx.x) * 2;
+    if (coef >= Ln) return;
+    const int i = (int)(coef / n);
     const PrimeConst& P = primes[i];
     const u64 q = P.q, q2 = P.two_q, nq = (u64)0 - q;
-    const u64* bp = base + (base_off ? (long)base_off[item] : item * base_stride);
-    // accumulators kept in [0, 2q): key is constant, so Shoup with precomputed companions
-    u64 acc0 = bp[(long)i * n + j];
-    u64 acc1 = bp[(long)(L + i) * n + j];
-    const u64* dp = D + item * (long)guse * L * n + (long)i * n + j;
-    const long Ln = (long)L * n;
-    const long ko = (long)i * n + j;
-    for (int g = 0; g < guse; ++g) {
-        const u64 d = dp[g * Ln];
-        const long k0 = (2L * g) * Ln + ko, k1 = k0 + Ln;
-        u64 t = acc0 + shoup_mul_nq(d, rlk[k0], rlk_s[k0], nq);
-        acc0 = t >= q2 ? t - q2 : t;
-        t = acc1 + shoup_mul_nq(d, rlk[k1], rlk_s[k1], nq);
-        acc1 = t >= q2 ? t - q2 : t;
+    typedef ulonglong2 V2;
+    const u64* bp = base + it * base_stride;
+    const V2 b0 = *(const V2*)(bp + coef), b1 = *(const V2*)(bp + Ln + coef);
+    u64 a0x = b0.x, a0y = b0.y, a1x = b1.x, a1y = b1.y;
+    const u64* dp = D + (long)it * guse * Ln + coef;
+    constexpr int U = 4;
+    for (int g0 = 0; g0 < guse; g0 += U) {
+        V2 d[U], w0[U], s0[U], w1[U], s1[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int g = min(g0 + t, guse - 1);  // clamped (re-read) tail, masked below
+            const long k0 = 2L * g * Ln + coef;
+            d[t] = *(const V2*)(dp + (long)g * Ln);
+            w0[t] = *(const V2*)(rlk + k0);
+            s0[t] = *(const V2*)(rlk_s + k0);
+            w1[t] = *(const V2*)(rlk + k0 + Ln);
+            s1[t] = *(const V2*)(rlk_s + k0 + Ln);
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            if (g0 + t < guse) {
+                u64 v = a0x + shoup_mul_nq(d[t].x, w0[t].x, s0[t].x, nq);
+                a0x = v >= q2 ? v - q2 : v;
+                v = a0y + shoup_mul_nq(d[t].y, w0[t].y, s0[t].y, nq);
+                a0y = v >= q2 ? v - q2 : v;
+                v = a1x + shoup_mul_nq(d[t].x, w1[t].x, s1[t].x, nq);
+                a1x = v >= q2 ? v - q2 : v;
+                v = a1y + shoup_mul_nq(d[t].y, w1[t].y, s1[t].y, nq);
+                a1y = v >= q2 ? v - q2 : v;
+            }
+        }
     }
-    u64* op = out + item * out_stride + (long)i * n + j;
-    op[0] = acc0 >= q ? acc0 - q : acc0;
-    op[Ln] = acc1 >= q ? acc1 - q : acc1;
+    u64* op = out + it * out_stride;
+    *(V2*)(op + coef) = make_ulonglong2(a0x >= q ? a0x - q : a0x, a0y >= q ? a0y - q : a0y);
+    *(V2*)(op + Ln + coef) = make_ulonglong2(a1x >= q ? a1x - q : a1x, a1y >= q ? a1y - q : a1y);
 }
 
-void launch_relin_mac(const u64* base, const u64* base_off, long base_stride, long /*base_poly0*/,
-                      const u64* D, const u64* rlk, const u64* rlk_s, int guse, u64* out, long out_stride,
-                      int items, int n, int L, const PrimeConst* primes, hipStream_t s) {
-    const long blocks = (long)items * L * blocks_per_row(n);
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(relin_mac_kernel, dim3(blocks), dim3(TPB), 0, s, base, base_off, base_stride, D,
-                       rlk, rlk_s, guse, out, out_stride, n, L, primes);
+void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
+                      int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
+                      hipStream_t s) {
+    if (items <= 0) return;
+    const long Ln = (long)L * n;
+    const long blocks = (long)items * ((Ln / 2 + TPB - 1) / TPB);
+    hipLaunchKernelGGL(relin_mac_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, base, base_stride, D, rlk, rlk_s,
+                       guse, out, out_stride, items, n, L, primes);
 }
 
 // ---------------------------------------------------------------- pointwise RNS ops
