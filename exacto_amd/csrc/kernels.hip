@@ -245,12 +245,13 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
 
 // ---------------------------------------------------------------- exact lift Q -> P
 
-template <bool NEAR, bool FAST, int LT>
+template <bool NEAR, bool FAST, int LT, int KT>
 __global__ void __launch_bounds__(TPB)
-exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L_arg, int K,
+exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L_arg, int K_arg,
                   const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
-    const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
+    const int L = LT ? LT : L_arg;  // LT/KT > 0: limb counts known at compile time
+    const int K = KT ? KT : K_arg;
     u64 x[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
@@ -272,23 +273,23 @@ void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtT
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s) {
     const long blocks = (long)items * 4 * blocks_per_row(n);
     if (blocks == 0) return;
-#define LIFT(NR, FS, LT)                                                                                      \
-    hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
+#define LIFT(NR, FS, LT, KT)                                                                                     \
+    hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
                        primes)
     if (mode == 2) {
         switch (L) {
-            case 1: LIFT(true, true, 1); break;
-            case 2: LIFT(true, true, 2); break;
-            case 3: LIFT(true, true, 3); break;
-            case 4: LIFT(true, true, 4); break;
-            case 5: LIFT(true, true, 5); break;
-            case 6: LIFT(true, true, 6); break;
-            default: LIFT(true, true, 0); break;
+            case 1: if (K == 2) LIFT(true, true, 1, 2); else LIFT(true, true, 1, 0); break;
+            case 2: if (K == 3) LIFT(true, true, 2, 3); else LIFT(true, true, 2, 0); break;
+            case 3: if (K == 4) LIFT(true, true, 3, 4); else LIFT(true, true, 3, 0); break;
+            case 4: if (K == 5) LIFT(true, true, 4, 5); else LIFT(true, true, 4, 0); break;
+            case 5: if (K == 6) LIFT(true, true, 5, 6); else LIFT(true, true, 5, 0); break;
+            case 6: if (K == 7) LIFT(true, true, 6, 7); else LIFT(true, true, 6, 0); break;
+            default: LIFT(true, true, 0, 0); break;
         }
     } else if (mode == 1) {
-        LIFT(true, false, 0);
+        LIFT(true, false, 0, 0);
     } else {
-        LIFT(false, false, 0);
+        LIFT(false, false, 0, 0);
     }
 #undef LIFT
 }
@@ -361,13 +362,14 @@ void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n
 
 // ---------------------------------------------------------------- exact scale-and-round
 
-template <bool NEAR, bool FAST, int LT>
+template <bool NEAR, bool FAST, int LT, int KT>
 __global__ void __launch_bounds__(TPB)
 exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                   u64* __restrict__ D, int guse, int n, int L_arg, int K,
+                   u64* __restrict__ D, int guse, int n, int L_arg, int K_arg,
                    const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
-    const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
+    const int L = LT ? LT : L_arg;  // LT/KT > 0: limb counts known at compile time
+    const int K = KT ? KT : K_arg;
     const int NP = L + K;
     const long item = row / 3;
     const int comp = (int)(row - item * 3);
@@ -449,23 +451,23 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
                         int K, int mode, hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-#define SCALE(NR, FS, LT)                                                                                     \
-    hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
+#define SCALE(NR, FS, LT, KT)                                                                                    \
+    hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
                        D, guse, n, L, K, ct, primes)
     if (mode == 2) {
         switch (L) {
-            case 1: SCALE(true, true, 1); break;
-            case 2: SCALE(true, true, 2); break;
-            case 3: SCALE(true, true, 3); break;
-            case 4: SCALE(true, true, 4); break;
-            case 5: SCALE(true, true, 5); break;
-            case 6: SCALE(true, true, 6); break;
-            default: SCALE(true, true, 0); break;
+            case 1: if (K == 2) SCALE(true, true, 1, 2); else SCALE(true, true, 1, 0); break;
+            case 2: if (K == 3) SCALE(true, true, 2, 3); else SCALE(true, true, 2, 0); break;
+            case 3: if (K == 4) SCALE(true, true, 3, 4); else SCALE(true, true, 3, 0); break;
+            case 4: if (K == 5) SCALE(true, true, 4, 5); else SCALE(true, true, 4, 0); break;
+            case 5: if (K == 6) SCALE(true, true, 5, 6); else SCALE(true, true, 5, 0); break;
+            case 6: if (K == 7) SCALE(true, true, 6, 7); else SCALE(true, true, 6, 0); break;
+            default: SCALE(true, true, 0, 0); break;
         }
     } else if (mode == 1) {
-        SCALE(true, false, 0);
+        SCALE(true, false, 0, 0);
     } else {
-        SCALE(false, false, 0);
+        SCALE(false, false, 0, 0);
     }
 #undef SCALE
 }
