@@ -578,6 +578,28 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     return 0;
 }
 
+static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt) {
+    const int NP = c->L + c->K;
+    ProfRec rec{};
+    if (c->prof) {
+        HIP_TRY(hipEventCreate(&rec.a));
+        HIP_TRY(hipEventCreate(&rec.b));
+        HIP_TRY(hipEventRecord(rec.a, c->stream));
+    }
+    bool lazy = true;
+    for (int t = 0; t < NP; ++t) lazy &= c->primes[t] < (1ull << 60);
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (c->prof) {
+        HIP_TRY(hipEventRecord(rec.b, c->stream));
+        rec.kind = 2;  // fused tensor + inverse
+        rec.polys = (u64)cnt * 3 * NP;
+        rec.bytes = 8.0 * c->n * 11.0 * cnt * NP;  // 8 operand reads + 3 writes per (item, prime)
+        c->recs.push_back(rec);
+    }
+    return 0;
+}
+
 static NttBatch contiguous(u64* data, long count_items, long poly_per_item, int prime_base, int period,
                            int n) {
     (void)count_items;
@@ -662,11 +684,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         CHECK_LAUNCH();
         // 3. forward NTT of the extended polynomials
         if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
-        // 4. tensor product in every prime
-        launch_tensor(o, c->ws_extP, c->ws_T, cnt, n, L, K, c->d_primes, c->stream);
-        CHECK_LAUNCH();
-        // 5. back to coefficients
-        if (int e = run_ntt(c, contiguous(c->ws_T, cnt, 3L * NP, 0, NP, n), (long)cnt * 3 * NP, true)) return e;
+        // 4+5. tensor product in every prime, fused into the inverse NTT of its components
+        if (int e = run_inv_tensor(c, o, cnt)) return e;
         // 6. scale-and-round (+ gadget digits of the third component)
         u64* R = out + s * out_stride;
         const int ncomp = relin ? 2 : 3;

@@ -91,12 +91,13 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
     long b_stride;
 };
 
+// Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
+void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
+                       const PrimeConst* primes, hipStream_t s);
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
-void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
-                   const PrimeConst* primes, hipStream_t s);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s);

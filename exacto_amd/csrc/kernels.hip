@@ -14,6 +14,8 @@
 // consecutive lanes touch consecutive 8-byte words of one residue polynomial.
 #include "exacto_internal.hpp"
 
+#include <cstdlib>
+
 namespace exacto {
 
 static constexpr int TPB = 256;
@@ -322,44 +324,6 @@ void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const Prim
     hipLaunchKernelGGL(hps_extend_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, K, primes);
 }
 
-// ---------------------------------------------------------------- tensor product
-
-__global__ void __launch_bounds__(TPB)
-tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ T, int n, int L, int K,
-              const PrimeConst* __restrict__ primes) {
-    ROW_SETUP(n)
-    const int NP = L + K;
-    const long item = row / NP;
-    const int t = (int)(row - item * NP);
-    const PrimeConst& P = primes[t];
-    u64 a0, a1, b0, b1;
-    if (t < L) {
-        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
-        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
-        a0 = A[(long)t * n + j];
-        a1 = A[(long)(L + t) * n + j];
-        b0 = B[(long)t * n + j];
-        b1 = B[(long)(L + t) * n + j];
-    } else {
-        const u64* E = extP + item * 4 * K * n + (long)(t - L) * n + j;
-        a0 = E[0];
-        a1 = E[(long)K * n];
-        b0 = E[2L * K * n];
-        b1 = E[3L * K * n];
-    }
-    u64* out = T + (item * 3 * NP + t) * n + j;
-    out[0] = mul_mod(a0, b0, P);
-    out[(long)NP * n] = add_mod(mul_mod(a0, b1, P), mul_mod(a1, b0, P), P.q);
-    out[2L * NP * n] = mul_mod(a1, b1, P);
-}
-
-void launch_tensor(const Operands& op, const u64* extP, u64* T, int items, int n, int L, int K,
-                   const PrimeConst* primes, hipStream_t s) {
-    const long blocks = (long)items * (L + K) * blocks_per_row(n);
-    if (blocks == 0) return;
-    hipLaunchKernelGGL(tensor_kernel, dim3(blocks), dim3(TPB), 0, s, op, extP, T, n, L, K, primes);
-}
-
 // ---------------------------------------------------------------- exact scale-and-round
 
 template <bool NEAR, bool FAST, int LT, int KT>
@@ -626,11 +590,74 @@ relin_mac_kernel(const u64* __restrict__ base, long base_stride, const u64* __re
     *(V2*)(op + Ln + coef) = make_ulonglong2(a1x >= q ? a1x - q : a1x, a1y >= q ? a1y - q : a1y);
 }
 
+// Same MAC with the key slice staged in LDS: a block owns 64 consecutive coefficients of one
+// limb and MAC_IG items; its key words and Shoup companions for every digit (guse * 2 KiB) are
+// read from HBM once and then served from LDS, so global traffic is D + base + out only.
+// Wave w of the block handles items it0 + w, it0 + w + 4, ...; lane = coefficient.
+constexpr int MAC_LS = 64;   // coefficients per block
+constexpr int MAC_IG = 64;   // items per block
+constexpr int MAC_GMAX = 32; // digits staged (LDS = 2 KiB per digit)
+
+__global__ void __launch_bounds__(TPB)
+relin_mac_lds_kernel(const u64* __restrict__ base, long base_stride, const u64* __restrict__ D,
+                     const u64* __restrict__ rlk, const u64* __restrict__ rlk_s, int guse, u64* out,
+                     long out_stride, int items, int n, int L, const PrimeConst* __restrict__ primes) {
+    extern __shared__ u64 ks[];  // [guse][4][MAC_LS]: w0, ws0, w1, ws1
+    const long Ln = (long)L * n;
+    const long c0 = (long)blockIdx.x * MAC_LS;  // first coefficient (flat limb*n + j)
+    const int lane = threadIdx.x & (MAC_LS - 1), wave = threadIdx.x / MAC_LS;
+    for (int r = threadIdx.x; r < guse * 4 * MAC_LS; r += TPB) {
+        const int g = r / (4 * MAC_LS), w = (r / MAC_LS) & 3, l = r & (MAC_LS - 1);
+        const long kk = (2L * g + (w >> 1)) * Ln + c0 + l;
+        ks[r] = (w & 1) ? rlk_s[kk] : rlk[kk];
+    }
+    __syncthreads();
+    const long coef = c0 + lane;
+    const int i = (int)(coef / n);
+    const PrimeConst& P = primes[i];
+    const u64 q = P.q, q2 = P.two_q, nq = (u64)0 - q;
+    const int it_end = min(items, (int)(blockIdx.y + 1) * MAC_IG);
+    for (int it = blockIdx.y * MAC_IG + wave; it < it_end; it += TPB / MAC_LS) {
+        const u64* bp = base + it * base_stride;
+        u64 a0 = bp[coef], a1 = bp[Ln + coef];
+        const u64* dp = D + (long)it * guse * Ln + coef;
+        constexpr int U = 4;
+        for (int g0 = 0; g0 < guse; g0 += U) {
+            u64 d[U];
+#pragma unroll
+            for (int t = 0; t < U; ++t) d[t] = dp[(long)min(g0 + t, guse - 1) * Ln];
+#pragma unroll
+            for (int t = 0; t < U; ++t) {
+                if (g0 + t < guse) {
+                    const u64* kg = ks + (g0 + t) * 4 * MAC_LS + lane;
+                    u64 v = a0 + shoup_mul_nq(d[t], kg[0], kg[MAC_LS], nq);
+                    a0 = v >= q2 ? v - q2 : v;
+                    v = a1 + shoup_mul_nq(d[t], kg[2 * MAC_LS], kg[3 * MAC_LS], nq);
+                    a1 = v >= q2 ? v - q2 : v;
+                }
+            }
+        }
+        u64* op = out + it * out_stride;
+        op[coef] = a0 >= q ? a0 - q : a0;
+        op[Ln + coef] = a1 >= q ? a1 - q : a1;
+    }
+}
+
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
                       hipStream_t s) {
     if (items <= 0) return;
     const long Ln = (long)L * n;
+    static const int use_lds = [] {
+        const char* e = getenv("EXACTO_MAC_LDS");
+        return e ? atoi(e) : 1;
+    }();
+    if (use_lds && guse <= MAC_GMAX && Ln % MAC_LS == 0) {
+        const dim3 grid((unsigned)(Ln / MAC_LS), (unsigned)((items + MAC_IG - 1) / MAC_IG));
+        hipLaunchKernelGGL(relin_mac_lds_kernel, grid, dim3(TPB), (size_t)guse * 4 * MAC_LS * sizeof(u64), s, base,
+                           base_stride, D, rlk, rlk_s, guse, out, out_stride, items, n, L, primes);
+        return;
+    }
     const long blocks = (long)items * ((Ln / 2 + TPB - 1) / TPB);
     hipLaunchKernelGGL(relin_mac_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, base, base_stride, D, rlk, rlk_s,
                        guse, out, out_stride, items, n, L, primes);

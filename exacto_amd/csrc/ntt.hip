@@ -123,7 +123,9 @@ __device__ __forceinline__ void fwd_round_direct(u64 (&x)[16], int tid, TwTab ta
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
         for (int g = 0; g < (8 >> lb); ++g) {
-            const TwPair t = ld_tw(tab, base + g);
+            // generic (flat) load: the scheduler keeps it next to its use instead of clustering
+            // a whole round's twiddles (the fused key switch has no VGPRs to spare)
+            const TwPair t = ((const TwPair*)tab)[base + g];
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m;
@@ -145,19 +147,23 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTa
     constexpr int BHI = LOGN - 1 - 4 * R;
     TwPair tw[15];
     if constexpr (PRELOAD) load_round_tw<LOGN, LO, BHI, LO>(tw, tid, tab);  // in flight across the exchange
+    int t2 = tid;
+    // direct-twiddle (fused key switch) callers run this inside a loop: stop the exchange and
+    // twiddle addresses derived from tid being hoisted out of it and spilled
+    if constexpr (!PRELOAD) asm volatile("" : "+v"(t2));
     if constexpr (R > 0) {
         constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
         lds_barrier();
-        lds_store<PLO>(lds, x, tid);
+        lds_store<PLO>(lds, x, t2);
         lds_barrier();
-        lds_load<LO>(lds, x, tid);
+        lds_load<LO>(lds, x, t2);
         if constexpr (LAZY) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) x[k] = x[k] >= q8 ? x[k] - q8 : x[k];
         }
     }
     if constexpr (PRELOAD) fwd_round<LOGN, LO, BHI, LO, LAZY>(x, tw, nq, q2);
-    else fwd_round_direct<LOGN, LO, BHI, LO, LAZY>(x, tid, tab, nq, q2);
+    else fwd_round_direct<LOGN, LO, BHI, LO, LAZY>(x, t2, tab, nq, q2);
     if constexpr (LO > 0) fwd_rounds<LOGN, R + 1, LAZY, PRELOAD>(x, lds, tid, tab, nq, q2, q8);
 }
 
@@ -367,6 +373,86 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
+// ---------------------------------------------------------------- tensor product + inverse
+
+// Degree-2 tensor of two degree-1 ciphertexts fused into the inverse transform of its
+// components (eval.rs:186-198 for HPS, the exact tensor of A22 for the generic path):
+// block = (item, component c, prime t), laid out like T[item][c][t][n].
+//   c0 = a0*b0,  c1 = a0*b1 + a1*b0,  c2 = a1*b1   (pointwise, NTT domain)
+// Operands of prime t < L come from the ciphertexts, of the auxiliary primes from extP
+// ([item][a0,a1,b0,b1][K][n], already forward-transformed).  LAZY products skip Barrett's
+// final corrections (< 3q) and c1 is brought under 4q: the inverse rounds' input bound.
+__device__ __forceinline__ u64 barrett_mul_lazy(u64 a, u64 b, const PrimeConst& P) {
+    const u64 hi = __umul64hi(a, b), lo = a * b;
+    const int s = P.bar_s;
+    const u64 xs = (lo >> (s - 1)) | (hi << (65 - s));
+    const u64 qhat = ((xs * P.bar_mu) >> (s + 1)) | (__umul64hi(xs, P.bar_mu) << (63 - s));
+    return lo - qhat * P.q;  // < 3q
+}
+
+template <int LOGN, bool LAZY>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
+                      const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    if (tid >= T) return;
+    const int NP = L + K;
+    const long p = blockIdx.x;
+    const long item = p / (3 * NP);
+    const int rem = (int)(p - item * 3 * NP);
+    const int c = rem / NP, t = rem - c * NP;
+    const PrimeConst& P = primes[t];
+    const u64 *A0, *A1, *B0, *B1;
+    if (t < L) {
+        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
+        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
+        A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
+        B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
+    } else {
+        const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
+        A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
+    }
+    auto mulr = [&](u64 a, u64 b) { return LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P); };
+    auto load = [&](const u64* src, u64 (&v)[16]) {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 w = s2[k];
+            v[2 * k] = w.x;
+            v[2 * k + 1] = w.y;
+        }
+    };
+    u64 x[16], y[16];
+    if (c != 1) {
+        load(c == 0 ? A0 : A1, x);
+        load(c == 0 ? B0 : B1, y);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = mulr(x[k], y[k]);
+    } else {
+        u64 z[16];
+        load(A0, x);
+        load(B1, y);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) z[k] = mulr(x[k], y[k]);
+        load(A1, x);
+        load(B0, y);
+        const u64 q = P.q, q2 = P.two_q;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u64 v = z[k] + mulr(x[k], y[k]);
+            x[k] = LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
+        }
+    }
+    inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
+    u64* dst = Tout + p * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
 // ---------------------------------------------------------------- fused key switching
 
 // One workgroup per (product, limb i) of relinearize (keyswitch.rs:86-95):
@@ -487,6 +573,38 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
     else
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
+}
+
+template <int LOGN>
+static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
+                      const PrimeConst* primes, hipStream_t s) {
+    constexpr int threads = (1 << LOGN) / 16;
+    if (lazy)
+        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L, K,
+                           primes);
+    else
+        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L,
+                           K, primes);
+}
+
+void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
+                       const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items * 3 * (L + K);
+    if (blocks == 0) return;
+    switch (logn) {
+        case 4: launch_it<4>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 5: launch_it<5>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 6: launch_it<6>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 7: launch_it<7>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 8: launch_it<8>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        default: break;
+    }
 }
 
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
