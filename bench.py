@@ -227,6 +227,15 @@ def main():
         "polys_per_step": dom["polys"],
         "ntt_share_of_step": round((fwd["ms"] + inv["ms"]) / ms_per_step, 3),
     }
+    # HBM bytes per launch from the committed PMC pass over this same bench configuration
+    # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch, gfx950 corrections), as
+    # its measured traffic/algorithmic ratio applied to this run's algorithmic bytes per launch
+    tfile = os.path.join(ROOT, "profiles", f"r1_{args.config}_fwd_traffic.json")
+    if dom_name.startswith("ntt_fwd") and os.path.exists(tfile):
+        with open(tfile) as f:
+            tr = json.load(f)
+        roofline["traffic"] = round(tr["traffic_over_algorithmic"] * roofline["bytes_per_launch"], 1)
+        roofline["traffic_source"] = os.path.relpath(tfile, ROOT)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cfg3":
