@@ -169,12 +169,11 @@ def main():
 
             def step():
                 # depth-`depth` chain: acc <- dbfv_mul(acc, y), mul_depth reset before every step
-                # (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220)
-                src = x
-                for k in range(depth):
-                    dst = bufs[k % 2]
-                    ctx.dbfv_mul_dev(d, base, dplain, src, y, dst, B)
-                    src = dst
+                # (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220), one native call
+                if depth == 1:
+                    ctx.dbfv_mul_dev(d, base, dplain, x, y, bufs[0], B)
+                else:
+                    ctx.dbfv_mul_chain_dev(d, base, dplain, x, y, bufs[0], B, depth)
             units_per_step = B
             unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
             metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else \

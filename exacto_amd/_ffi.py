@@ -75,6 +75,14 @@ _SIGS = [
     ("exacto_gadget_decompose_dev", [_P, _P, _P, _SZ, _SZ], C.c_int),
     ("exacto_dbfv_mul", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
     ("exacto_dbfv_mul_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
+    ("exacto_dbfv_mul_chain", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_bfv_decrypt", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_decrypt_dev", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_dbfv_decrypt", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_dbfv_decrypt_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_dbfv_decrypt_poly", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_dbfv_decrypt_poly_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_dbfv_mul_chain_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -248,6 +256,38 @@ class HipContext:
                                         out.ctypes.data, B, _ptr(da), _ptr(db), dout.ctypes.data))
         return out, dout
 
+    def dbfv_mul_chain(self, d, base, plain, x: np.ndarray, y: np.ndarray, depth: int):
+        """paper_repro.rs:203-236 chain: x * y^depth, mul_depth reset before every step."""
+        x, y = _u64(x), _u64(y)
+        out = np.zeros_like(x)
+        check(self._lib.exacto_dbfv_mul_chain(self._h, d, base, plain, x.ctypes.data, y.ctypes.data,
+                                              out.ctypes.data, x.shape[0], depth))
+        return out
+
+    def bfv_decrypt(self, ct: np.ndarray, sk: np.ndarray) -> np.ndarray:
+        """encrypt.rs:111-178 batched: ct [B][polys][L][n], sk [L][n] (NTT) -> [B][n] mod p."""
+        ct, sk = _u64(ct), _u64(sk)
+        out = np.zeros((ct.shape[0], ct.shape[-1]), dtype=np.uint64)
+        check(self._lib.exacto_bfv_decrypt(self._h, ct.ctypes.data, ct.shape[1], sk.ctypes.data,
+                                           out.ctypes.data, ct.shape[0]))
+        return out
+
+    def dbfv_decrypt(self, d, base, plain, ct: np.ndarray, sk: np.ndarray) -> np.ndarray:
+        """dbfv/decrypt.rs:20-43: ct [B][d][2][L][n] -> [B] scalars."""
+        ct, sk = _u64(ct), _u64(sk)
+        out = np.zeros(ct.shape[0], dtype=np.uint64)
+        check(self._lib.exacto_dbfv_decrypt(self._h, d, base, plain, ct.ctypes.data, sk.ctypes.data,
+                                            out.ctypes.data, ct.shape[0]))
+        return out
+
+    def dbfv_decrypt_poly(self, d, base, plain, ct: np.ndarray, sk: np.ndarray) -> np.ndarray:
+        """dbfv/decrypt.rs:48-79: ct [B][d][2][L][n] -> [B][n] mod p."""
+        ct, sk = _u64(ct), _u64(sk)
+        out = np.zeros((ct.shape[0], ct.shape[-1]), dtype=np.uint64)
+        check(self._lib.exacto_dbfv_decrypt_poly(self._h, d, base, plain, ct.ctypes.data, sk.ctypes.data,
+                                                 out.ctypes.data, ct.shape[0]))
+        return out
+
     # ---- device-pointer API (asynchronous; torch tensors or raw ints)
     def _p(self, x):
         return x if isinstance(x, int) else _ptr(x)
@@ -308,6 +348,17 @@ class HipContext:
         db = np.ascontiguousarray(depth_b, dtype=np.uint32) if depth_b is not None else None
         check(self._lib.exacto_dbfv_mul_dev(self._h, d, base, plain, self._p(a), self._p(b),
                                             self._p(out), batch, _ptr(da), _ptr(db), None))
+
+    def dbfv_mul_chain_dev(self, d, base, plain, x, y, out, batch, depth):
+        check(self._lib.exacto_dbfv_mul_chain_dev(self._h, d, base, plain, self._p(x), self._p(y),
+                                                  self._p(out), batch, depth))
+
+    def bfv_decrypt_dev(self, ct, polys, sk, out, batch):
+        check(self._lib.exacto_bfv_decrypt_dev(self._h, self._p(ct), polys, self._p(sk), self._p(out), batch))
+
+    def dbfv_decrypt_dev(self, d, base, plain, ct, sk, out, batch, poly=False):
+        fn = self._lib.exacto_dbfv_decrypt_poly_dev if poly else self._lib.exacto_dbfv_decrypt_dev
+        check(fn(self._h, d, base, plain, self._p(ct), self._p(sk), self._p(out), batch))
 
     # ---- profiling
     def prof_enable(self, on=True):

@@ -191,6 +191,12 @@ struct exacto_ctx {
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
     size_t ws_items = 0;
     u64 *ws_coefQ = nullptr, *ws_extP = nullptr, *ws_T = nullptr, *ws_D = nullptr;
+    u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
+    size_t chain_bytes = 0;
+    u64* dec_buf = nullptr;    // decryption phase [B][L][n]
+    size_t dec_bytes = 0;
+    u64* dig_buf = nullptr;    // dBFV decrypted digits [B][d][n]
+    size_t dig_bytes = 0;
     // staging for host-pointer API and dBFV products
     u64* io = nullptr;
     size_t io_bytes = 0;
@@ -310,6 +316,7 @@ static int build_tables(exacto_ctx* c) {
         set_shoup(C.pmod_w[t], C.pmod_ws[t], c->plain % pt, pt);
     }
     for (int i = 0; i < L && i < (int)Q.w.size(); ++i) C.Qwords[i] = Q.w[i];
+    for (int t = 0; t < NP; ++t) C.hq[t] = H.mod(c->primes[t]);
     if (c->path == EXACTO_PATH_HPS) {
         const u64 q = qv[0];
         for (int a = 0; a < K && a < 2; ++a) C.hps_qinv[a] = invmod_h(q % pv[a], pv[a]);
@@ -478,7 +485,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
-    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D);
+    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -995,23 +1002,26 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
     return 0;
 }
 
+// DbfvParams::new checks (params/mod.rs:168-184)
+static int dbfv_params_check(size_t d, uint64_t base, uint64_t plain) {
+    if (base < 2) return invalid_param("base must be >= 2");
+    if (d < 1) return invalid_param("num_digits must be >= 1");
+    u128 bd = 1;
+    const u128 sat = ~(u128)0;
+    for (size_t i = 0; i < d; ++i) bd = (bd > sat / base) ? sat : bd * base;
+    const u128 p128 = plain == 0 ? ((u128)1 << 64) : (u128)plain;
+    if (bd < p128) {
+        auto u128s = [](u128 v) { std::string s; do { s.insert(s.begin(), char('0' + (int)(v % 10))); v /= 10; } while (v); return s; };
+        return invalid_param("base^digits = " + u128s(bd) + " < plain_modulus = " + u128s(p128));
+    }
+    return 0;
+}
+
 extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
                                    const uint64_t* b, uint64_t* out, size_t B, const uint32_t* depth_a,
                                    const uint32_t* depth_b, uint32_t* depth_out) {
     if (int e = check_ctx(c)) return e;
-    // DbfvParams::new checks (params/mod.rs:168-184)
-    if (base < 2) return invalid_param("base must be >= 2");
-    if (d < 1) return invalid_param("num_digits must be >= 1");
-    {
-        u128 bd = 1;
-        const u128 sat = ~(u128)0;
-        for (size_t i = 0; i < d; ++i) bd = (bd > sat / base) ? sat : bd * base;
-        const u128 p128 = plain == 0 ? ((u128)1 << 64) : (u128)plain;
-        if (bd < p128) {
-            auto u128s = [](u128 v) { std::string s; do { s.insert(s.begin(), char('0' + (int)(v % 10))); v /= 10; } while (v); return s; };
-            return invalid_param("base^digits = " + u128s(bd) + " < plain_modulus = " + u128s(p128));
-        }
-    }
+    if (int e = dbfv_params_check(d, base, plain)) return e;
     // depth guard (dbfv/eval.rs:96-102)
     for (size_t i = 0; i < B; ++i) {
         const uint32_t da = depth_a ? depth_a[i] : 0, db = depth_b ? depth_b[i] : 0;
@@ -1037,6 +1047,125 @@ extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint6
     if (depth_out)
         for (size_t i = 0; i < B; ++i) depth_out[i] = 1;
     return 0;
+}
+
+// ============================================================== decryption
+
+// bfv/encrypt.rs:111-178 for a batch: phase = sum_k c_k s^k (NTT domain), INTT, exact rounding.
+// ct = [B][polys][L][n] (stride ct_stride words per ciphertext), sk = [L][n] NTT domain.
+static int decrypt_batch(exacto_ctx* c, const u64* ct, size_t polys, long ct_stride, const u64* sk, u64* out,
+                         size_t B) {
+    if (polys < 1) return invalid_param("ciphertext has no polynomials");
+    if (B == 0) return 0;
+    const int L = c->L, n = c->n;
+    if (L >= 2 && (c->K < 1 || c->plain >= c->primes[L]))
+        return fail(EXACTO_ERR_NOT_IMPLEMENTED, "not yet implemented: GPU decryption needs plain_modulus below the "
+                                                "first internal auxiliary prime");
+    size_t cap = c->dec_bytes;
+    if (grow(&c->dec_buf, &cap, B * L * poly_bytes(c))) return EXACTO_ERR_HIP;
+    c->dec_bytes = cap;
+    launch_phase(ct, (int)polys, ct_stride, sk, c->dec_buf, (int)B, n, L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = run_ntt(c, contiguous(c->dec_buf, (long)B, L, 0, L, n), (long)B * L, true)) return e;
+    launch_decrypt_round(c->dec_buf, out, (int)B, n, L, c->d_crt, c->d_primes, c->plain, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_bfv_decrypt_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* sk,
+                                      uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    return decrypt_batch(c, ct, polys, (long)polys * c->L * c->n, sk, out, B);
+}
+
+extern "C" int exacto_bfv_decrypt(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* sk,
+                                  uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{ct, B * polys * c->L * poly_bytes(c)}, {sk, c->L * poly_bytes(c)}}, B * poly_bytes(c), out,
+                     [&](std::vector<u64*>& dv, u64* o) { return exacto_bfv_decrypt_dev(c, dv[0], polys, dv[1], o, B); });
+}
+
+// dbfv/decrypt.rs:20-79: every limb decrypted with the BFV plaintext modulus t, then signed
+// recomposition mod p coefficient-wise (poly) or of coefficient 0 (scalar).
+static int dbfv_decrypt_common(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* ct,
+                               const uint64_t* sk, uint64_t* out, size_t B, bool scalar) {
+    if (int e = check_ctx(c)) return e;
+    if (int e = dbfv_params_check(d, base, plain)) return e;
+    if (!scalar && plain == 0)
+        return invalid_param("polynomial dBFV decrypt requires finite plain_modulus (plain_modulus=0 is scalar-only)");
+    if (B == 0) return 0;
+    const size_t nd = B * d;
+    size_t cap = c->dig_bytes;
+    if (grow(&c->dig_buf, &cap, nd * poly_bytes(c))) return EXACTO_ERR_HIP;
+    c->dig_bytes = cap;
+    if (int e = decrypt_batch(c, ct, 2, 2L * c->L * c->n, sk, c->dig_buf, nd)) return e;
+    launch_dbfv_recompose(c->dig_buf, out, (int)B, c->n, (int)d, base, plain, c->plain, scalar, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_dbfv_decrypt_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* ct,
+                                       const uint64_t* sk, uint64_t* out, size_t B) {
+    return dbfv_decrypt_common(c, d, base, plain, ct, sk, out, B, true);
+}
+
+extern "C" int exacto_dbfv_decrypt_poly_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
+                                            const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t B) {
+    return dbfv_decrypt_common(c, d, base, plain, ct, sk, out, B, false);
+}
+
+extern "C" int exacto_dbfv_decrypt(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* ct,
+                                   const uint64_t* sk, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{ct, B * d * 2 * c->L * poly_bytes(c)}, {sk, c->L * poly_bytes(c)}}, B * sizeof(u64), out,
+                     [&](std::vector<u64*>& dv, u64* o) {
+                         return exacto_dbfv_decrypt_dev(c, d, base, plain, dv[0], dv[1], o, B);
+                     });
+}
+
+extern "C" int exacto_dbfv_decrypt_poly(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
+                                        const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{ct, B * d * 2 * c->L * poly_bytes(c)}, {sk, c->L * poly_bytes(c)}}, B * poly_bytes(c), out,
+                     [&](std::vector<u64*>& dv, u64* o) {
+                         return exacto_dbfv_decrypt_poly_dev(c, d, base, plain, dv[0], dv[1], o, B);
+                     });
+}
+
+// dBFV multiplication chain with the guard-bypass semantics of paper_repro.rs:203-236 (and the
+// chain of bfv_host.rs:258-288 without its bootstrap): acc <- dbfv_mul(acc, y) `depth` times,
+// both mul_depth reset to 0 before every step; intermediates ping-pong between two
+// context-owned device buffers and never leave HBM.
+extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
+                                         const uint64_t* x, const uint64_t* y, uint64_t* out, size_t B,
+                                         size_t depth) {
+    if (int e = check_ctx(c)) return e;
+    const size_t bytes = B * d * 2 * c->L * poly_bytes(c);
+    if (depth == 0) {
+        if (B && out != x) HIP_TRY(hipMemcpyAsync(out, x, bytes, hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    }
+    if (depth > 1 && B) {
+        size_t cap = c->chain_bytes;
+        if (grow(&c->chain_buf, &cap, 2 * bytes)) return EXACTO_ERR_HIP;
+        c->chain_bytes = cap;
+    }
+    const uint64_t* src = x;
+    for (size_t k = 0; k < depth; ++k) {
+        uint64_t* dst = (k + 1 == depth) ? out : c->chain_buf + (k % 2) * (bytes / sizeof(u64));
+        if (int e = exacto_dbfv_mul_dev(c, d, base, plain, src, y, dst, B, nullptr, nullptr, nullptr)) return e;
+        src = dst;
+    }
+    return 0;
+}
+
+extern "C" int exacto_dbfv_mul_chain(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* x,
+                                     const uint64_t* y, uint64_t* out, size_t B, size_t depth) {
+    if (!c) return invalid_param("null context");
+    const size_t bytes = B * d * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{x, bytes}, {y, bytes}}, bytes, out, [&](std::vector<u64*>& dv, u64* o) {
+        return exacto_dbfv_mul_chain_dev(c, d, base, plain, dv[0], dv[1], o, B, depth);
+    });
 }
 
 extern "C" int exacto_dbfv_mul(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,

@@ -54,6 +54,7 @@ struct CrtTables {
     int digit_small;  // gadget base <= every ciphertext prime: digit magnitudes are already reduced
     u64 pmod_w[EXACTO_MAX_PRIMES], pmod_ws[EXACTO_MAX_PRIMES];  // plain mod prime_t
     u64 Qwords[EXACTO_MAX_L];                   // Q as little-endian 64-bit words
+    u64 hq[EXACTO_MAX_PRIMES];                  // floor(Q/2) mod prime_t (decryption rounding)
     // HPS (single q, 1 or 2 aux primes), eval.rs:257-413
     u64 hps_qinv[2];        // q^-1 mod p_j
     u64 hps_p1_inv_p0, hps_p0_inv_p1;
@@ -94,6 +95,13 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
                        const PrimeConst* primes, hipStream_t s);
+// Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
+void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
+                  const PrimeConst* primes, hipStream_t s);
+void launch_decrypt_round(const u64* X, u64* out, int items, int n, int L, const CrtTables* ct,
+                          const PrimeConst* primes, u64 plain, hipStream_t s);
+void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d, u64 base, u64 plain, u64 t,
+                           bool scalar, hipStream_t s);
 void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,

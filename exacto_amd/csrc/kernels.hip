@@ -436,6 +436,118 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
 #undef SCALE
 }
 
+// ---------------------------------------------------------------- decryption
+
+// phase = sum_k c_k * s^k (encrypt.rs:115-123), NTT domain, one thread per (item, limb, coeff).
+__global__ void __launch_bounds__(TPB)
+phase_kernel(const u64* __restrict__ ct, int polys, long ct_stride, const u64* __restrict__ sk,
+             u64* __restrict__ out, int n, int L, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const long item = row / L;
+    const int i = (int)(row - item * L);
+    const PrimeConst& P = primes[i];
+    const long Ln = (long)L * n;
+    const u64* c = ct + item * ct_stride + (long)i * n + j;
+    const u64 s = sk[(long)i * n + j];
+    u64 acc = c[0], sp = s;
+    for (int k = 1; k < polys; ++k) {
+        acc = add_mod(acc, mul_mod(c[k * Ln], sp, P), P.q);
+        if (k + 1 < polys) sp = mul_mod(sp, s, P);
+    }
+    out[row * n + j] = acc;
+}
+
+void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
+                  const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items * L * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(phase_kernel, dim3(blocks), dim3(TPB), 0, s, ct, polys, ct_stride, sk, out, n, L, primes);
+}
+
+// m = floor((x p + floor(Q/2)) / Q) mod p for x = CRT(phase) in [0, Q) (encrypt.rs:145-171),
+// one thread per (item, coefficient).  L = 1: one 128-by-64 division.  L >= 2: in RNS, with
+// s = (p x + floor(Q/2)) mod Q from its Garner digits and r = (p x + floor(Q/2) - s) / Q
+// evaluated in the first auxiliary prime P0 > p, where it is exact because 0 <= r <= p.
+__global__ void __launch_bounds__(TPB)
+decrypt_round_kernel(const u64* __restrict__ X, u64* __restrict__ out, int n, int L,
+                     const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes, u64 plain) {
+    ROW_SETUP(n)
+    u64 r;
+    if (L == 1) {
+        const u64 q = primes[0].q;
+        const u128 y = (u128)X[row * n + j] * plain + (q >> 1);
+        r = (u64)(y / q);
+    } else {
+        u64 x[EXACTO_MAX_L], s[EXACTO_MAX_L], vx[EXACTO_MAX_L], vs[EXACTO_MAX_L];
+#pragma unroll
+        for (int i = 0; i < EXACTO_MAX_L; ++i) {
+            if (i < L) {
+                const u64 qi = primes[i].q;
+                x[i] = X[(row * L + i) * n + j];
+                s[i] = add_mod(shoup_mul_red(x[i], C->pmod_w[i], C->pmod_ws[i], qi), C->hq[i], qi);
+            }
+        }
+        garner_q<false>(vx, x, L, C, primes);
+        garner_q<false>(vs, s, L, C, primes);
+        const int t = L;
+        const PrimeConst& P0 = primes[t];
+        const u64 p0 = P0.q;
+        const u64 xP = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, false>(vx, L, false, &C->qpref_w[0][0],
+                                                                       &C->qpref_ws[0][0], t, P0);
+        const u64 sP = mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, false>(vs, L, false, &C->qpref_w[0][0],
+                                                                       &C->qpref_ws[0][0], t, P0);
+        const u64 a = shoup_mul_red(xP, C->pq_w[0], C->pq_ws[0], p0);
+        const u64 b = shoup_mul_red(sub_mod(C->hq[t], sP, p0), C->qinvp_w[0], C->qinvp_ws[0], p0);
+        r = add_mod(a, b, p0);
+    }
+    out[row * n + j] = r >= plain ? r - plain : r;  // r <= p
+}
+
+void launch_decrypt_round(const u64* X, u64* out, int items, int n, int L, const CrtTables* ct,
+                          const PrimeConst* primes, u64 plain, hipStream_t s) {
+    const long blocks = (long)items * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(decrypt_round_kernel, dim3(blocks), dim3(TPB), 0, s, X, out, n, L, ct, primes, plain);
+}
+
+// Signed digit recomposition (dbfv/decomposition.rs:45-68, 112-127): sum centred(mu_k) b^k in
+// i128 with Rust's release-mode wrapping, then mod p (p = 0: truncation to 64 bits).
+__global__ void __launch_bounds__(TPB)
+dbfv_recompose_kernel(const u64* __restrict__ digits, u64* __restrict__ out, int items, int n, int d, u64 base,
+                      u64 plain, u64 t, int scalar) {
+    const long idx = (long)blockIdx.x * TPB + threadIdx.x;
+    const int ncoef = scalar ? 1 : n;
+    if (idx >= (long)items * ncoef) return;
+    const long item = idx / ncoef;
+    const int j = (int)(idx - item * ncoef);
+    const u64 half_t = t / 2;
+    u128 result = 0, power = 1;  // two's-complement i128, wrapping
+    for (int k = 0; k < d; ++k) {
+        const u64 dk = digits[(item * d + k) * n + j];
+        const u128 centred = dk > half_t ? (u128)dk - (u128)t : (u128)dk;  // wraps to a negative i128
+        result += centred * power;
+        power *= (u128)base;
+    }
+    u64 r;
+    if (plain == 0) {
+        r = (u64)result;
+    } else if ((i128)result >= 0) {
+        r = (u64)(result % plain);
+    } else {
+        const u64 m = (u64)((~result + 1) % plain);  // |result| mod p
+        r = m == 0 ? 0 : plain - m;
+    }
+    out[idx] = r;
+}
+
+void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d, u64 base, u64 plain, u64 t,
+                           bool scalar, hipStream_t s) {
+    const long total = (long)items * (scalar ? 1 : n);
+    if (total == 0) return;
+    hipLaunchKernelGGL(dbfv_recompose_kernel, dim3((unsigned)((total + TPB - 1) / TPB)), dim3(TPB), 0, s, digits,
+                       out, items, n, d, base, plain, t, scalar ? 1 : 0);
+}
+
 // ---------------------------------------------------------------- literal HPS scale
 
 __device__ __forceinline__ u64 hps_ext(u64 a, u64 q, u64 pj) {

@@ -169,6 +169,39 @@ int exacto_dbfv_mul_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_
                         const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch,
                         const uint32_t* depth_a, const uint32_t* depth_b, uint32_t* depth_out);
 
+/* dBFV multiplication chain, device-resident (paper_repro.rs:203-236 guard-bypass semantics;
+ * bfv_host.rs:258-288 without the bootstrap): out = (((x*y)*y)...*y), `depth` dbfv_mul steps,
+ * each with both inputs' mul_depth reset to 0, intermediates kept in context-owned HBM buffers.
+ * x, y, out = [B][d][2][L][n]; depth 0 copies x.  Errors as exacto_dbfv_mul. */
+int exacto_dbfv_mul_chain(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                          const uint64_t* x, const uint64_t* y, uint64_t* out, size_t batch, size_t depth);
+int exacto_dbfv_mul_chain_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                              const uint64_t* x, const uint64_t* y, uint64_t* out, size_t batch, size_t depth);
+
+/* ---- decryption ----
+ * BFV decrypt (bfv/encrypt.rs:111-178), batched: phase = sum_k c_k * s^k in the NTT domain,
+ * INTT, x = CRT(phase) in [0, Q), m = floor((x*p + floor(Q/2)) / Q) mod p, exact for any Q.
+ * ct = [B][polys][L][n] (polys >= 1), sk = secret key [L][n] (NTT domain), out = [B][n] mod p.
+ * L >= 2 needs p below the first internal auxiliary prime (~2^60), else NotImplemented. */
+int exacto_bfv_decrypt(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* sk, uint64_t* out,
+                       size_t batch);
+int exacto_bfv_decrypt_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* sk,
+                           uint64_t* out, size_t batch);
+/* dBFV decrypt (dbfv/decrypt.rs:20-43): each limb decrypted mod t (the context's plain modulus),
+ * coefficient 0 of every limb centred and recomposed: sum centred(mu_i) * base^i mod p (i128,
+ * p = 0 -> mod 2^64).  ct = [B][d][2][L][n], out = [B]. */
+int exacto_dbfv_decrypt(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                        const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t batch);
+int exacto_dbfv_decrypt_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                            const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t batch);
+/* dbfv_decrypt_poly (dbfv/decrypt.rs:48-79): the same recomposition for every coefficient,
+ * out = [B][n]; plain modulus 0 -> InvalidParam "polynomial dBFV decrypt requires finite
+ * plain_modulus (plain_modulus=0 is scalar-only)". */
+int exacto_dbfv_decrypt_poly(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                             const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t batch);
+int exacto_dbfv_decrypt_poly_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                                 const uint64_t* ct, const uint64_t* sk, uint64_t* out, size_t batch);
+
 /* ---- diagnostics ---- */
 /* Copies the last error message of this thread (NUL-terminated); returns its length. */
 size_t exacto_last_error(char* buf, size_t len);

@@ -132,3 +132,17 @@ def dbfv_decrypt_scalar(ct: DbfvCiphertext, sk) -> int:
     digits = [bfv.decode_scalar(bfv.decrypt(l, sk)) for l in ct.limbs]
     use = min(params.num_digits, len(digits))
     return digit_recompose_signed(digits[:use], params.base, params.plain_modulus, t)
+
+
+def dbfv_decrypt_poly(ct: DbfvCiphertext, sk):
+    """dbfv/decrypt.rs:48-79: per-limb BFV decrypt, signed recomposition of every coefficient."""
+    params = ct.params
+    if params.plain_modulus == 0:
+        raise ExactoError.invalid_param(
+            "polynomial dBFV decrypt requires finite plain_modulus (plain_modulus=0 is scalar-only)")
+    t = params.bfv_params.plain_modulus
+    use = min(params.num_digits, len(ct.limbs))
+    polys = [bfv.decrypt(l, sk).coeffs for l in ct.limbs[:use]]
+    n = min(len(p) for p in polys)
+    return [digit_recompose_signed([p[i] for p in polys], params.base, params.plain_modulus, t)
+            for i in range(n)]
