@@ -121,6 +121,18 @@ struct RelinKey {
     BfvParamsPtr params;
 };
 
+// SecretKey (src/bfv/keygen.rs): the secret polynomial s in the NTT domain, [L][n].
+struct SecretKey {
+    RnsPoly poly;
+    BfvParamsPtr params;
+};
+
+// CoeffPoly (src/ring/poly.rs:6-9): plaintext coefficients mod `modulus`.
+struct CoeffPoly {
+    std::vector<uint64_t> coeffs;
+    uint64_t modulus = 0;
+};
+
 namespace detail {
 inline std::vector<uint64_t> flatten(const std::vector<BfvCiphertext>& cts, size_t polys) {
     std::vector<uint64_t> out;
@@ -207,6 +219,25 @@ inline BfvCiphertext bfv_mul_and_relin(const BfvCiphertext& a, const BfvCipherte
     return bfv_mul_and_relin(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b}, rlk)[0];
 }
 
+// decrypt (src/bfv/encrypt.rs:111-178), batched over ciphertexts of one degree.
+inline std::vector<CoeffPoly> decrypt(const std::vector<BfvCiphertext>& cts, const SecretKey& sk) {
+    if (cts.empty()) return {};
+    const BfvParams& prm = *cts[0].params;
+    const size_t polys = cts[0].c.size(), n = prm.ring_degree;
+    auto flat = detail::flatten(cts, polys);
+    std::vector<uint64_t> out(cts.size() * n);
+    detail::check(exacto_bfv_decrypt(prm.ctx(), flat.data(), polys, sk.poly.data.data(), out.data(), cts.size()));
+    std::vector<CoeffPoly> res(cts.size());
+    for (size_t b = 0; b < cts.size(); ++b) {
+        res[b].coeffs.assign(out.begin() + (long)(b * n), out.begin() + (long)((b + 1) * n));
+        res[b].modulus = prm.plain_modulus;
+    }
+    return res;
+}
+inline CoeffPoly decrypt(const BfvCiphertext& ct, const SecretKey& sk) {
+    return decrypt(std::vector<BfvCiphertext>{ct}, sk)[0];
+}
+
 // ---- exacto::dbfv
 struct DbfvParams {
     BfvParamsPtr bfv_params;
@@ -259,6 +290,54 @@ inline std::vector<DbfvCiphertext> dbfv_mul(const std::vector<DbfvCiphertext>& a
 
 inline DbfvCiphertext dbfv_mul(const DbfvCiphertext& a, const DbfvCiphertext& b, const RelinKey& rlk) {
     return dbfv_mul(std::vector<DbfvCiphertext>{a}, std::vector<DbfvCiphertext>{b}, rlk)[0];
+}
+
+namespace detail {
+inline std::vector<uint64_t> flatten_dbfv(const DbfvCiphertext& ct) {
+    if (ct.num_limbs() != ct.params->num_digits)
+        throw ExactoError(1, "invalid parameter: expected d-limb dBFV ciphertext");
+    return flatten(ct.limbs, 2);
+}
+}  // namespace detail
+
+// dbfv_decrypt (src/dbfv/decrypt.rs:20-43): scalar plaintext (coefficient 0).
+inline uint64_t dbfv_decrypt(const DbfvCiphertext& ct, const SecretKey& sk) {
+    const auto& dp = *ct.params;
+    auto flat = detail::flatten_dbfv(ct);
+    uint64_t out = 0;
+    detail::check(exacto_dbfv_decrypt(dp.bfv_params->ctx(), dp.num_digits, dp.base, dp.plain_modulus, flat.data(),
+                                      sk.poly.data.data(), &out, 1));
+    return out;
+}
+
+// dbfv_decrypt_poly (src/dbfv/decrypt.rs:48-79).
+inline CoeffPoly dbfv_decrypt_poly(const DbfvCiphertext& ct, const SecretKey& sk) {
+    const auto& dp = *ct.params;
+    auto flat = detail::flatten_dbfv(ct);
+    CoeffPoly res;
+    res.coeffs.resize(dp.bfv_params->ring_degree);
+    res.modulus = dp.plain_modulus;
+    detail::check(exacto_dbfv_decrypt_poly(dp.bfv_params->ctx(), dp.num_digits, dp.base, dp.plain_modulus,
+                                           flat.data(), sk.poly.data.data(), res.coeffs.data(), 1));
+    return res;
+}
+
+// The benchmark chain of src/bin/paper_repro.rs:203-236: x * y^depth with mul_depth reset before
+// every dbfv_mul (guard bypass), run device-resident in one call.
+inline DbfvCiphertext dbfv_mul_chain(const DbfvCiphertext& x, const DbfvCiphertext& y, const RelinKey& rlk,
+                                     size_t depth) {
+    const auto& dp = *x.params;
+    detail::load_key(rlk);
+    auto fx = detail::flatten_dbfv(x), fy = detail::flatten_dbfv(y);
+    std::vector<uint64_t> out(fx.size());
+    detail::check(exacto_dbfv_mul_chain(dp.bfv_params->ctx(), dp.num_digits, dp.base, dp.plain_modulus, fx.data(),
+                                        fy.data(), out.data(), 1, depth));
+    DbfvCiphertext res;
+    res.limbs = detail::unflatten(out, dp.num_digits, 2, dp.bfv_params);
+    res.degree = dp.num_digits;
+    res.mul_depth = depth ? 1 : x.mul_depth;
+    res.params = x.params;
+    return res;
 }
 
 }  // namespace exacto

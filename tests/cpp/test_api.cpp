@@ -107,6 +107,11 @@ static int run_case(const std::string& dir, const std::string& name) {
             limbs.insert(limbs.end(), x.limbs.begin(), x.limbs.end());
         }
         if (!same(limbs, read_u64(dir + "/" + name + ".out.u64"))) return 6;
+        // paper_repro.rs:203-236 chain: depth 1 is one dbfv_mul, depth 0 the input
+        if (!same(dbfv_mul_chain(A[0], Bc[0], rlk, 1).limbs, std::vector<uint64_t>(
+                      read_u64(dir + "/" + name + ".out.u64").begin(),
+                      read_u64(dir + "/" + name + ".out.u64").begin() + (long)per)))
+            return 9;
         // dbfv/eval.rs:292-313: chained multiplication is rejected
         try {
             dbfv_mul(r[0], Bc[0], rlk);
@@ -151,6 +156,17 @@ static int error_cases() {
         return 16;
     } catch (const ExactoError& e) {
         if (std::string(e.what()).find("relinearization only supports degree-2 ciphertexts") == std::string::npos) return 17;
+    }
+    // encrypt.rs:111-178 known answer: s = 0, c0 = Delta*m (constant, so every evaluation is
+    // Delta*m), Delta = floor(q/p) = 255 for q = 65537, p = 257 -> decrypts to m, other coeffs 0
+    {
+        auto p1 = BfvParamsBuilder().ring_degree(16).plain_modulus(257).ct_moduli({65537}).build();
+        RnsPoly c0{16, 1, std::vector<uint64_t>(16, 255 * 7)}, c1{16, 1, std::vector<uint64_t>(16, 12345)};
+        SecretKey sk{RnsPoly{16, 1, std::vector<uint64_t>(16, 0)}, p1};
+        auto m = decrypt(BfvCiphertext{{c0, c1}, p1}, sk);
+        if (m.modulus != 257 || m.coeffs[0] != 7) return 18;
+        for (size_t i = 1; i < 16; ++i)
+            if (m.coeffs[i] != 0) return 19;
     }
     return 0;
 }
