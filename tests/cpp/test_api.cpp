@@ -106,11 +106,11 @@ static int run_case(const std::string& dir, const std::string& name) {
             if (x.mul_depth != 1 || x.degree != m.d) return 5;
             limbs.insert(limbs.end(), x.limbs.begin(), x.limbs.end());
         }
-        if (!same(limbs, read_u64(dir + "/" + name + ".out.u64"))) return 6;
+        const auto want = read_u64(dir + "/" + name + ".out.u64");
+        if (!same(limbs, want)) return 6;
         // paper_repro.rs:203-236 chain: depth 1 is one dbfv_mul, depth 0 the input
-        if (!same(dbfv_mul_chain(A[0], Bc[0], rlk, 1).limbs, std::vector<uint64_t>(
-                      read_u64(dir + "/" + name + ".out.u64").begin(),
-                      read_u64(dir + "/" + name + ".out.u64").begin() + (long)per)))
+        if (!same(dbfv_mul_chain(A[0], Bc[0], rlk, 1).limbs,
+                  std::vector<uint64_t>(want.begin(), want.begin() + (long)per)))
             return 9;
         // dbfv/eval.rs:292-313: chained multiplication is rejected
         try {
