@@ -186,6 +186,7 @@ struct exacto_ctx {
     size_t rlk_keys = 0, rlk_cap = 0, rlk_s_cap = 0;
     bool rlk_s_valid = false;
     bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
+    bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
@@ -474,6 +475,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
     c->own_stream = true;
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
@@ -571,9 +573,12 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
         HIP_TRY(hipEventCreate(&rec.b));
         HIP_TRY(hipEventRecord(rec.a, c->stream));
     }
-    bool lazy = true;
-    for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) lazy &= c->primes[t] < (1ull << 60);
-    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream);
+    bool lazy = true, near60 = c->ntt_asm;
+    for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) {
+        lazy &= c->primes[t] < (1ull << 60);
+        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 56);
+    }
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));

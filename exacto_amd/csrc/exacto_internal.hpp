@@ -61,8 +61,10 @@ struct CrtTables {
 };
 
 // lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)
+// asm_fwd: every prime of the batch is in (2^60 - 2^56, 2^60) and the hand-scheduled forward
+// kernel (ntt_asm.inc) may be used for n = 4096 / 8192
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s);
+                hipStream_t s, bool asm_fwd = false);
 
 // Fused relinearisation: see keyswitch_kernel in ntt.hip.
 struct KsArgs {

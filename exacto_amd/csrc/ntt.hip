@@ -233,6 +233,100 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     }
 }
 
+// ---------------------------------------------------------------- forward, hand-scheduled rounds
+
+// n = 4096 / 8192 with every prime of the batch in (2^60 - 2^56, 2^60): the butterfly rounds are
+// the generated inline-asm statements of ntt_asm.inc (tools/gen_ntt_asm.py): two butterflies
+// interleaved so that the SGPR carry chains of the 64-bit arithmetic need no s_nop padding.
+// Same convention, same LDS exchanges and same output layout as ntt_fwd_kernel.
+#include "ntt_asm.inc"
+
+// The swizzle is linear over GF(2) and elem_index<LO>(tid, k) = A(tid) ^ (k << LO) with disjoint
+// bits, so every exchange address is one per-thread base XOR a compile-time constant: one VALU
+// per access instead of recomputing the swizzle of each index.
+template <int LO>
+__device__ __forceinline__ int lds_base_bytes(int tid) {
+    return swz(((tid >> LO) << (LO + 4)) | (tid & ((1 << LO) - 1))) << 3;
+}
+
+template <int LO>
+__device__ __forceinline__ void lds_store_x(u64* lds, const u64 (&x)[16], int tid) {
+    char* lb = reinterpret_cast<char*>(lds);
+    const int b = lds_base_bytes<LO>(tid);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) *reinterpret_cast<u64*>(lb + (b ^ (swz(k << LO) << 3))) = x[k];
+}
+
+template <int LO>
+__device__ __forceinline__ void lds_load_x(const u64* lds, u64 (&x)[16], int tid) {
+    const char* lb = reinterpret_cast<const char*>(lds);
+    const int b = lds_base_bytes<LO>(tid);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = *reinterpret_cast<const u64*>(lb + (b ^ (swz(k << LO) << 3)));
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
+    constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
+    constexpr int BHI = LOGN - 1 - 4 * R;
+    TwPair tw[15];
+    load_round_tw<LOGN, LO, BHI, LO>(tw, tid, tab);  // in flight across the exchange
+    if constexpr (R > 0) {
+        constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
+        // recompute the exchange addresses per round instead of keeping 32 of them live
+        int t2 = tid;
+        asm volatile("" : "+v"(t2));
+        lds_barrier();
+        lds_store_x<PLO>(lds, x, t2);
+        lds_barrier();
+        lds_load_x<LO>(lds, x, t2);
+    }
+    FwdRoundAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
+}
+
+#ifndef EXACTO_ASM_WAVES
+#define EXACTO_ASM_WAVES 3
+#endif
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(EXACTO_ASM_WAVES)))
+ntt_fwd_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64 q = P.q;
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+
+    u64 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+
+    AsmK K;
+    const u64 nq = (u64)0 - q, q2 = 2 * q, nq8 = (u64)0 - 8 * q;
+    K.n0 = (uint32_t)nq; K.n1 = (uint32_t)(nq >> 32);
+    K.q2l = (uint32_t)q2; K.q2h = (uint32_t)(q2 >> 32);
+    K.nq8l = (uint32_t)nq8; K.nq8h = (uint32_t)(nq8 >> 32);
+    K.nql = K.n0; K.nqh = K.n1;
+    K.q8 = 8 * q; K.q = q;
+    fwd_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_fwd), K);
+
+    // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
+    int t2 = tid;
+    asm volatile("" : "+v"(t2));
+    lds_barrier();
+    lds_store_x<0>(lds, x, t2);
+    lds_barrier();
+    lds_load_x<LOGN - 4>(lds, x, t2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+}
+
 // ---------------------------------------------------------------- inverse
 
 template <int LOGN, int LO, int BLO, int BHI>
@@ -608,8 +702,16 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
 }
 
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s) {
+                hipStream_t s, bool asm_fwd) {
     if (count <= 0) return;
+    if (asm_fwd && !inverse && logn == 12) {
+        hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        return;
+    }
+    if (asm_fwd && !inverse && logn == 13) {
+        hipLaunchKernelGGL((ntt_fwd_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        return;
+    }
     switch (logn) {
         case 4: launch_one<4>(nb, count, inverse, lazy, primes, s); break;
         case 5: launch_one<5>(nb, count, inverse, lazy, primes, s); break;
