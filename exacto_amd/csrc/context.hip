@@ -192,6 +192,13 @@ struct exacto_ctx {
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
     size_t ws_items = 0;
     u64 *ws_coefQ = nullptr, *ws_extP = nullptr, *ws_T = nullptr, *ws_D = nullptr;
+    // second pipeline lane: odd chunks run on aux_stream with their own workspace, so the
+    // kernels of two chunks overlap (the NTTs are latency-bound; EXACTO_DUAL_STREAM=0 disables)
+    bool dual = true;
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    size_t ws2_items = 0;
+    u64 *ws2_coefQ = nullptr, *ws2_extP = nullptr, *ws2_T = nullptr, *ws2_D = nullptr;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
     size_t chain_bytes = 0;
     u64* dec_buf = nullptr;    // decryption phase [B][L][n]
@@ -476,6 +483,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     c->own_stream = true;
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
@@ -488,6 +496,10 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
+    free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
+    if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -644,6 +656,38 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     return 0;
 }
 
+// Lane 1 of the pipeline: aux stream + second workspace (allocated on first use).
+static int ensure_lane2(exacto_ctx* c, size_t items) {
+    if (!c->aux_stream) HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    if (c->ws2_items >= items) return 0;
+    free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
+    c->ws2_coefQ = c->ws2_extP = c->ws2_T = c->ws2_D = nullptr;
+    c->ws2_items = 0;
+    const size_t pb = poly_bytes(c);
+    const int NP = c->L + c->K;
+    HIP_TRY(hipMalloc((void**)&c->ws2_coefQ, items * 4 * c->L * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws2_extP, items * 4 * std::max(c->K, 1) * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws2_T, items * 3 * NP * pb));
+    HIP_TRY(hipMalloc((void**)&c->ws2_D, items * std::max(c->G, 1) * c->L * pb));
+    c->ws2_items = items;
+    return 0;
+}
+
+// Points the context's stream and workspace at lane 1 for the lifetime of the guard.
+struct LaneGuard {
+    exacto_ctx* c;
+    bool on;
+    LaneGuard(exacto_ctx* c_, bool on_) : c(c_), on(on_) { if (on) flip(); }
+    ~LaneGuard() { if (on) flip(); }
+    void flip() {
+        std::swap(c->stream, c->aux_stream);
+        std::swap(c->ws_coefQ, c->ws2_coefQ); std::swap(c->ws_extP, c->ws2_extP);
+        std::swap(c->ws_T, c->ws2_T); std::swap(c->ws_D, c->ws2_D);
+    }
+};
+
 static int ensure_rlk_companions(exacto_ctx* c) {
     if (c->rlk_s_valid) return 0;
     const size_t count = c->rlk_keys * 2 * c->L * (size_t)c->n;
@@ -673,8 +717,27 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
     const size_t C = std::min<size_t>(c->chunk, (size_t)P);
     if (int e = ensure_workspace(c, C)) return e;
+    if (relin && guse > 0)
+        if (int e = ensure_rlk_companions(c)) return e;
+    // two chunks or more: odd chunks on the second lane (profiling keeps one lane so its per-kernel
+    // events time each kernel alone)
+    const bool dual = c->dual && !c->prof && P > (long)C;
+    if (dual) {
+        if (int e = ensure_lane2(c, C)) return e;
+        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+    }
+    struct Join {
+        exacto_ctx* c;
+        bool on;
+        ~Join() {
+            if (on && hipEventRecord(c->ev_join, c->aux_stream) == hipSuccess)
+                (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+        }
+    } join{c, dual};
     for (long s = 0; s < P; s += (long)C) {
         const int cnt = (int)std::min<long>((long)C, P - s);
+        LaneGuard lane(c, dual && ((s / (long)C) & 1));
         Operands o = op;
         if (o.a_off) o.a_off += s; else o.a += s * o.a_stride;
         if (o.b_off) o.b_off += s; else o.b += s * o.b_stride;

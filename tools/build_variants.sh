@@ -27,6 +27,8 @@ for v in "$@"; do
     w5) build w5 -DEXACTO_NTT_WAVES=5 ;;
     ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
+    probe0) build probe0 -DEXACTO_ASM_PROBE=0 ;;
+    probe2) build probe2 -DEXACTO_ASM_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
