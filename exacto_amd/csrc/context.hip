@@ -199,6 +199,11 @@ struct exacto_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     size_t ws2_items = 0;
     u64 *ws2_coefQ = nullptr, *ws2_extP = nullptr, *ws2_T = nullptr, *ws2_D = nullptr;
+    // dBFV: per-ciphertext extensions shared by the products that use the ciphertext
+    // (EXACTO_SHARE_EXT=0 recomputes them per product)
+    bool share_ext = true;
+    u64 *ext_a = nullptr, *ext_b = nullptr;
+    size_t ext_a_cap = 0, ext_b_cap = 0;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
     size_t chain_bytes = 0;
     u64* dec_buf = nullptr;    // decryption phase [B][L][n]
@@ -484,6 +489,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
@@ -497,6 +503,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
+    free_dev(c->ext_a); free_dev(c->ext_b);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -741,24 +748,29 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         Operands o = op;
         if (o.a_off) o.a_off += s; else o.a += s * o.a_stride;
         if (o.b_off) o.b_off += s; else o.b += s * o.b_stride;
-        // 1. inputs -> coefficient domain (INTT), coefQ[item] = [c0, c1, d0, d1][L][n]
-        NttBatch nb{};
-        nb.src = o.a; nb.src_off = o.a_off; nb.src_item_stride = o.a_stride;
-        nb.dst = c->ws_coefQ; nb.dst_item_stride = 4 * Ln;
-        nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
-        if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
-        nb.src = o.b; nb.src_off = o.b_off; nb.src_item_stride = o.b_stride;
-        nb.dst = c->ws_coefQ + 2 * Ln;
-        if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
-        // 2. extension to the auxiliary primes
-        if (c->path == EXACTO_PATH_HPS)
-            launch_hps_extend(c->ws_coefQ, c->ws_extP, cnt, n, c->d_primes, K, c->stream);
-        else
-            launch_exact_lift(c->ws_coefQ, c->ws_extP, cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0),
-                              c->stream);
-        CHECK_LAUNCH();
-        // 3. forward NTT of the extended polynomials
-        if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
+        if (!o.ea) {
+            // 1. inputs -> coefficient domain (INTT), coefQ[item] = [c0, c1, d0, d1][L][n]
+            NttBatch nb{};
+            nb.src = o.a; nb.src_off = o.a_off; nb.src_item_stride = o.a_stride;
+            nb.dst = c->ws_coefQ; nb.dst_item_stride = 4 * Ln;
+            nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
+            if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
+            nb.src = o.b; nb.src_off = o.b_off; nb.src_item_stride = o.b_stride;
+            nb.dst = c->ws_coefQ + 2 * Ln;
+            if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
+            // 2. extension to the auxiliary primes
+            if (c->path == EXACTO_PATH_HPS)
+                launch_hps_extend(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_primes, K, c->stream);
+            else
+                launch_exact_lift(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_crt, c->d_primes, L, K,
+                                  c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
+            CHECK_LAUNCH();
+            // 3. forward NTT of the extended polynomials
+            if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
+        } else {
+            o.ea_off += s;
+            o.eb_off += s;
+        }
         // 4+5. tensor product in every prime, fused into the inverse NTT of its components
         if (int e = run_inv_tensor(c, o, cnt)) return e;
         // 6. scale-and-round (+ gadget digits of the third component)
@@ -1047,12 +1059,17 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
         }
     }
     start[d] = (int)terms.size();
-    const long Ln2 = 2L * c->L * c->n;
-    std::vector<u64> off(2 * B * npairs);
+    const long Ln2 = 2L * c->L * c->n, Kn2 = 2L * c->K * c->n;
+    // [0, BP): a offsets, [BP, 2BP): b offsets (ciphertexts), [2BP, 4BP): the same into the
+    // per-ciphertext extension buffers
+    const size_t BP = B * npairs;
+    std::vector<u64> off(4 * BP);
     for (size_t b = 0; b < B; ++b)
         for (int pi = 0; pi < npairs; ++pi) {
             off[b * npairs + pi] = (u64)((b * d + pairs[pi].first) * Ln2);
-            off[B * npairs + b * npairs + pi] = (u64)((b * d + pairs[pi].second) * Ln2);
+            off[BP + b * npairs + pi] = (u64)((b * d + pairs[pi].second) * Ln2);
+            off[2 * BP + b * npairs + pi] = (u64)((b * d + pairs[pi].first) * Kn2);
+            off[3 * BP + b * npairs + pi] = (u64)((b * d + pairs[pi].second) * Kn2);
         }
     size_t cap = c->off_cap;
     if (grow(&c->d_off, &cap, off.size() * sizeof(u64) + 8)) return EXACTO_ERR_HIP;
@@ -1085,6 +1102,66 @@ static int dbfv_params_check(size_t d, uint64_t base, uint64_t plain) {
     return 0;
 }
 
+// Every input ciphertext of a dBFV product batch enters d products (dbfv/eval.rs:109-122): its
+// inverse NTT, its exact (or HPS) extension to the auxiliary primes and their forward NTT
+// (pipeline steps 1-3) are computed here once per ciphertext, ext = [ct][2][K][n], instead of
+// once per product.  The results are identical: steps 1-3 depend on the ciphertext alone.
+static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
+    const int n = c->n, L = c->L, K = c->K;
+    const long Ln2 = 2L * L * n, Kn2 = 2L * K * n;
+    if (int e = ensure_workspace(c, std::min<size_t>(c->chunk, (ncts + 1) / 2))) return e;
+    const size_t G = 2 * c->ws_items;  // ciphertexts per pass: coefQ holds 4 polys x L per item
+    for (size_t g0 = 0; g0 < ncts; g0 += G) {
+        const long cnt = (long)std::min(G, ncts - g0);
+        NttBatch nb{};
+        nb.src = cts + g0 * Ln2; nb.src_off = nullptr; nb.src_item_stride = Ln2;
+        nb.dst = c->ws_coefQ; nb.dst_item_stride = Ln2;
+        nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
+        if (int e = run_ntt(c, nb, cnt * 2 * L, true)) return e;
+        u64* eo = ext + g0 * Kn2;
+        if (c->path == EXACTO_PATH_HPS)
+            launch_hps_extend(c->ws_coefQ, eo, 2 * cnt, n, c->d_primes, K, c->stream);
+        else
+            launch_exact_lift(c->ws_coefQ, eo, 2 * cnt, n, c->d_crt, c->d_primes, L, K,
+                              c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
+        CHECK_LAUNCH();
+        if (int e = run_ntt(c, contiguous(eo, cnt, 2L * K, L, K, n), cnt * 2 * K, false)) return e;
+    }
+    return 0;
+}
+
+// b_extended: c->ext_b already holds the extensions of b (a chain's constant right operand)
+static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                         const uint64_t* b, uint64_t* out, size_t B, bool b_extended) {
+    if (int e = dbfv_plan(c, B, d, base, plain)) return e;
+    const int npairs = c->cached_npairs;
+    const long Ln2 = 2L * c->L * c->n;
+    const long P = (long)B * npairs;
+    size_t cap = c->prod_bytes;
+    if (grow(&c->prod, &cap, (size_t)P * Ln2 * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->prod_bytes = cap;
+    Operands op{};
+    const size_t BP = (size_t)B * npairs;
+    op.a = a; op.a_off = c->d_off; op.a_stride = 0;
+    op.b = b; op.b_off = c->d_off + BP; op.b_stride = 0;
+    if (c->share_ext && c->K > 0 && !c->deferred_code) {
+        const size_t nct = B * d, bytes = nct * 2 * c->K * poly_bytes(c);
+        if (grow(&c->ext_a, &c->ext_a_cap, bytes)) return EXACTO_ERR_HIP;
+        if (int e = extend_cts(c, a, nct, c->ext_a)) return e;
+        if (!b_extended) {
+            if (grow(&c->ext_b, &c->ext_b_cap, bytes)) return EXACTO_ERR_HIP;
+            if (int e = extend_cts(c, b, nct, c->ext_b)) return e;
+        }
+        op.ea = c->ext_a; op.ea_off = c->d_off + 2 * BP;
+        op.eb = c->ext_b; op.eb_off = c->d_off + 3 * BP;
+    }
+    if (int e = run_mul(c, op, P, c->prod, Ln2, true)) return e;
+    launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
+                        c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
 extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
                                    const uint64_t* b, uint64_t* out, size_t B, const uint32_t* depth_a,
                                    const uint32_t* depth_b, uint32_t* depth_out) {
@@ -1098,20 +1175,7 @@ extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint6
                                                     "ciphertext-level lattice reduction (paper §4.6.2)");
     }
     if (B == 0) return 0;
-    if (int e = dbfv_plan(c, B, d, base, plain)) return e;
-    const int npairs = c->cached_npairs;
-    const long Ln2 = 2L * c->L * c->n;
-    const long P = (long)B * npairs;
-    size_t cap = c->prod_bytes;
-    if (grow(&c->prod, &cap, (size_t)P * Ln2 * sizeof(u64))) return EXACTO_ERR_HIP;
-    c->prod_bytes = cap;
-    Operands op{};
-    op.a = a; op.a_off = c->d_off; op.a_stride = 0;
-    op.b = b; op.b_off = c->d_off + (size_t)B * npairs; op.b_stride = 0;
-    if (int e = run_mul(c, op, P, c->prod, Ln2, true)) return e;
-    launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
-                        c->stream);
-    CHECK_LAUNCH();
+    if (int e = dbfv_mul_core(c, d, base, plain, a, b, out, B, false)) return e;
     if (depth_out)
         for (size_t i = 0; i < B; ++i) depth_out[i] = 1;
     return 0;
@@ -1218,10 +1282,13 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
         if (grow(&c->chain_buf, &cap, 2 * bytes)) return EXACTO_ERR_HIP;
         c->chain_bytes = cap;
     }
+    if (int e = dbfv_params_check(d, base, plain)) return e;
+    if (B == 0) return 0;
     const uint64_t* src = x;
     for (size_t k = 0; k < depth; ++k) {
         uint64_t* dst = (k + 1 == depth) ? out : c->chain_buf + (k % 2) * (bytes / sizeof(u64));
-        if (int e = exacto_dbfv_mul_dev(c, d, base, plain, src, y, dst, B, nullptr, nullptr, nullptr)) return e;
+        // y's extensions are computed by the first step and reused by the others
+        if (int e = dbfv_mul_core(c, d, base, plain, src, y, dst, B, k > 0)) return e;
         src = dst;
     }
     return 0;

@@ -92,6 +92,13 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
     const u64* b;
     const u64* b_off;
     long b_stride;
+    // optional: the operands already extended to the auxiliary primes, forward-transformed,
+    // [2][K][n] per ciphertext at ea + ea_off[item] / eb + eb_off[item] (shared by every product
+    // that uses the ciphertext, dBFV); when set the pipeline skips steps 1-3
+    const u64* ea;
+    const u64* ea_off;
+    const u64* eb;
+    const u64* eb_off;
 };
 
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
@@ -104,9 +111,10 @@ void launch_decrypt_round(const u64* X, u64* out, int items, int n, int L, const
                           const PrimeConst* primes, u64 plain, hipStream_t s);
 void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d, u64 base, u64 plain, u64 t,
                            bool scalar, hipStream_t s);
-void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
+// rows = polynomials of coefQ ([rows][L][n] -> extP [rows][K][n])
+void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtTables* ct,
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
-void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
+void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,

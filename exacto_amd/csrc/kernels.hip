@@ -271,9 +271,9 @@ exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
     }
 }
 
-void launch_exact_lift(const u64* coefQ, u64* extP, int items, int n, const CrtTables* ct,
+void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtTables* ct,
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s) {
-    const long blocks = (long)items * 4 * blocks_per_row(n);
+    const long blocks = rows * blocks_per_row(n);
     if (blocks == 0) return;
 #define LIFT(NR, FS, LT, KT)                                                                                     \
     hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
@@ -317,9 +317,9 @@ hps_extend_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
     }
 }
 
-void launch_hps_extend(const u64* coefQ, u64* extP, int items, int n, const PrimeConst* primes,
+void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const PrimeConst* primes,
                        int K, hipStream_t s) {
-    const long blocks = (long)items * 4 * blocks_per_row(n);
+    const long blocks = rows * blocks_per_row(n);
     if (blocks == 0) return;
     hipLaunchKernelGGL(hps_extend_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, K, primes);
 }

@@ -506,6 +506,10 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
         A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
         B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
+    } else if (op.ea) {  // shared per-ciphertext extensions (dBFV)
+        const u64* EA = op.ea + (long)op.ea_off[item] + (long)(t - L) * N;
+        const u64* EB = op.eb + (long)op.eb_off[item] + (long)(t - L) * N;
+        A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
     } else {
         const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
         A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
