@@ -18,7 +18,7 @@ def per_dispatch(path, counter):
     vals = {}
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "ntt_fwd_kernel" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
+            if "ntt_fwd" not in r["Kernel_Name"] or r["Counter_Name"] != counter:
                 continue
             key = int(r["Dispatch_Id"])
             grid = int(r.get("Grid_Size", 0) or 0)
@@ -38,7 +38,7 @@ wr = [1024 * v[0] for v in write.values()]
 polys = [v[1] // max(v[2], 1) for v in fetch.values()]
 alg = [16.0 * n * p for p in polys]
 res = {
-    "kernel": "ntt_fwd_kernel<12, true>",
+    "kernel": "ntt_fwd_asm_kernel<12> (hand-scheduled forward NTT)",
     "dispatches": len(rd),
     "read_bytes_avg": sum(rd) / len(rd),
     "write_bytes_avg": sum(wr) / len(wr),
