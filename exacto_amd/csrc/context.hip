@@ -192,6 +192,10 @@ struct exacto_ctx {
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
     size_t ws_items = 0;
     u64 *ws_coefQ = nullptr, *ws_extP = nullptr, *ws_T = nullptr, *ws_D = nullptr;
+    // exact path with gadget base <= 2^16: the scale kernel writes each digit once as int16 and
+    // the digit NTT converts it per limb on load (EXACTO_DIGIT16=0: u64 digits per limb)
+    bool digit16 = true;
+    int16_t *ws_D16 = nullptr, *ws2_D16 = nullptr;
     // second pipeline lane: odd chunks run on aux_stream with their own workspace, so the
     // kernels of two chunks overlap (the NTTs are latency-bound; EXACTO_DUAL_STREAM=0 disables)
     bool dual = true;
@@ -490,6 +494,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
@@ -504,6 +509,8 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
+    if (c->ws_D16) (void)hipFree(c->ws_D16);
+    if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -659,6 +666,8 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     HIP_TRY(hipMalloc((void**)&c->ws_extP, items * 4 * std::max(c->K, 1) * pb));
     HIP_TRY(hipMalloc((void**)&c->ws_T, items * 3 * NP * pb));
     HIP_TRY(hipMalloc((void**)&c->ws_D, items * std::max(c->G, 1) * c->L * pb));
+    if (c->ws_D16) (void)hipFree(c->ws_D16);
+    HIP_TRY(hipMalloc((void**)&c->ws_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
     c->ws_items = items;
     return 0;
 }
@@ -678,6 +687,8 @@ static int ensure_lane2(exacto_ctx* c, size_t items) {
     HIP_TRY(hipMalloc((void**)&c->ws2_extP, items * 4 * std::max(c->K, 1) * pb));
     HIP_TRY(hipMalloc((void**)&c->ws2_T, items * 3 * NP * pb));
     HIP_TRY(hipMalloc((void**)&c->ws2_D, items * std::max(c->G, 1) * c->L * pb));
+    if (c->ws2_D16) (void)hipFree(c->ws2_D16);
+    HIP_TRY(hipMalloc((void**)&c->ws2_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
     c->ws2_items = items;
     return 0;
 }
@@ -691,7 +702,7 @@ struct LaneGuard {
     void flip() {
         std::swap(c->stream, c->aux_stream);
         std::swap(c->ws_coefQ, c->ws2_coefQ); std::swap(c->ws_extP, c->ws2_extP);
-        std::swap(c->ws_T, c->ws2_T); std::swap(c->ws_D, c->ws2_D);
+        std::swap(c->ws_T, c->ws2_T); std::swap(c->ws_D, c->ws2_D); std::swap(c->ws_D16, c->ws2_D16);
     }
 };
 
@@ -777,11 +788,14 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         u64* R = out + s * out_stride;
         const int ncomp = relin ? 2 : 3;
         u64* D = relin ? c->ws_D : nullptr;
+        const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
+                         c->gbase <= 65536;
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
-            launch_exact_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, L, K,
-                               c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
+            launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D, d16 ? c->ws_D16 : nullptr, guse,
+                               cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0),
+                               c->stream);
         CHECK_LAUNCH();
         // 7. forward NTT of the results (and digits)
         NttBatch rb{};
@@ -801,7 +815,12 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         }
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
         if (relin && guse > 0) {
-            if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false)) return e;
+            NttBatch db = contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n);
+            if (d16) {  // int16 digits [item][g][n] -> NTT residues [item][g][L][n]
+                db.src16 = c->ws_D16;
+                db.src16_item_stride = (long)guse * n;
+            }
+            if (int e = run_ntt(c, db, (long)cnt * guse * L, false)) return e;
             // 8. relinearisation MAC, in place on the output
             if (int e = ensure_rlk_companions(c)) return e;
             launch_relin_mac(R, out_stride, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n, L,

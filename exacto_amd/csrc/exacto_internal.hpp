@@ -18,6 +18,10 @@ struct NttBatch {
     int ppi;
     int prime_base;
     int period;
+    // optional int16 source (gadget digits): polynomial (item, sub) reads
+    // src16 + item * src16_item_stride + (sub / period) * n, converted to residues mod its prime
+    const int16_t* src16;
+    long src16_item_stride;
 };
 
 enum class MulPath : int { Exact = 0, Hps = 1 };
@@ -116,7 +120,8 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
-void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+// D16 (or nullptr): gadget digits of the third component as int16 [item][g][n] instead of D
+void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,

@@ -137,11 +137,14 @@ __device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool 
 // Balanced gadget digits of the centred CRT value of residues res[0..L) (mod Q).
 // keyswitch.rs:24-44 literally (truncating %, [-B/2, B/2) adjustment, final carry dropped),
 // on the exact value (extension semantics for Q >= 2^64; identical to rns.rs:114-151 below).
-// Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j).
+// Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j), or, with
+// D16 (gadget base <= 2^16: every balanced digit lies in [-2^15, 2^15)), the signed digit once
+// at D16[g * n] for all limbs: 2 bytes per digit instead of 8 L.
 template <bool NEAR, int LT = 0>
 __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L_arg,
                                               const CrtTables* __restrict__ C,
-                                              const PrimeConst* __restrict__ primes, u64* D, int n, int guse) {
+                                              const PrimeConst* __restrict__ primes, u64* D, int n, int guse,
+                                              int16_t* D16 = nullptr) {
     const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
     u64 z[EXACTO_MAX_L];
     garner_q<NEAR>(z, res, L, C, primes);
@@ -230,6 +233,10 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
                     M[w] = s;
                 }
             }
+        }
+        if (D16) {
+            D16[(long)g * n] = (int16_t)(dneg ? -(i64)mag : (i64)mag);
+            continue;
         }
         // digit residue (rem mod Q) mod q_i == rem mod q_i; |rem| < B <= q_i when digit_small
         const bool small = C->digit_small != 0;
@@ -329,7 +336,7 @@ void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const Prim
 template <bool NEAR, bool FAST, int LT, int KT>
 __global__ void __launch_bounds__(TPB)
 exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                   u64* __restrict__ D, int guse, int n, int L_arg, int K_arg,
+                   u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n, int L_arg, int K_arg,
                    const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
     const int L = LT ? LT : L_arg;  // LT/KT > 0: limb counts known at compile time
@@ -406,18 +413,20 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
         for (int i = 0; i < EXACTO_MAX_L; ++i)
             if (i < L) out[(long)i * n] = res[i];
     }
-    if (comp == 2 && D != nullptr)
+    if (comp == 2 && D16 != nullptr)
+        gadget_digits<NEAR, LT>(res, L, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
+    else if (comp == 2 && D != nullptr)
         gadget_digits<NEAR, LT>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
 }
 
-void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
+void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
 #define SCALE(NR, FS, LT, KT)                                                                                    \
     hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
-                       D, guse, n, L, K, ct, primes)
+                       D, D16, guse, n, L, K, ct, primes)
     if (mode == 2) {
         switch (L) {
             case 1: if (K == 2) SCALE(true, true, 1, 2); else SCALE(true, true, 1, 0); break;

@@ -183,6 +183,25 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTa
 #define NTT_OCC
 #endif
 
+// Coefficient-domain input of a forward transform: element tid + k*T of the polynomial, from
+// the u64 source or, for int16 gadget digits, the signed digit as a residue mod q.
+template <int N>
+__device__ __forceinline__ void load_coeffs(u64 (&x)[16], const NttBatch& nb, const u64* src, int item, int sub,
+                                            u64 q, int tid) {
+    constexpr int T = N / 16;
+    if (nb.src16) {
+        const int16_t* s16 = nb.src16 + (long)item * nb.src16_item_stride + (long)(sub / nb.period) * N;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const i64 d = s16[tid + k * T];
+            x[k] = d < 0 ? q + (u64)d : (u64)d;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+    }
+}
+
 template <int LOGN, bool LAZY>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16) NTT_OCC
 ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
@@ -200,8 +219,7 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
 
     u64 x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+    load_coeffs<N>(x, nb, src, item, sub, q, tid);
 
     const u64 q8 = 8 * q;
     fwd_rounds<LOGN, 0, LAZY, EXACTO_NTT_PRELOAD>(x, lds, tid, tw_table(P.tw_fwd), (u64)0 - q, q2, q8);
@@ -304,8 +322,7 @@ ntt_fwd_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
 
     u64 x[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+    load_coeffs<N>(x, nb, src, item, sub, q, tid);
 
     AsmK K;
     const u64 nq = (u64)0 - q, q2 = 2 * q, nq8 = (u64)0 - 8 * q;
