@@ -83,6 +83,16 @@ _SIGS = [
     ("exacto_dbfv_decrypt_poly", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
     ("exacto_dbfv_decrypt_poly_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
     ("exacto_dbfv_mul_chain_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_gen_secret_key", [_P, _P, _U64, _P], C.c_int),
+    ("exacto_gen_secret_key_dev", [_P, _P, _U64, _P], C.c_int),
+    ("exacto_gen_public_key", [_P, _P, C.c_double, _P, _U64, _P], C.c_int),
+    ("exacto_gen_public_key_dev", [_P, _P, C.c_double, _P, _U64, _P], C.c_int),
+    ("exacto_gen_relin_key", [_P, _P, C.c_double, _P, _U64, _SZ, _P], C.c_int),
+    ("exacto_gen_relin_key_dev", [_P, _P, C.c_double, _P, _U64, _SZ, _P], C.c_int),
+    ("exacto_encrypt_sk", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
+    ("exacto_encrypt_sk_dev", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
+    ("exacto_encrypt_pk", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
+    ("exacto_encrypt_pk_dev", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -287,6 +297,63 @@ class HipContext:
         check(self._lib.exacto_dbfv_decrypt_poly(self._h, d, base, plain, ct.ctypes.data, sk.ctypes.data,
                                                  out.ctypes.data, ct.shape[0]))
         return out
+
+    # ---- key generation / encryption (keygen.rs:64-162, encrypt.rs:29-106); key = 4 u64 words
+    @staticmethod
+    def _key(key):
+        k = _u64(key).reshape(-1)
+        if k.size != 4:
+            raise ValueError("key must be 4 64-bit words")
+        return k
+
+    def gen_secret_key(self, key, stream=0) -> np.ndarray:
+        k = self._key(key)
+        sk = np.zeros((self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_gen_secret_key(self._h, k.ctypes.data, stream, sk.ctypes.data))
+        return sk
+
+    def gen_public_key(self, sk, key, stream=0, sigma=3.2) -> np.ndarray:
+        k, sk = self._key(key), _u64(sk)
+        pk = np.zeros((2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_gen_public_key(self._h, sk.ctypes.data, sigma, k.ctypes.data, stream, pk.ctypes.data))
+        return pk
+
+    def gen_relin_key(self, sk, key, stream=0, sigma=3.2, num_keys=None, resident=False):
+        """resident=True: generate into the context's resident key (returns None)."""
+        k, sk = self._key(key), _u64(sk)
+        nk = self.G if num_keys is None else num_keys
+        if resident:
+            check(self._lib.exacto_gen_relin_key(self._h, sk.ctypes.data, sigma, k.ctypes.data, stream, nk, None))
+            return None
+        rlk = np.zeros((nk, 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_gen_relin_key(self._h, sk.ctypes.data, sigma, k.ctypes.data, stream, nk,
+                                             rlk.ctypes.data))
+        return rlk
+
+    def encrypt_sk(self, pt, sk, key, stream=0, sigma=3.2) -> np.ndarray:
+        """pt [B][n] plaintext coefficients -> ct [B][2][L][n]."""
+        k, pt, sk = self._key(key), _u64(pt), _u64(sk)
+        ct = np.zeros((pt.shape[0], 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_encrypt_sk(self._h, pt.ctypes.data, sk.ctypes.data, sigma, k.ctypes.data, stream,
+                                          ct.ctypes.data, pt.shape[0]))
+        return ct
+
+    def encrypt_pk(self, pt, pk, key, stream=0, sigma=3.2) -> np.ndarray:
+        k, pt, pk = self._key(key), _u64(pt), _u64(pk)
+        ct = np.zeros((pt.shape[0], 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_encrypt_pk(self._h, pt.ctypes.data, pk.ctypes.data, sigma, k.ctypes.data, stream,
+                                          ct.ctypes.data, pt.shape[0]))
+        return ct
+
+    def gen_relin_key_dev(self, sk, key, stream, num_keys, rlk=None, sigma=3.2):
+        k = self._key(key)
+        check(self._lib.exacto_gen_relin_key_dev(self._h, self._p(sk), sigma, k.ctypes.data, stream, num_keys,
+                                                 None if rlk is None else self._p(rlk)))
+
+    def encrypt_sk_dev(self, pt, sk, key, stream, ct, batch, sigma=3.2):
+        k = self._key(key)
+        check(self._lib.exacto_encrypt_sk_dev(self._h, self._p(pt), self._p(sk), sigma, k.ctypes.data, stream,
+                                              self._p(ct), batch))
 
     # ---- device-pointer API (asynchronous; torch tensors or raw ints)
     def _p(self, x):

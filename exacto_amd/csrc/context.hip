@@ -5,6 +5,7 @@
 // HBM, the exact-CRT tables, the resident relinearisation key and a chunked
 // workspace.  Every `_dev` entry point only enqueues kernels on the context stream.
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -206,6 +207,16 @@ struct exacto_ctx {
     // dBFV: per-ciphertext extensions shared by the products that use the ciphertext
     // (EXACTO_SHARE_EXT=0 recomputes them per product)
     bool share_ext = true;
+    // keygen / encryption
+    double* d_cdt = nullptr;
+    size_t cdt_cap = 0;
+    double cdt_sigma = 0.0;
+    u64* d_gpow = nullptr;
+    size_t gpow_cap = 0;
+    u64* d_delta = nullptr;
+    bool delta_ok = false;
+    u64* enc_buf = nullptr;
+    size_t enc_cap = 0;
     u64 *ext_a = nullptr, *ext_b = nullptr;
     size_t ext_a_cap = 0, ext_b_cap = 0;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
@@ -509,6 +520,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
@@ -1330,6 +1342,263 @@ extern "C" int exacto_dbfv_mul(exacto_ctx* c, size_t d, uint64_t base, uint64_t 
     return host_call(c, {{a, bytes}, {b, bytes}}, bytes, out, [&](std::vector<u64*>& dv, u64* o) {
         return exacto_dbfv_mul_dev(c, d, base, plain, dv[0], dv[1], o, B, depth_a, depth_b, depth_out);
     });
+}
+
+// ============================================================== keygen / encryption
+
+// Gaussian CDT of sampling/gaussian.rs:18-33 (unnormalised cumulative weights over
+// [-ceil(6 sigma), ceil(6 sigma)]), cached on the device per sigma.
+static int gaussian_table(exacto_ctx* c, double sigma, int* tail, int* len, double* total) {
+    if (!(sigma > 0.0) || sigma > 1e6) return invalid_param("sigma must be positive");
+    const int t = (int)std::ceil(6.0 * sigma);
+    std::vector<double> cdf;
+    double cum = 0.0;
+    const double two_s2 = 2.0 * sigma * sigma;
+    for (long x = -t; x <= t; ++x) {
+        cum += std::exp(-(double)(x * x) / two_s2);
+        cdf.push_back(cum);
+    }
+    if (c->cdt_sigma != sigma || !c->d_cdt) {
+        size_t cap = c->cdt_cap;
+        if (grow((u64**)&c->d_cdt, &cap, cdf.size() * sizeof(double))) return EXACTO_ERR_HIP;
+        c->cdt_cap = cap;
+        HIP_TRY(hipMemcpy(c->d_cdt, cdf.data(), cdf.size() * sizeof(double), hipMemcpyHostToDevice));
+        c->cdt_sigma = sigma;
+    }
+    *tail = t;
+    *len = (int)cdf.size();
+    *total = cum;
+    return 0;
+}
+
+static ChaChaKey chacha_key(const uint64_t* key) {
+    ChaChaKey k{};
+    for (int i = 0; i < 4; ++i) k.w[i] = key ? key[i] : 0;
+    return k;
+}
+
+// Sample `polys` polynomials ([L][n] residues each, at out + p * stride) with indices base + p * step.
+static int sample_polys(exacto_ctx* c, int kind, const ChaChaKey& key, u64 stream, u64* out, long stride, u64 base,
+                        u64 step, long polys, double sigma) {
+    int tail = 0, len = 0;
+    double total = 0.0;
+    if (kind == KG_GAUSSIAN)
+        if (int e = gaussian_table(c, sigma, &tail, &len, &total)) return e;
+    launch_sample(kind, key, stream, out, stride, base, step, polys, c->n, c->L, c->d_primes, c->d_cdt, len, tail,
+                  total, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+// Forward NTT of `items` groups of `polys_per_item` [L][n] blocks spaced `stride` words apart.
+static int ntt_items(exacto_ctx* c, u64* data, long items, long stride, long polys_per_item) {
+    NttBatch nb{};
+    nb.src = data; nb.src_item_stride = stride;
+    nb.dst = data; nb.dst_item_stride = stride;
+    nb.ppi = (int)polys_per_item; nb.prime_base = 0; nb.period = c->L;
+    return run_ntt(c, nb, items * polys_per_item, false);
+}
+
+extern "C" int exacto_gen_secret_key_dev(exacto_ctx* c, const uint64_t* key, uint64_t stream, uint64_t* sk) {
+    if (int e = check_ctx(c)) return e;
+    if (!key || !sk) return invalid_param("null argument");
+    // keygen.rs:69-79: ternary s mod q0 -> RnsPoly::from_coeff_poly
+    if (int e = sample_polys(c, KG_TERNARY, chacha_key(key), stream, sk, 0, 0, 1, 1, 0.0)) return e;
+    return ntt_items(c, sk, 1, 0, c->L);
+}
+
+extern "C" int exacto_gen_public_key_dev(exacto_ctx* c, const uint64_t* sk, double sigma, const uint64_t* key,
+                                         uint64_t stream, uint64_t* pk) {
+    if (int e = check_ctx(c)) return e;
+    if (!key || !sk || !pk) return invalid_param("null argument");
+    const long Ln = (long)c->L * c->n;
+    const ChaChaKey k = chacha_key(key);
+    // keygen.rs:90-110: a (-> pk1), e (-> pk0 slot), pk0 = -(a s + e)
+    if (int e = sample_polys(c, KG_UNIFORM, k, stream, pk + Ln, 0, 0, 1, 1, sigma)) return e;
+    if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, pk, 0, 1, 1, 1, sigma)) return e;
+    if (int e = ntt_items(c, pk, 1, 0, 2L * c->L)) return e;
+    launch_combine(KG_PK, pk, 1, 0, Ln, sk, nullptr, nullptr, nullptr, nullptr, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, double sigma, const uint64_t* key,
+                                        uint64_t stream, size_t num_keys, uint64_t* rlk) {
+    if (int e = check_ctx(c)) return e;
+    if (!key || !sk) return invalid_param("null argument");
+    const long Ln = (long)c->L * c->n;
+    const bool resident = rlk == nullptr;
+    if (resident) {  // generate straight into the context's resident key (no host build, no upload)
+        rlk = exacto_ctx_relin_key_buffer(c, num_keys);
+        if (!rlk && num_keys) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
+    }
+    if (num_keys == 0) return 0;
+    // g_i = base^i mod q_l (keygen.rs:133-158: gadget_s_sq scaled by base after every key)
+    std::vector<u64> gpow(num_keys * c->L);
+    for (int l = 0; l < c->L; ++l) {
+        const u64 q = c->primes[l];
+        u64 g = 1 % q;
+        const u64 b = c->gbase % q;
+        for (size_t i = 0; i < num_keys; ++i) {
+            gpow[i * c->L + l] = g;
+            g = (u64)((u128)g * b % q);
+        }
+    }
+    size_t cap = c->gpow_cap;
+    if (grow(&c->d_gpow, &cap, gpow.size() * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->gpow_cap = cap;
+    HIP_TRY(hipMemcpyAsync(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    const ChaChaKey k = chacha_key(key);
+    // key i: a_i (index 2i) into the rlk1 slot, e_i (index 2i+1) into the rlk0 slot
+    if (int e = sample_polys(c, KG_UNIFORM, k, stream, rlk + Ln, 2 * Ln, 0, 2, (long)num_keys, sigma)) return e;
+    if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, rlk, 2 * Ln, 1, 2, (long)num_keys, sigma)) return e;
+    if (int e = ntt_items(c, rlk, (long)num_keys, 2 * Ln, 2L * c->L)) return e;
+    launch_combine(KG_RLK, rlk, (long)num_keys, 2 * Ln, Ln, sk, nullptr, nullptr, nullptr, c->d_gpow, c->n, c->L,
+                   c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (resident) {
+        HIP_TRY(hipStreamSynchronize(c->stream));  // the key must be complete before it is marked loaded
+        c->rlk_keys = num_keys;
+        c->rlk_loaded = true;
+        c->rlk_s_valid = false;
+    }
+    return 0;
+}
+
+// Delta_i = floor(Q / p) mod q_i (encrypt.rs:205-229), device copy in c->d_delta.
+static int delta_residues(exacto_ctx* c) {
+    if (c->delta_ok) return 0;
+    // Q as little-endian 64-bit words, then floor(Q / p) by long division, then mod each q_i
+    std::vector<u64> Qw(1, 1);
+    for (int i = 0; i < c->L; ++i) {
+        u128 carry = 0;
+        for (auto& w : Qw) {
+            const u128 t = (u128)w * c->primes[i] + carry;
+            w = (u64)t;
+            carry = t >> 64;
+        }
+        if (carry) Qw.push_back((u64)carry);
+    }
+    std::vector<u64> D(Qw.size());
+    u128 rem = 0;
+    for (size_t w = Qw.size(); w-- > 0;) {
+        const u128 cur = (rem << 64) | Qw[w];
+        D[w] = (u64)(cur / c->plain);
+        rem = cur % c->plain;
+    }
+    bool zero = true;
+    for (u64 w : D) zero &= (w == 0);
+    if (zero) return invalid_param("ciphertext modulus product Q must be >= plaintext modulus p");
+    std::vector<u64> dr(c->L);
+    for (int i = 0; i < c->L; ++i) {
+        u128 r = 0;
+        for (size_t w = D.size(); w-- > 0;) r = ((r << 64) | D[w]) % c->primes[i];
+        dr[i] = (u64)r;
+    }
+    if (!c->d_delta) HIP_TRY(hipMalloc((void**)&c->d_delta, EXACTO_MAX_L * sizeof(u64)));
+    HIP_TRY(hipMemcpy(c->d_delta, dr.data(), dr.size() * sizeof(u64), hipMemcpyHostToDevice));
+    c->delta_ok = true;
+    return 0;
+}
+
+// encrypt.rs:29-106 for a batch: pt = [B][n] plaintext coefficients, ct = [B][2][L][n] (NTT domain).
+// pk == nullptr: secret-key encryption with sk; otherwise public-key encryption with pk [2][L][n].
+static int encrypt_batch(exacto_ctx* c, const u64* pt, const u64* sk, const u64* pk, double sigma,
+                         const uint64_t* key, u64 stream, u64* ct, size_t B) {
+    if (!key || !pt || !ct || (!sk && !pk)) return invalid_param("null argument");
+    if (B == 0) return 0;
+    if (int e = delta_residues(c)) return e;
+    const long Ln = (long)c->L * c->n;
+    const ChaChaKey k = chacha_key(key);
+    // scratch: Delta m [B][L][n], and u [B][L][n] for pk-encryption
+    size_t cap = c->enc_cap;
+    if (grow(&c->enc_buf, &cap, (size_t)B * (pk ? 2 : 1) * Ln * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->enc_cap = cap;
+    u64* dm = c->enc_buf;
+    u64* u = c->enc_buf + (size_t)B * Ln;
+    launch_scale_plain(pt, c->d_delta, dm, (long)B, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = ntt_items(c, dm, (long)B, Ln, c->L)) return e;
+    if (!pk) {
+        // encrypt.rs:79-106, item b: a (index 2b) -> c1, e (index 2b+1) -> c0 slot
+        if (int e = sample_polys(c, KG_UNIFORM, k, stream, ct + Ln, 2 * Ln, 0, 2, (long)B, sigma)) return e;
+        if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, ct, 2 * Ln, 1, 2, (long)B, sigma)) return e;
+        if (int e = ntt_items(c, ct, (long)B, 2 * Ln, 2L * c->L)) return e;
+        launch_combine(KG_ENC_SK, ct, (long)B, 2 * Ln, Ln, sk, dm, nullptr, nullptr, nullptr, c->n, c->L, c->d_primes,
+                       c->stream);
+    } else {
+        // encrypt.rs:29-69, item b: u binary (3b), e1 (3b+1) -> c0 slot, e2 (3b+2) -> c1 slot
+        if (int e = sample_polys(c, KG_BINARY, k, stream, u, Ln, 0, 3, (long)B, sigma)) return e;
+        if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, ct, 2 * Ln, 1, 3, (long)B, sigma)) return e;
+        if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, ct + Ln, 2 * Ln, 2, 3, (long)B, sigma)) return e;
+        if (int e = ntt_items(c, u, (long)B, Ln, c->L)) return e;
+        if (int e = ntt_items(c, ct, (long)B, 2 * Ln, 2L * c->L)) return e;
+        launch_combine(KG_ENC_PK, ct, (long)B, 2 * Ln, Ln, nullptr, u, dm, pk, nullptr, c->n, c->L, c->d_primes,
+                       c->stream);
+    }
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_encrypt_sk_dev(exacto_ctx* c, const uint64_t* pt, const uint64_t* sk, double sigma,
+                                     const uint64_t* key, uint64_t stream, uint64_t* ct, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!sk) return invalid_param("null argument");
+    return encrypt_batch(c, pt, sk, nullptr, sigma, key, stream, ct, B);
+}
+
+extern "C" int exacto_encrypt_pk_dev(exacto_ctx* c, const uint64_t* pt, const uint64_t* pk, double sigma,
+                                     const uint64_t* key, uint64_t stream, uint64_t* ct, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!pk) return invalid_param("null argument");
+    return encrypt_batch(c, pt, nullptr, pk, sigma, key, stream, ct, B);
+}
+
+// Host-pointer variants (synchronous); `key` is always a host pointer to 4 words.
+extern "C" int exacto_gen_secret_key(exacto_ctx* c, const uint64_t* key, uint64_t stream, uint64_t* sk) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {}, c->L * poly_bytes(c), sk,
+                     [&](std::vector<u64*>&, u64* o) { return exacto_gen_secret_key_dev(c, key, stream, o); });
+}
+
+extern "C" int exacto_gen_public_key(exacto_ctx* c, const uint64_t* sk, double sigma, const uint64_t* key,
+                                     uint64_t stream, uint64_t* pk) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{sk, c->L * poly_bytes(c)}}, 2 * c->L * poly_bytes(c), pk, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_gen_public_key_dev(c, d[0], sigma, key, stream, o);
+    });
+}
+
+extern "C" int exacto_gen_relin_key(exacto_ctx* c, const uint64_t* sk, double sigma, const uint64_t* key,
+                                    uint64_t stream, size_t num_keys, uint64_t* rlk) {
+    if (!c) return invalid_param("null context");
+    if (!rlk) {  // resident key only: stage the secret key, generate in place
+        return host_call(c, {{sk, c->L * poly_bytes(c)}}, 0, nullptr, [&](std::vector<u64*>& d, u64*) {
+            return exacto_gen_relin_key_dev(c, d[0], sigma, key, stream, num_keys, nullptr);
+        });
+    }
+    return host_call(c, {{sk, c->L * poly_bytes(c)}}, num_keys * 2 * c->L * poly_bytes(c), rlk,
+                     [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_gen_relin_key_dev(c, d[0], sigma, key, stream, num_keys, o);
+                     });
+}
+
+extern "C" int exacto_encrypt_sk(exacto_ctx* c, const uint64_t* pt, const uint64_t* sk, double sigma,
+                                 const uint64_t* key, uint64_t stream, uint64_t* ct, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{pt, B * poly_bytes(c)}, {sk, c->L * poly_bytes(c)}}, B * 2 * c->L * poly_bytes(c), ct,
+                     [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_encrypt_sk_dev(c, d[0], d[1], sigma, key, stream, o, B);
+                     });
+}
+
+extern "C" int exacto_encrypt_pk(exacto_ctx* c, const uint64_t* pt, const uint64_t* pk, double sigma,
+                                 const uint64_t* key, uint64_t stream, uint64_t* ct, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{pt, B * poly_bytes(c)}, {pk, 2 * c->L * poly_bytes(c)}}, B * 2 * c->L * poly_bytes(c), ct,
+                     [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_encrypt_pk_dev(c, d[0], d[1], sigma, key, stream, o, B);
+                     });
 }
 
 // ============================================================== diagnostics

@@ -148,3 +148,18 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const PrimeConst* primes, hipStream_t s);
 
 }  // namespace exacto
+
+namespace exacto {
+// ---- key generation / encryption (keygen.hip) ----
+struct ChaChaKey { u64 w[4]; };
+enum { KG_UNIFORM = 0, KG_TERNARY = 1, KG_BINARY = 2, KG_GAUSSIAN = 3 };
+enum { KG_RLK = 0, KG_PK = 1, KG_ENC_SK = 2, KG_ENC_PK = 3 };
+void launch_sample(int kind, const ChaChaKey& key, u64 nonce, u64* out, long out_stride, u64 poly_base,
+                   u64 poly_step, long polys, int n, int L, const PrimeConst* primes, const double* cdt, int cdt_len,
+                   int tail, double total, hipStream_t s);
+void launch_scale_plain(const u64* pt, const u64* delta, u64* dm, long items, int n, int L, const PrimeConst* primes,
+                        hipStream_t s);
+void launch_combine(int op, u64* x, long items, long item_stride, long x1_off, const u64* s, const u64* aux,
+                    const u64* aux2, const u64* pk, const u64* gpow, int n, int L, const PrimeConst* primes,
+                    hipStream_t st);
+}  // namespace exacto

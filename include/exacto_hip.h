@@ -204,6 +204,36 @@ int exacto_dbfv_decrypt_poly_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint6
 
 /* ---- diagnostics ---- */
 /* Copies the last error message of this thread (NUL-terminated); returns its length. */
+/* ---- key generation and encryption on the device ----
+ * keygen.rs:64-162 and encrypt.rs:29-106, 181-229.  Polynomials are sampled exactly as the
+ * reference's samplers define them (sampling/uniform.rs, sampling/gaussian.rs: values of a CoeffPoly
+ * modulo the FIRST ciphertext prime, then reduced modulo every q_i), from a ChaCha20 stream in
+ * counter mode (the reference's ChaCha20Rng primitive; the word stream is this library's own):
+ * `key` = 4 words (256 bits, HOST pointer, also for _dev), `stream` = 64-bit nonce.  Equal
+ * (key, stream) reproduce the same output.  sigma: Gaussian width (BfvParams.sigma, 3.2 default).
+ * sk [L][n], pk [2][L][n], rlk [num_keys][2][L][n], ct [B][2][L][n]: NTT domain.  pt [B][n]:
+ * plaintext coefficients (CoeffPoly mod p). */
+int exacto_gen_secret_key(exacto_ctx* ctx, const uint64_t* key, uint64_t stream, uint64_t* sk);
+int exacto_gen_secret_key_dev(exacto_ctx* ctx, const uint64_t* key, uint64_t stream, uint64_t* sk);
+int exacto_gen_public_key(exacto_ctx* ctx, const uint64_t* sk, double sigma, const uint64_t* key,
+                          uint64_t stream, uint64_t* pk);
+int exacto_gen_public_key_dev(exacto_ctx* ctx, const uint64_t* sk, double sigma, const uint64_t* key,
+                              uint64_t stream, uint64_t* pk);
+/* rlk == NULL: the key is generated straight into the context's resident relinearisation key
+ * (replaces exacto_ctx_load_relin_key: no host build, no upload). */
+int exacto_gen_relin_key(exacto_ctx* ctx, const uint64_t* sk, double sigma, const uint64_t* key,
+                         uint64_t stream, size_t num_keys, uint64_t* rlk);
+int exacto_gen_relin_key_dev(exacto_ctx* ctx, const uint64_t* sk, double sigma, const uint64_t* key,
+                             uint64_t stream, size_t num_keys, uint64_t* rlk);
+int exacto_encrypt_sk(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* sk, double sigma, const uint64_t* key,
+                      uint64_t stream, uint64_t* ct, size_t batch);
+int exacto_encrypt_sk_dev(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* sk, double sigma,
+                          const uint64_t* key, uint64_t stream, uint64_t* ct, size_t batch);
+int exacto_encrypt_pk(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* pk, double sigma, const uint64_t* key,
+                      uint64_t stream, uint64_t* ct, size_t batch);
+int exacto_encrypt_pk_dev(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* pk, double sigma,
+                          const uint64_t* key, uint64_t stream, uint64_t* ct, size_t batch);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic
