@@ -238,6 +238,117 @@ inline CoeffPoly decrypt(const BfvCiphertext& ct, const SecretKey& sk) {
     return decrypt(std::vector<BfvCiphertext>{ct}, sk)[0];
 }
 
+// ---- key generation / encryption on the device (src/bfv/keygen.rs, src/bfv/encrypt.rs:29-106)
+// ChaChaRng stands in for the reference's `R: Rng` argument (ChaCha20Rng): a 256-bit key and a
+// stream counter; every call consumes one stream id, as a call consumes words of the reference's
+// RNG.  The word stream is this library's own (see include/exacto_hip.h).
+struct ChaChaRng {
+    uint64_t key[4];
+    uint64_t stream = 0;
+    explicit ChaChaRng(uint64_t seed) {  // SplitMix64 expansion of a 64-bit seed
+        uint64_t z = seed;
+        for (auto& k : key) {
+            z += 0x9E3779B97F4A7C15ull;
+            uint64_t x = z;
+            x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+            x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+            k = x ^ (x >> 31);
+        }
+    }
+    uint64_t next() { return stream++; }
+};
+
+// PublicKey (keygen.rs:28-34): pk0 = -(a s + e), pk1 = a.
+struct PublicKey {
+    RnsPoly pk0, pk1;
+    BfvParamsPtr params;
+};
+
+namespace detail {
+inline RnsPoly make_poly(const BfvParams& prm, const uint64_t* src) {
+    RnsPoly p;
+    p.ring_degree = prm.ring_degree;
+    p.num_limbs = prm.num_limbs();
+    p.data.assign(src, src + p.ring_degree * p.num_limbs);
+    return p;
+}
+}  // namespace detail
+
+// gen_secret_key_with_rng (keygen.rs:64-79)
+inline SecretKey gen_secret_key_with_rng(const BfvParamsPtr& prm, ChaChaRng& rng) {
+    std::vector<uint64_t> sk(prm->num_limbs() * prm->ring_degree);
+    detail::check(exacto_gen_secret_key(prm->ctx(), rng.key, rng.next(), sk.data()));
+    return SecretKey{detail::make_poly(*prm, sk.data()), prm};
+}
+
+// gen_public_key_with_rng (keygen.rs:87-110)
+inline PublicKey gen_public_key_with_rng(const SecretKey& sk, ChaChaRng& rng) {
+    const BfvParams& prm = *sk.params;
+    const size_t Ln = prm.num_limbs() * prm.ring_degree;
+    std::vector<uint64_t> pk(2 * Ln);
+    detail::check(exacto_gen_public_key(prm.ctx(), sk.poly.data.data(), prm.sigma, rng.key, rng.next(), pk.data()));
+    return PublicKey{detail::make_poly(prm, pk.data()), detail::make_poly(prm, pk.data() + Ln), sk.params};
+}
+
+// gen_relin_key_with_rng (keygen.rs:123-162): gadget_digits keys
+inline RelinKey gen_relin_key_with_rng(const SecretKey& sk, ChaChaRng& rng) {
+    const BfvParams& prm = *sk.params;
+    const size_t Ln = prm.num_limbs() * prm.ring_degree, G = prm.gadget_digits;
+    std::vector<uint64_t> flat(G * 2 * Ln);
+    detail::check(exacto_gen_relin_key(prm.ctx(), sk.poly.data.data(), prm.sigma, rng.key, rng.next(), G,
+                                       flat.data()));
+    RelinKey rlk;
+    rlk.params = sk.params;
+    for (size_t g = 0; g < G; ++g)
+        rlk.keys.emplace_back(detail::make_poly(prm, flat.data() + 2 * g * Ln),
+                              detail::make_poly(prm, flat.data() + (2 * g + 1) * Ln));
+    return rlk;
+}
+
+// encrypt_sk_with_rng / encrypt_pk_with_rng (encrypt.rs:29-106), batched over plaintexts
+inline std::vector<BfvCiphertext> encrypt_batch(const std::vector<CoeffPoly>& pts, const SecretKey* sk,
+                                                const PublicKey* pk, const BfvParamsPtr& prm, ChaChaRng& rng) {
+    const size_t n = prm->ring_degree, Ln = prm->num_limbs() * n;
+    std::vector<uint64_t> pt;
+    for (auto& p : pts) {
+        if (p.coeffs.size() != n) throw ExactoError(2, "dimension mismatch: expected " + std::to_string(n) +
+                                                           ", got " + std::to_string(p.coeffs.size()));
+        pt.insert(pt.end(), p.coeffs.begin(), p.coeffs.end());
+    }
+    std::vector<uint64_t> ct(pts.size() * 2 * Ln);
+    if (sk) {
+        detail::check(exacto_encrypt_sk(prm->ctx(), pt.data(), sk->poly.data.data(), prm->sigma, rng.key,
+                                        rng.next(), ct.data(), pts.size()));
+    } else {
+        std::vector<uint64_t> pkf(pk->pk0.data);
+        pkf.insert(pkf.end(), pk->pk1.data.begin(), pk->pk1.data.end());
+        detail::check(exacto_encrypt_pk(prm->ctx(), pt.data(), pkf.data(), prm->sigma, rng.key, rng.next(),
+                                        ct.data(), pts.size()));
+    }
+    return detail::unflatten(ct, pts.size(), 2, prm);
+}
+inline BfvCiphertext encrypt_sk_with_rng(const CoeffPoly& pt, const SecretKey& sk, const BfvParamsPtr& prm,
+                                         ChaChaRng& rng) {
+    return encrypt_batch({pt}, &sk, nullptr, prm, rng)[0];
+}
+inline BfvCiphertext encrypt_pk_with_rng(const CoeffPoly& pt, const PublicKey& pk, const BfvParamsPtr& prm,
+                                         ChaChaRng& rng) {
+    return encrypt_batch({pt}, nullptr, &pk, prm, rng)[0];
+}
+
+// encode_scalar / decode_scalar (src/bfv/encoding.rs:7-20)
+inline CoeffPoly encode_scalar(uint64_t m, const BfvParamsPtr& prm) {
+    if (m >= prm->plain_modulus)
+        throw ExactoError(1, "invalid parameter: plaintext " + std::to_string(m) + " >= plain_modulus " +
+                                 std::to_string(prm->plain_modulus));
+    CoeffPoly p;
+    p.coeffs.assign(prm->ring_degree, 0);
+    p.coeffs[0] = m;
+    p.modulus = prm->plain_modulus;
+    return p;
+}
+inline uint64_t decode_scalar(const CoeffPoly& p) { return p.coeffs.empty() ? 0 : p.coeffs[0]; }
+
 // ---- exacto::dbfv
 struct DbfvParams {
     BfvParamsPtr bfv_params;

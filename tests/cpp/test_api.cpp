@@ -171,6 +171,24 @@ static int error_cases() {
     return 0;
 }
 
+// keygen.rs / encrypt.rs on the device through the C++ mirror: the reference's own round trips
+// (encrypt.rs:262-285 sk/pk encrypt-decrypt of 42; eval.rs:883-899 3 * 7 = 21 with relinearisation)
+static int keygen_case() {
+    auto prm = BfvParamsBuilder().ring_degree(1024).plain_modulus(257).ct_moduli({1099509805057ull})
+                   .aux_moduli({562949953443841ull}).sigma(3.2).build();
+    ChaChaRng rng(42);
+    auto sk = gen_secret_key_with_rng(prm, rng);
+    auto pk = gen_public_key_with_rng(sk, rng);
+    auto rlk = gen_relin_key_with_rng(sk, rng);
+    if (rlk.keys.size() != prm->gadget_digits) return 20;
+    if (decode_scalar(decrypt(encrypt_sk_with_rng(encode_scalar(42, prm), sk, prm, rng), sk)) != 42) return 21;
+    if (decode_scalar(decrypt(encrypt_pk_with_rng(encode_scalar(42, prm), pk, prm, rng), sk)) != 42) return 22;
+    auto c3 = encrypt_sk_with_rng(encode_scalar(3, prm), sk, prm, rng);
+    auto c7 = encrypt_pk_with_rng(encode_scalar(7, prm), pk, prm, rng);
+    if (decode_scalar(decrypt(bfv_mul_and_relin(c3, c7, rlk), sk)) != 21) return 23;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <fixture-dir> <case>...\n", argv[0]);
@@ -191,6 +209,15 @@ int main(int argc, char** argv) {
     const int e = error_cases();
     std::printf("%s error_cases (%d)\n", e ? "FAIL" : "PASS", e);
     bad |= e != 0;
+    int k;
+    try {
+        k = keygen_case();
+    } catch (const std::exception& ex) {
+        std::printf("ERROR keygen: %s\n", ex.what());
+        k = 99;
+    }
+    std::printf("%s keygen (%d)\n", k ? "FAIL" : "PASS", k);
+    bad |= k != 0;
     if (!bad) std::printf("ALL OK\n");
     return bad;
 }
