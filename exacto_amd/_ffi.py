@@ -93,6 +93,10 @@ _SIGS = [
     ("exacto_encrypt_sk_dev", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
     ("exacto_encrypt_pk", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
     ("exacto_encrypt_pk_dev", [_P, _P, _P, C.c_double, _P, _U64, _P, _SZ], C.c_int),
+    ("exacto_gen_galois_key", [_P, _P, _U64, C.c_double, _P, _U64, _SZ, _P], C.c_int),
+    ("exacto_gen_galois_key_dev", [_P, _P, _U64, C.c_double, _P, _U64, _SZ, _P], C.c_int),
+    ("exacto_bfv_apply_automorphism", [_P, _P, _SZ, _U64, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_apply_automorphism_dev", [_P, _P, _SZ, _U64, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -344,6 +348,24 @@ class HipContext:
         check(self._lib.exacto_encrypt_pk(self._h, pt.ctypes.data, pk.ctypes.data, sigma, k.ctypes.data, stream,
                                           ct.ctypes.data, pt.shape[0]))
         return ct
+
+    def gen_galois_key(self, sk, element, key, stream=0, sigma=3.2, num_keys=None) -> np.ndarray:
+        """keygen.rs:171-209 -> [num_keys][2][L][n]."""
+        k, sk = self._key(key), _u64(sk)
+        nk = self.G if num_keys is None else num_keys
+        gk = np.zeros((nk, 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_gen_galois_key(self._h, sk.ctypes.data, element, sigma, k.ctypes.data, stream, nk,
+                                              gk.ctypes.data))
+        return gk
+
+    def bfv_apply_automorphism(self, ct, element, gk) -> np.ndarray:
+        """eval.rs:512-561 batched: ct [B][2][L][n], gk [K][2][L][n] -> [B][2][L][n]."""
+        ct, gk = _u64(ct), _u64(gk)
+        out = np.zeros((ct.shape[0], 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_bfv_apply_automorphism(self._h, ct.ctypes.data, ct.shape[1], element,
+                                                      gk.ctypes.data if gk.size else None, gk.shape[0],
+                                                      out.ctypes.data, ct.shape[0]))
+        return out
 
     def gen_relin_key_dev(self, sk, key, stream, num_keys, rlk=None, sigma=3.2):
         k = self._key(key)

@@ -217,6 +217,8 @@ struct exacto_ctx {
     bool delta_ok = false;
     u64* enc_buf = nullptr;
     size_t enc_cap = 0;
+    u64* gk_s = nullptr;  // Shoup companions of the Galois key of the last automorphism call
+    size_t gk_s_cap = 0;
     u64 *ext_a = nullptr, *ext_b = nullptr;
     size_t ext_a_cap = 0, ext_b_cap = 0;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
@@ -520,7 +522,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
@@ -1362,6 +1364,7 @@ static int gaussian_table(exacto_ctx* c, double sigma, int* tail, int* len, doub
         size_t cap = c->cdt_cap;
         if (grow((u64**)&c->d_cdt, &cap, cdf.size() * sizeof(double))) return EXACTO_ERR_HIP;
         c->cdt_cap = cap;
+        HIP_TRY(hipStreamSynchronize(c->stream));  // in-flight samplers may still read the old table
         HIP_TRY(hipMemcpy(c->d_cdt, cdf.data(), cdf.size() * sizeof(double), hipMemcpyHostToDevice));
         c->cdt_sigma = sigma;
     }
@@ -1447,7 +1450,9 @@ extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, doubl
     size_t cap = c->gpow_cap;
     if (grow(&c->d_gpow, &cap, gpow.size() * sizeof(u64))) return EXACTO_ERR_HIP;
     c->gpow_cap = cap;
-    HIP_TRY(hipMemcpyAsync(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice, c->stream));
+    // the table is host-pageable and d_gpow may still be read by a previous call's kernels
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice));
     const ChaChaKey k = chacha_key(key);
     // key i: a_i (index 2i) into the rlk1 slot, e_i (index 2i+1) into the rlk0 slot
     if (int e = sample_polys(c, KG_UNIFORM, k, stream, rlk + Ln, 2 * Ln, 0, 2, (long)num_keys, sigma)) return e;
@@ -1552,6 +1557,120 @@ extern "C" int exacto_encrypt_pk_dev(exacto_ctx* c, const uint64_t* pt, const ui
     if (int e = check_ctx(c)) return e;
     if (!pk) return invalid_param("null argument");
     return encrypt_batch(c, pt, nullptr, pk, sigma, key, stream, ct, B);
+}
+
+// ---- Galois automorphisms (eval.rs:512-561, keygen.rs:171-262)
+
+// gen_galois_key_with_rng (keygen.rs:171-209).  s(X^k) is formed as the reference does: limb 0 of s
+// in the coefficient domain (mod q0), sigma_k mod q0, then reduced modulo every q_i (keygen.rs:179-182).
+extern "C" int exacto_gen_galois_key_dev(exacto_ctx* c, const uint64_t* sk, uint64_t element, double sigma,
+                                         const uint64_t* key, uint64_t stream, size_t num_keys, uint64_t* gk) {
+    if (int e = check_ctx(c)) return e;
+    if (!key || !sk || !gk) return invalid_param("null argument");
+    if (num_keys == 0) return 0;
+    const int n = c->n, L = c->L;
+    const long Ln = (long)L * n;
+    size_t cap = c->enc_cap;
+    if (grow(&c->enc_buf, &cap, (size_t)(2 * n + Ln) * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->enc_cap = cap;
+    u64 *t0 = c->enc_buf, *t1 = t0 + n, *s_auto = t1 + n;
+    HIP_TRY(hipMemcpyAsync(t0, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    if (int e = run_ntt(c, contiguous(t0, 1, 1, 0, 1, n), 1, true)) return e;
+    launch_automorph(t0, n, t1, n, 1, 1, n, 1, element, c->d_primes, 0, c->stream);
+    launch_lift_q0(t1, s_auto, 1, n, L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = ntt_items(c, s_auto, 1, 0, L)) return e;
+    std::vector<u64> gpow(num_keys * L);
+    for (int l = 0; l < L; ++l) {
+        const u64 q = c->primes[l];
+        u64 g = 1 % q;
+        const u64 b = c->gbase % q;
+        for (size_t i = 0; i < num_keys; ++i) {
+            gpow[i * L + l] = g;
+            g = (u64)((u128)g * b % q);
+        }
+    }
+    cap = c->gpow_cap;
+    if (grow(&c->d_gpow, &cap, gpow.size() * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->gpow_cap = cap;
+    // the table is host-pageable and d_gpow may still be read by a previous call's kernels
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice));
+    const ChaChaKey k = chacha_key(key);
+    if (int e = sample_polys(c, KG_UNIFORM, k, stream, gk + Ln, 2 * Ln, 0, 2, (long)num_keys, sigma)) return e;
+    if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, gk, 2 * Ln, 1, 2, (long)num_keys, sigma)) return e;
+    if (int e = ntt_items(c, gk, (long)num_keys, 2 * Ln, 2L * L)) return e;
+    launch_combine(KG_GALOIS, gk, (long)num_keys, 2 * Ln, Ln, sk, s_auto, nullptr, nullptr, c->d_gpow, n, L,
+                   c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    // gpow / s_auto scratch is reused by the next call: finish this one first
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// bfv_apply_automorphism (eval.rs:512-561), batched: sigma_k(c0) + sum_i d_i (.) gk_i0, sum_i d_i (.) gk_i1
+// with d = gadget digits of sigma_k(c1) (exact CRT: extension semantics for Q >= 2^64, as relinearize).
+extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t element,
+                                                 const uint64_t* gk, size_t num_keys, uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (polys != 2) return invalid_param("automorphism requires degree-1 ciphertext");
+    if (num_keys == 0 || !gk) return invalid_param("galois key is empty");
+    if (B == 0) return 0;
+    const int n = c->n, L = c->L;
+    const long Ln = (long)L * n;
+    const int guse = (int)std::min<size_t>(c->G, num_keys);
+    const size_t count = (size_t)guse * 2 * Ln;
+    size_t cap = c->gk_s_cap;
+    if (grow(&c->gk_s, &cap, count * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->gk_s_cap = cap;
+    launch_shoup_companions(gk, c->gk_s, (long)count, n, L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    const size_t C = std::min<size_t>(c->chunk, B);
+    if (int e = ensure_workspace(c, C)) return e;
+    for (size_t s0 = 0; s0 < B; s0 += C) {
+        const int cnt = (int)std::min(C, B - s0);
+        const u64* src = ct + s0 * 2 * Ln;
+        u64* dst = out + s0 * 2 * Ln;
+        NttBatch nb{};
+        nb.src = src; nb.src_item_stride = 2 * Ln;
+        nb.dst = c->ws_coefQ; nb.dst_item_stride = 2 * Ln;
+        nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
+        if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
+        launch_automorph(c->ws_coefQ, 2 * Ln, c->ws_T, 2 * Ln, cnt, 2, n, L, element, c->d_primes, -1, c->stream);
+        CHECK_LAUNCH();
+        NttBatch c0{};
+        c0.src = c->ws_T; c0.src_item_stride = 2 * Ln;
+        c0.dst = dst; c0.dst_item_stride = 2 * Ln;
+        c0.ppi = L; c0.prime_base = 0; c0.period = L;
+        if (int e = run_ntt(c, c0, (long)cnt * L, false)) return e;
+        HIP_TRY(hipMemset2DAsync(dst + Ln, 2 * Ln * sizeof(u64), 0, Ln * sizeof(u64), cnt, c->stream));
+        launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream);
+        CHECK_LAUNCH();
+        if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false))
+            return e;
+        launch_relin_mac(dst, 2 * Ln, c->ws_D, gk, c->gk_s, guse, dst, 2 * Ln, cnt, n, L, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+extern "C" int exacto_gen_galois_key(exacto_ctx* c, const uint64_t* sk, uint64_t element, double sigma,
+                                     const uint64_t* key, uint64_t stream, size_t num_keys, uint64_t* gk) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{sk, c->L * poly_bytes(c)}}, num_keys * 2 * c->L * poly_bytes(c), gk,
+                     [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_gen_galois_key_dev(c, d[0], element, sigma, key, stream, num_keys, o);
+                     });
+}
+
+extern "C" int exacto_bfv_apply_automorphism(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t element,
+                                             const uint64_t* gk, size_t num_keys, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    if (polys != 2) return invalid_param("automorphism requires degree-1 ciphertext");
+    return host_call(c, {{ct, B * 2 * c->L * poly_bytes(c)}, {gk, num_keys * 2 * c->L * poly_bytes(c)}},
+                     B * 2 * c->L * poly_bytes(c), out, [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_bfv_apply_automorphism_dev(c, d[0], polys, element, d[1], num_keys, o, B);
+                     });
 }
 
 // Host-pointer variants (synchronous); `key` is always a host pointer to 4 words.

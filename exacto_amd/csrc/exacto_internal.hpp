@@ -153,7 +153,12 @@ namespace exacto {
 // ---- key generation / encryption (keygen.hip) ----
 struct ChaChaKey { u64 w[4]; };
 enum { KG_UNIFORM = 0, KG_TERNARY = 1, KG_BINARY = 2, KG_GAUSSIAN = 3 };
-enum { KG_RLK = 0, KG_PK = 1, KG_ENC_SK = 2, KG_ENC_PK = 3 };
+enum { KG_RLK = 0, KG_PK = 1, KG_ENC_SK = 2, KG_ENC_PK = 3, KG_GALOIS = 4 };
+// sigma_k (keygen.rs:239-262) on coefficient-domain rows [item][poly][limb][n]; prime_fixed >= 0:
+// every row is modulo that prime (limb index ignored)
+void launch_automorph(const u64* in, long in_stride, u64* out, long out_stride, long items, int polys, int n, int L,
+                      u64 k, const PrimeConst* primes, int prime_fixed, hipStream_t s);
+void launch_lift_q0(const u64* v, u64* out, long rows, int n, int L, const PrimeConst* primes, hipStream_t s);
 void launch_sample(int kind, const ChaChaKey& key, u64 nonce, u64* out, long out_stride, u64 poly_base,
                    u64 poly_step, long polys, int n, int L, const PrimeConst* primes, const double* cdt, int cdt_len,
                    int tail, double total, hipStream_t s);

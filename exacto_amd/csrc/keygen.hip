@@ -178,6 +178,7 @@ combine_kernel(int op, u64* __restrict__ x, long item_stride, long x1_off, const
     }
     u64 r = neg_mod(add_mod(as, *x0, q), q);
     if (op == KG_RLK) r = add_mod(r, mul_mod(mul_mod(sv, sv, P), gpow[item * L + i], P), q);
+    if (op == KG_GALOIS) r = add_mod(r, mul_mod(aux[li], gpow[item * L + i], P), q);  // aux = s(X^k)
     *x0 = r;
 }
 
@@ -188,6 +189,87 @@ void launch_combine(int op, u64* x, long items, long item_stride, long x1_off, c
     if (blocks == 0) return;
     hipLaunchKernelGGL(combine_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, st, op, x, item_stride, x1_off, s, aux,
                        aux2, pk, gpow, n, L, primes);
+}
+
+// ---------------------------------------------------------------- Galois automorphisms
+
+// sigma_k on coefficient-domain residues (keygen.rs:239-262), odd k: a signed permutation, as a
+// gather: out[j] = +in[t] if t = j * k^-1 mod 2n < n, else -in[t - n].  rows = [item][poly][limb].
+__global__ void __launch_bounds__(KG_TPB)
+automorph_kernel(const u64* __restrict__ in, long in_stride, u64* __restrict__ out, long out_stride, int polys,
+                 int n, int L, u64 kinv, const PrimeConst* __restrict__ primes, int prime_fixed) {
+    const int nblk = (n + KG_TPB - 1) / KG_TPB;
+    const long row = blockIdx.x / nblk;
+    const int j = (blockIdx.x - row * nblk) * KG_TPB + threadIdx.x;
+    if (j >= n) return;
+    const long pl = (long)polys * L;
+    const long item = row / pl;
+    const long r = row - item * pl;
+    const int i = (int)(r % L);
+    const u64 q = primes[prime_fixed >= 0 ? prime_fixed : i].q;
+    const u64 t = ((u64)j * kinv) % (2 * (u64)n);
+    const u64 v = in[item * in_stride + r * n + (t < (u64)n ? t : t - n)];
+    out[item * out_stride + r * n + j] = t < (u64)n ? v : neg_mod(v, q);
+}
+
+// even k (not an automorphism of the ring; the reference computes it anyway): the literal
+// accumulation, one thread per row.  out must be zeroed.
+__global__ void automorph_serial_kernel(const u64* __restrict__ in, long in_stride, u64* __restrict__ out,
+                                        long out_stride, int polys, int n, int L, u64 k, long rows,
+                                        const PrimeConst* __restrict__ primes, int prime_fixed) {
+    const long row = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= rows) return;
+    const long pl = (long)polys * L;
+    const long item = row / pl;
+    const long r = row - item * pl;
+    const int i = (int)(r % L);
+    const u64 q = primes[prime_fixed >= 0 ? prime_fixed : i].q;
+    const u64* a = in + item * in_stride + r * n;
+    u64* o = out + item * out_stride + r * n;
+    for (int c = 0; c < n; ++c) {
+        if (a[c] == 0) continue;
+        const u64 e = ((u64)c * k) % (2 * (u64)n);
+        if (e < (u64)n) o[e] = add_mod(o[e], a[c], q);
+        else o[e - n] = sub_mod(o[e - n], a[c], q);
+    }
+}
+
+void launch_automorph(const u64* in, long in_stride, u64* out, long out_stride, long items, int polys, int n, int L,
+                      u64 k, const PrimeConst* primes, int prime_fixed, hipStream_t s) {
+    const u64 two_n = 2 * (u64)n;
+    k %= two_n;
+    const long rows = items * polys * L;
+    if (rows == 0) return;
+    if (k & 1) {
+        u64 kinv = 1;  // k^-1 mod 2n by Newton iteration (2n is a power of two)
+        for (int it = 0; it < 7; ++it) kinv = kinv * (2 - k * kinv);
+        kinv &= two_n - 1;
+        const long blocks = rows * ((n + KG_TPB - 1) / KG_TPB);
+        hipLaunchKernelGGL(automorph_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, in, in_stride, out,
+                           out_stride, polys, n, L, kinv, primes, prime_fixed);
+    } else {
+        (void)hipMemset2DAsync(out, out_stride * sizeof(u64), 0, (size_t)polys * L * n * sizeof(u64), items, s);
+        hipLaunchKernelGGL(automorph_serial_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, in,
+                           in_stride, out, out_stride, polys, n, L, k, rows, primes, prime_fixed);
+    }
+}
+
+// v (canonical mod q0, [rows][n]) -> [rows][L][n] residues mod each q_i (RnsPoly::from_coeff_poly)
+__global__ void __launch_bounds__(KG_TPB)
+lift_q0_kernel(const u64* __restrict__ v, u64* __restrict__ out, int n, int L, const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + KG_TPB - 1) / KG_TPB;
+    const long row = blockIdx.x / nblk;
+    const int j = (blockIdx.x - row * nblk) * KG_TPB + threadIdx.x;
+    if (j >= n) return;
+    const u64 x = v[row * n + j];
+    for (int i = 0; i < L; ++i)
+        out[(row * L + i) * n + j] = i == 0 ? x : reduce64(x, primes[i].q, primes[i].mu64);
+}
+
+void launch_lift_q0(const u64* v, u64* out, long rows, int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = rows * ((n + KG_TPB - 1) / KG_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(lift_q0_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, v, out, n, L, primes);
 }
 
 }  // namespace exacto

@@ -234,6 +234,21 @@ int exacto_encrypt_pk(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* pk, d
 int exacto_encrypt_pk_dev(exacto_ctx* ctx, const uint64_t* pt, const uint64_t* pk, double sigma,
                           const uint64_t* key, uint64_t stream, uint64_t* ct, size_t batch);
 
+/* ---- Galois automorphisms ----
+ * gen_galois_key_with_rng (keygen.rs:171-209): key-switch key from s(X^element) to s(X), gk =
+ * [num_keys][2][L][n]; s(X^element) is formed from limb 0 of s as the reference does
+ * (keygen.rs:179-182).  bfv_apply_automorphism (eval.rs:512-561), batched: ct/out [B][2][L][n],
+ * polys must be 2 ("automorphism requires degree-1 ciphertext"); min(G, num_keys) digits are
+ * used; an empty key is InvalidParam (the reference panics on it). */
+int exacto_gen_galois_key(exacto_ctx* ctx, const uint64_t* sk, uint64_t element, double sigma,
+                          const uint64_t* key, uint64_t stream, size_t num_keys, uint64_t* gk);
+int exacto_gen_galois_key_dev(exacto_ctx* ctx, const uint64_t* sk, uint64_t element, double sigma,
+                              const uint64_t* key, uint64_t stream, size_t num_keys, uint64_t* gk);
+int exacto_bfv_apply_automorphism(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t element,
+                                  const uint64_t* gk, size_t num_keys, uint64_t* out, size_t batch);
+int exacto_bfv_apply_automorphism_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t element,
+                                      const uint64_t* gk, size_t num_keys, uint64_t* out, size_t batch);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic

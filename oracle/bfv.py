@@ -377,6 +377,62 @@ def relinearize(ct, rlk):
     return BfvCiphertext([c0, c1], params)
 
 
+# ------------------------------------------------------------------ Galois automorphisms
+
+class GaloisKey:
+    """keygen.rs:49-56: key-switch key from s(X^element) to s(X)."""
+
+    def __init__(self, keys, element, params):
+        self.keys = keys
+        self.element = element
+        self.params = params
+
+
+def apply_automorphism(poly: CoeffPoly, k: int) -> CoeffPoly:
+    """keygen.rs:239-262: X^i -> X^(ik) mod X^n + 1, accumulated with mod_add / mod_sub."""
+    n, q = len(poly.coeffs), poly.modulus
+    res = [0] * n
+    for i, c in enumerate(poly.coeffs):
+        if c == 0:
+            continue
+        e = (i * k) % (2 * n)
+        if e < n:
+            res[e] = (res[e] + c) % q
+        else:
+            res[e - n] = (res[e - n] - c) % q
+    return CoeffPoly(res, q)
+
+
+def bfv_apply_automorphism(ct, gk):
+    """eval.rs:512-561 (to_coeff_poly under extension semantics for Q >= 2^64, as relinearize)."""
+    if len(ct.c) != 2:
+        raise ExactoError.invalid_param("automorphism requires degree-1 ciphertext")
+    params = ct.params
+    basis = params.ct_basis
+    k = gk.element
+    c0 = apply_automorphism(ct.c[0].to_coeff_poly(basis), k)
+    c1 = apply_automorphism(ct.c[1].to_coeff_poly(basis), k)
+    c0f = RnsPoly.from_coeff_poly(c0, basis)
+    digits = gadget_decompose(c1, params.gadget_base, params.gadget_digits)
+    c1f = None
+    for i, digit in enumerate(digits):
+        if i >= len(gk.keys):
+            break
+        d = RnsPoly.from_coeff_poly(digit, basis)
+        c0f = c0f.add(d.mul(gk.keys[i][0]))
+        p1 = d.mul(gk.keys[i][1])
+        c1f = p1 if c1f is None else c1f.add(p1)
+    if c1f is None:
+        raise ExactoError.invalid_param("galois key is empty")  # the reference unwraps None (panic)
+    return BfvCiphertext([c0f, c1f], params)
+
+
+def galois_s_auto(sk_poly: RnsPoly, k: int, basis) -> RnsPoly:
+    """keygen.rs:179-182: limb 0 of s in the coefficient domain (mod q0), permuted, lifted to every limb."""
+    s0 = sk_poly.components[0].to_coeff_poly()
+    return RnsPoly.from_coeff_poly(apply_automorphism(s0, k), basis)
+
+
 # ------------------------------------------------------------------ keygen / encrypt / decrypt
 # Not on the hot path: mathematically equivalent restatement of bfv/keygen.rs:64-162 and
 # bfv/encrypt.rs:79-178 with this build's own sampler (signed small values reduced per limb).

@@ -296,3 +296,13 @@ def test_dbfv_vectors(name):
         B = odbfv.DbfvCiphertext([np_to_ct(b[i, k], prm) for k in range(d)], d, 0, dp)
         r = odbfv.dbfv_mul(A, B, rk)
         assert np.array_equal(np.stack([ct_to_np(l) for l in r.limbs]), z[f"{name}__out"][i])
+
+
+def test_apply_automorphism_kat():
+    """keygen.rs:264-279: X -> X^3 on 1 + X + X^2 + X^3 in Z_17[X]/(X^4 + 1) = [1, 1, 16, 1]."""
+    from oracle import bfv as obfv
+    from oracle.ring import CoeffPoly
+    assert obfv.apply_automorphism(CoeffPoly([1, 1, 1, 1], 17), 3).coeffs == [1, 1, 16, 1]
+    # sigma_k then sigma_k^-1 is the identity (odd k)
+    p = CoeffPoly([5, 0, 7, 1, 0, 0, 3, 2], 97)
+    assert obfv.apply_automorphism(obfv.apply_automorphism(p, 3), 11).coeffs == p.coeffs  # 3 * 11 = 33 = 1 mod 16
