@@ -336,6 +336,48 @@ inline BfvCiphertext encrypt_pk_with_rng(const CoeffPoly& pt, const PublicKey& p
     return encrypt_batch({pt}, nullptr, &pk, prm, rng)[0];
 }
 
+// GaloisKey (keygen.rs:49-56) and bfv_apply_automorphism (eval.rs:512-561)
+struct GaloisKey {
+    std::vector<std::pair<RnsPoly, RnsPoly>> keys;
+    size_t element = 0;
+    BfvParamsPtr params;
+};
+
+inline GaloisKey gen_galois_key_with_rng(const SecretKey& sk, size_t element, ChaChaRng& rng) {
+    const BfvParams& prm = *sk.params;
+    const size_t Ln = prm.num_limbs() * prm.ring_degree, G = prm.gadget_digits;
+    std::vector<uint64_t> flat(G * 2 * Ln);
+    detail::check(exacto_gen_galois_key(prm.ctx(), sk.poly.data.data(), element, prm.sigma, rng.key, rng.next(), G,
+                                        flat.data()));
+    GaloisKey gk;
+    gk.element = element;
+    gk.params = sk.params;
+    for (size_t g = 0; g < G; ++g)
+        gk.keys.emplace_back(detail::make_poly(prm, flat.data() + 2 * g * Ln),
+                             detail::make_poly(prm, flat.data() + (2 * g + 1) * Ln));
+    return gk;
+}
+
+inline std::vector<BfvCiphertext> bfv_apply_automorphism(const std::vector<BfvCiphertext>& cts, const GaloisKey& gk) {
+    if (cts.empty()) return {};
+    const BfvParams& prm = *cts[0].params;
+    const size_t polys = cts[0].c.size();
+    if (polys != 2) throw ExactoError(1, "invalid parameter: automorphism requires degree-1 ciphertext");
+    auto flat = detail::flatten(cts, polys);
+    std::vector<uint64_t> key;
+    for (auto& k : gk.keys) {
+        key.insert(key.end(), k.first.data.begin(), k.first.data.end());
+        key.insert(key.end(), k.second.data.begin(), k.second.data.end());
+    }
+    std::vector<uint64_t> out(flat.size());
+    detail::check(exacto_bfv_apply_automorphism(prm.ctx(), flat.data(), polys, gk.element, key.data(),
+                                                gk.keys.size(), out.data(), cts.size()));
+    return detail::unflatten(out, cts.size(), 2, cts[0].params);
+}
+inline BfvCiphertext bfv_apply_automorphism(const BfvCiphertext& ct, const GaloisKey& gk) {
+    return bfv_apply_automorphism(std::vector<BfvCiphertext>{ct}, gk)[0];
+}
+
 // encode_scalar / decode_scalar (src/bfv/encoding.rs:7-20)
 inline CoeffPoly encode_scalar(uint64_t m, const BfvParamsPtr& prm) {
     if (m >= prm->plain_modulus)

@@ -186,6 +186,15 @@ static int keygen_case() {
     auto c3 = encrypt_sk_with_rng(encode_scalar(3, prm), sk, prm, rng);
     auto c7 = encrypt_pk_with_rng(encode_scalar(7, prm), pk, prm, rng);
     if (decode_scalar(decrypt(bfv_mul_and_relin(c3, c7, rlk), sk)) != 21) return 23;
+    // eval.rs:954-976: sigma_3(1 + 2X) = 1 + 2X^3
+    CoeffPoly m;
+    m.coeffs.assign(prm->ring_degree, 0);
+    m.coeffs[0] = 1;
+    m.coeffs[1] = 2;
+    m.modulus = prm->plain_modulus;
+    auto gk = gen_galois_key_with_rng(sk, 3, rng);
+    auto d = decrypt(bfv_apply_automorphism(encrypt_sk_with_rng(m, sk, prm, rng), gk), sk);
+    if (d.coeffs[0] != 1 || d.coeffs[1] != 0 || d.coeffs[2] != 0 || d.coeffs[3] != 2) return 24;
     return 0;
 }
 
