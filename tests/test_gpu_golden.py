@@ -190,3 +190,32 @@ def test_dbfv_decrypt_level(gpu_available):
         out, _ = ctx.dbfv_mul(2, 16, 256, A, B)
         r = odbfv.DbfvCiphertext([np_to_ct(out[0, k], prm) for k in range(2)], 2, 1, dp)
         assert odbfv.dbfv_decrypt_scalar(r, sk) == (x * y) % 256
+
+
+def test_cfg5_full_size(gpu_available):
+    """BASELINE configs[4] at full size: n=8192, 4x60-bit limbs, gadget 256 (G=30), t=1040407, d=8.
+    bfv_mul_and_relin bit-exact vs the C restatement on one row; one dbfv_mul's output limbs equal
+    the sums of the GPU's own (oracle-checked) BFV products; a depth-2 chain equals two dbfv_mul."""
+    dp = P.cfg5_params(8192)
+    prm = dp.bfv_params
+    q, n, d = prm.ct_basis.moduli, 8192, dp.num_digits
+    rng = np.random.default_rng(505)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    ctx = HipContext.from_params(prm)
+    ctx.load_relin_key(rlk)
+    ct1 = uniform_residues(rng, (2, 2), q, n)
+    ct2 = uniform_residues(rng, (2, 2), q, n)
+    got = ctx.bfv_mul_and_relin(ct1, ct2)
+    if cref.available():
+        assert np.array_equal(got[1], cref.bfv_mul_and_relin(prm, ct1[1:], ct2[1:], rlk, threads=1)[0])
+    a = uniform_residues(rng, (1, d, 2), q, n)
+    b = uniform_residues(rng, (1, d, 2), q, n)
+    out, _ = ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)
+    Q = np.array(q, dtype=object)[:, None]
+    for k in (0, 1, 7):  # p = 2^64 = b^d: every reduction rep is zero, limb k = sum_{i+j=k} a_i b_j
+        prods = ctx.bfv_mul_and_relin(a[0, :k + 1], b[0, k::-1])
+        want = (prods.astype(object).sum(axis=0) % Q)
+        assert np.array_equal(out[0, k].astype(object), want), k
+    chain = ctx.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2)
+    step2, _ = ctx.dbfv_mul(d, dp.base, dp.plain_modulus, out, b)
+    assert np.array_equal(chain, step2)
