@@ -97,6 +97,16 @@ _SIGS = [
     ("exacto_gen_galois_key_dev", [_P, _P, _U64, C.c_double, _P, _U64, _SZ, _P], C.c_int),
     ("exacto_bfv_apply_automorphism", [_P, _P, _SZ, _U64, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_apply_automorphism_dev", [_P, _P, _SZ, _U64, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_plain_mul", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_plain_mul_dev", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_plain_add", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_plain_add_dev", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
+    ("exacto_bfv_inner_product", [_P, _P, _P, _SZ, _SZ, _P], C.c_int),
+    ("exacto_bfv_inner_product_dev", [_P, _P, _P, _SZ, _SZ, _P], C.c_int),
+    ("exacto_bfv_monomial_mul", [_P, _P, _SZ, _U64, _P, _SZ], C.c_int),
+    ("exacto_bfv_monomial_mul_dev", [_P, _P, _SZ, _U64, _P, _SZ], C.c_int),
+    ("exacto_bfv_trace", [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_trace_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -365,6 +375,59 @@ class HipContext:
         check(self._lib.exacto_bfv_apply_automorphism(self._h, ct.ctypes.data, ct.shape[1], element,
                                                       gk.ctypes.data if gk.size else None, gk.shape[0],
                                                       out.ctypes.data, ct.shape[0]))
+        return out
+
+    def _pt(self, pt, rows):
+        pt = _u64(pt).reshape(rows, self.n)
+        return pt
+
+    def bfv_plain_mul(self, ct, pt) -> np.ndarray:
+        """eval.rs:468-486 batched: ct [B][polys][L][n], pt [B][n] -> [B][polys][L][n]."""
+        ct = _u64(ct)
+        pt = self._pt(pt, ct.shape[0])
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_bfv_plain_mul(self._h, ct.ctypes.data, ct.shape[1], pt.ctypes.data, out.ctypes.data,
+                                             ct.shape[0]))
+        return out
+
+    def bfv_plain_add(self, ct, pt) -> np.ndarray:
+        """eval.rs:489-503 batched: c0 + Delta m."""
+        ct = _u64(ct)
+        pt = self._pt(pt, ct.shape[0])
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_bfv_plain_add(self._h, ct.ctypes.data, ct.shape[1], pt.ctypes.data, out.ctypes.data,
+                                             ct.shape[0]))
+        return out
+
+    def bfv_inner_product(self, cts, pts) -> np.ndarray:
+        """eval.rs:588-606: cts [K][polys][L][n], pts [K][n] -> [polys][L][n]."""
+        cts = _u64(cts)
+        K = cts.shape[0]
+        pts = _u64(pts).reshape(K, self.n) if K else _u64(pts)
+        polys = cts.shape[1] if K else 2
+        out = np.zeros((polys, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_bfv_inner_product(self._h, cts.ctypes.data, pts.ctypes.data, K, polys,
+                                                 out.ctypes.data))
+        return out
+
+    def bfv_monomial_mul(self, ct, j) -> np.ndarray:
+        """eval.rs:613-652 batched: X^j * ct."""
+        ct = _u64(ct)
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_bfv_monomial_mul(self._h, ct.ctypes.data, ct.shape[1], j, out.ctypes.data,
+                                                ct.shape[0]))
+        return out
+
+    def bfv_trace(self, ct, elements, gks) -> np.ndarray:
+        """eval.rs:572-586 batched: elements [E], gks [E][K][2][L][n] (the key of elements[e] at e)."""
+        ct = _u64(ct)
+        el = np.ascontiguousarray(np.asarray(elements, dtype=np.uint64))
+        gks = _u64(gks)
+        E = el.shape[0]
+        nk = gks.shape[1] if E else 0
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_bfv_trace(self._h, ct.ctypes.data, ct.shape[1], el.ctypes.data if E else None, E,
+                                         gks.ctypes.data if E else None, nk, out.ctypes.data, ct.shape[0]))
         return out
 
     def gen_relin_key_dev(self, sk, key, stream, num_keys, rlk=None, sigma=3.2):

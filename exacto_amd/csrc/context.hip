@@ -219,6 +219,8 @@ struct exacto_ctx {
     size_t enc_cap = 0;
     u64* gk_s = nullptr;  // Shoup companions of the Galois key of the last automorphism call
     size_t gk_s_cap = 0;
+    u64* pl_buf = nullptr;  // lifted plaintexts / monomial scratch
+    size_t pl_cap = 0;
     u64 *ext_a = nullptr, *ext_b = nullptr;
     size_t ext_a_cap = 0, ext_b_cap = 0;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
@@ -522,7 +524,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
@@ -1009,7 +1011,7 @@ static int host_call(exacto_ctx* c, const std::vector<std::pair<const void*, siz
     std::vector<u64*> dins;
     char* p = (char*)c->io;
     for (auto& in : ins) {
-        HIP_TRY(hipMemcpy(p, in.first, in.second, hipMemcpyHostToDevice));
+        if (in.second) HIP_TRY(hipMemcpy(p, in.first, in.second, hipMemcpyHostToDevice));
         dins.push_back((u64*)p);
         p += (in.second + 255) / 256 * 256;
     }
@@ -1670,6 +1672,159 @@ extern "C" int exacto_bfv_apply_automorphism(exacto_ctx* c, const uint64_t* ct, 
     return host_call(c, {{ct, B * 2 * c->L * poly_bytes(c)}, {gk, num_keys * 2 * c->L * poly_bytes(c)}},
                      B * 2 * c->L * poly_bytes(c), out, [&](std::vector<u64*>& d, u64* o) {
                          return exacto_bfv_apply_automorphism_dev(c, d[0], polys, element, d[1], num_keys, o, B);
+                     });
+}
+
+// ---- plaintext-ciphertext operations and the trace (bfv/eval.rs:468-503, 572-652) ----
+
+static int pl_scratch(exacto_ctx* c, size_t words) {
+    size_t cap = c->pl_cap;
+    if (grow(&c->pl_buf, &cap, words * sizeof(u64))) return EXACTO_ERR_HIP;
+    c->pl_cap = cap;
+    return 0;
+}
+
+// pt [items][n] (any u64) -> NTT(pt mod q_i [* Delta_i]) as [items][L][n] in c->pl_buf
+static int lift_plain(exacto_ctx* c, const u64* pt, long items, bool delta) {
+    const long Ln = (long)c->L * c->n;
+    if (delta)
+        if (int e = delta_residues(c)) return e;
+    if (int e = pl_scratch(c, (size_t)items * Ln)) return e;
+    launch_scale_plain(pt, delta ? c->d_delta : nullptr, c->pl_buf, items, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return ntt_items(c, c->pl_buf, items, Ln, c->L);
+}
+
+extern "C" int exacto_bfv_plain_mul_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* pt,
+                                        uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!ct || !pt || !out) return invalid_param("null argument");
+    if (polys == 0) return invalid_param("ciphertext has no components");
+    if (B == 0) return 0;
+    if (int e = lift_plain(c, pt, (long)B, false)) return e;
+    launch_plain_apply(PLAIN_MUL, ct, out, (long)B, (int)polys, c->pl_buf, (long)c->L * c->n, c->n, c->L,
+                       c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_bfv_plain_add_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* pt,
+                                        uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!ct || !pt || !out) return invalid_param("null argument");
+    if (polys == 0) return invalid_param("ciphertext has no components");
+    if (B == 0) return 0;
+    if (int e = lift_plain(c, pt, (long)B, true)) return e;
+    launch_plain_apply(PLAIN_ADD, ct, out, (long)B, (int)polys, c->pl_buf, (long)c->L * c->n, c->n, c->L,
+                       c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_bfv_inner_product_dev(exacto_ctx* c, const uint64_t* cts, const uint64_t* pts, size_t K,
+                                            size_t polys, uint64_t* out) {
+    if (int e = check_ctx(c)) return e;
+    if (K == 0) return invalid_param("mismatched ct/pt lengths");
+    if (!cts || !pts || !out) return invalid_param("null argument");
+    if (polys == 0) return invalid_param("ciphertext has no components");
+    if (int e = lift_plain(c, pts, (long)K, false)) return e;
+    launch_inner_product(cts, c->pl_buf, out, (int)K, (int)polys, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_bfv_monomial_mul_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t j,
+                                           uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!ct || !out) return invalid_param("null argument");
+    if (B == 0 || polys == 0) return 0;
+    const long Ln = (long)c->L * c->n;
+    j %= 2 * (u64)c->n;
+    if (j == 0) {  // eval.rs:619-621: a clone
+        if (out != ct)
+            HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+        return 0;
+    }
+    if (int e = pl_scratch(c, (size_t)Ln)) return e;
+    launch_monomial(c->pl_buf, j, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = ntt_items(c, c->pl_buf, 1, 0, c->L)) return e;
+    launch_plain_apply(PLAIN_MUL, ct, out, (long)B, (int)polys, c->pl_buf, 0, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+// eval.rs:572-586 batched: result = ct; for k in elements: result += sigma_k(result).
+// elements is a host array [E]; gks = [E][num_keys][2][L][n], the key of elements[e] at index e.
+extern "C" int exacto_bfv_trace_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* elements,
+                                    size_t E, const uint64_t* gks, size_t num_keys, uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!ct || !out || (E && (!elements || !gks))) return invalid_param("null argument");
+    if (B == 0) return 0;
+    const long Ln = (long)c->L * c->n;
+    const size_t words = B * polys * Ln;
+    if (out != ct) HIP_TRY(hipMemcpyAsync(out, ct, words * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    if (E == 0) return 0;
+    if (polys != 2) return invalid_param("automorphism requires degree-1 ciphertext");
+    u64* rot = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&rot, words * sizeof(u64), c->stream));
+    int rc = 0;
+    for (size_t e = 0; e < E && rc == 0; ++e) {
+        rc = exacto_bfv_apply_automorphism_dev(c, out, 2, elements[e], gks + e * num_keys * 2 * Ln, num_keys, rot, B);
+        if (rc == 0) {
+            launch_pointwise(PwOp::Add, out, rot, out, (long)B * 2 * c->L, c->n, c->L, nullptr, c->d_primes,
+                             c->stream);
+            if (hipGetLastError() != hipSuccess) rc = EXACTO_ERR_HIP;
+        }
+    }
+    HIP_TRY(hipFreeAsync(rot, c->stream));
+    return rc;
+}
+
+extern "C" int exacto_bfv_plain_mul(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* pt,
+                                    uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * polys * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}, {pt, B * poly_bytes(c)}}, ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_bfv_plain_mul_dev(c, d[0], polys, d[1], o, B);
+    });
+}
+
+extern "C" int exacto_bfv_plain_add(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* pt,
+                                    uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * polys * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}, {pt, B * poly_bytes(c)}}, ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_bfv_plain_add_dev(c, d[0], polys, d[1], o, B);
+    });
+}
+
+extern "C" int exacto_bfv_inner_product(exacto_ctx* c, const uint64_t* cts, const uint64_t* pts, size_t K,
+                                        size_t polys, uint64_t* out) {
+    if (!c) return invalid_param("null context");
+    if (K == 0) return invalid_param("mismatched ct/pt lengths");
+    const size_t ctb = polys * c->L * poly_bytes(c);
+    return host_call(c, {{cts, K * ctb}, {pts, K * poly_bytes(c)}}, ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_bfv_inner_product_dev(c, d[0], d[1], K, polys, o);
+    });
+}
+
+extern "C" int exacto_bfv_monomial_mul(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t j, uint64_t* out,
+                                       size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * polys * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}}, ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_bfv_monomial_mul_dev(c, d[0], polys, j, o, B);
+    });
+}
+
+extern "C" int exacto_bfv_trace(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* elements, size_t E,
+                                const uint64_t* gks, size_t num_keys, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * polys * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}, {gks, E * num_keys * 2 * c->L * poly_bytes(c)}}, ctb, out,
+                     [&](std::vector<u64*>& d, u64* o) {
+                         return exacto_bfv_trace_dev(c, d[0], polys, elements, E, d[1], num_keys, o, B);
                      });
 }
 

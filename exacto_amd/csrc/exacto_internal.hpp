@@ -167,4 +167,12 @@ void launch_scale_plain(const u64* pt, const u64* delta, u64* dm, long items, in
 void launch_combine(int op, u64* x, long items, long item_stride, long x1_off, const u64* s, const u64* aux,
                     const u64* aux2, const u64* pk, const u64* gpow, int n, int L, const PrimeConst* primes,
                     hipStream_t st);
+
+// ---- plaintext-ciphertext operations (plain.hip) ----
+enum { PLAIN_MUL = 0, PLAIN_ADD = 1 };
+void launch_plain_apply(int op, const u64* x, u64* out, long items, int polys, const u64* pt, long pt_item_stride,
+                        int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int polys, int n, int L,
+                          const PrimeConst* primes, hipStream_t s);
+void launch_monomial(u64* out, u64 j, int n, int L, const PrimeConst* primes, hipStream_t s);
 }  // namespace exacto

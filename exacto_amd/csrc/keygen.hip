@@ -130,7 +130,8 @@ scale_plain_kernel(const u64* __restrict__ pt, const u64* __restrict__ delta, u6
     const long b = row / L;
     const int i = (int)(row - b * L);
     const PrimeConst& P = primes[i];
-    dm[row * n + j] = mul_mod(reduce64(pt[b * n + j], P.q, P.mu64), delta[i], P);
+    const u64 m = reduce64(pt[b * n + j], P.q, P.mu64);
+    dm[row * n + j] = delta ? mul_mod(m, delta[i], P) : m;  // delta == nullptr: plain lift
 }
 
 void launch_scale_plain(const u64* pt, const u64* delta, u64* dm, long items, int n, int L, const PrimeConst* primes,

@@ -1,0 +1,96 @@
+// Plaintext-ciphertext operations on the device (the linear layer under
+// CoeffsToSlots): bfv_plain_mul, bfv_plain_add, bfv_inner_product, bfv_monomial_mul
+// (bfv/eval.rs:468-503, 588-652).  All of them are coefficient-wise in the NTT domain once the
+// plaintext is lifted into it, so each is one HBM-bound streaming pass over the ciphertexts:
+//   plain_mul  : c_p <- c_p * NTT(pt mod q_i)                        (eval.rs:468-486)
+//   plain_add  : c_0 <- c_0 + NTT(Delta * pt mod q_i)                 (eval.rs:489-503)
+//   inner prod : sum_k c_{k,p} * NTT(pt_k mod q_i)                    (eval.rs:588-606)
+//   monomial   : c_p <- c_p * NTT(X^j)  -- the reference's coefficient rotation with sign
+//                (eval.rs:613-652) is multiplication by X^j in Z_q[X]/(X^n+1), which the NTT
+//                diagonalises; per limb, rotating the CRT representative mod Q and reducing mod
+//                q_i equals rotating the residue mod q_i, so this is bit-identical.
+#include "exacto_internal.hpp"
+
+namespace exacto {
+
+static constexpr int PL_TPB = 256;
+
+// rows [item][poly][limb][n]; plaintext rows [item (or 0 when pt_item_stride == 0)][limb][n]
+//   op PLAIN_MUL: out = x * pt      (every poly)
+//   op PLAIN_ADD: out = x + pt on poly 0, x elsewhere
+__global__ void __launch_bounds__(PL_TPB)
+plain_apply_kernel(int op, const u64* __restrict__ x, u64* __restrict__ out, int polys, const u64* __restrict__ pt,
+                   long pt_item_stride, int n, int L, const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;
+    const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (j >= n) return;
+    const long pl = (long)polys * L;
+    const long item = row / pl;
+    const long r = row - item * pl;
+    const int i = (int)(r % L);
+    const int poly = (int)(r / L);
+    const PrimeConst& P = primes[i];
+    const long idx = row * n + j;
+    const u64 v = x[idx];
+    const u64 m = pt[item * pt_item_stride + (long)i * n + j];
+    u64 res;
+    if (op == PLAIN_MUL) res = mul_mod(v, m, P);
+    else res = poly == 0 ? add_mod(v, m, P.q) : v;
+    out[idx] = res;
+}
+
+void launch_plain_apply(int op, const u64* x, u64* out, long items, int polys, const u64* pt, long pt_item_stride,
+                        int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = items * polys * L * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(plain_apply_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, op, x, out, polys, pt,
+                       pt_item_stride, n, L, primes);
+}
+
+// out[poly][limb][j] = sum_k cts[k][poly][limb][j] * pts[k][limb][j]  (accumulated in the
+// reference's order: acc = c_0 pt_0, then acc + c_k pt_k, every step reduced mod q_i)
+__global__ void __launch_bounds__(PL_TPB)
+inner_product_kernel(const u64* __restrict__ cts, const u64* __restrict__ pts, u64* __restrict__ out, int K,
+                     int polys, int n, int L, const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;  // row = poly * L + limb
+    const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (j >= n) return;
+    const int i = (int)(row % L);
+    const PrimeConst& P = primes[i];
+    const long ct_stride = (long)polys * L * n;
+    const long Ln = (long)L * n;
+    u64 acc = 0;
+    for (int k = 0; k < K; ++k)
+        acc = add_mod(acc, mul_mod(cts[k * ct_stride + row * n + j], pts[k * Ln + (long)i * n + j], P), P.q);
+    out[row * n + j] = acc;
+}
+
+void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int polys, int n, int L,
+                          const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)polys * L * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0 || K == 0) return;
+    hipLaunchKernelGGL(inner_product_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, cts, pts, out, K, polys, n,
+                       L, primes);
+}
+
+// X^j mod (X^n + 1) as coefficient rows [limb][n]: +1 at j (j < n) or q_i - 1 at j - n.
+__global__ void __launch_bounds__(PL_TPB)
+monomial_kernel(u64* __restrict__ out, u64 jj, int n, int L, const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;
+    const int c = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (c >= n) return;
+    const u64 pos = jj < (u64)n ? jj : jj - n;
+    u64 v = 0;
+    if ((u64)c == pos) v = jj < (u64)n ? 1 : primes[row].q - 1;
+    out[row * n + c] = v;
+}
+
+void launch_monomial(u64* out, u64 j, int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)L * ((n + PL_TPB - 1) / PL_TPB);
+    hipLaunchKernelGGL(monomial_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, j, n, L, primes);
+}
+
+}  // namespace exacto

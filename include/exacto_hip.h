@@ -249,6 +249,36 @@ int exacto_bfv_apply_automorphism(exacto_ctx* ctx, const uint64_t* ct, size_t po
 int exacto_bfv_apply_automorphism_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t element,
                                       const uint64_t* gk, size_t num_keys, uint64_t* out, size_t batch);
 
+/* Plaintext-ciphertext operations (CoeffsToSlots' linear layer), all in the NTT domain.
+ * ct/out [B][polys][L][n]; pt [B][n] plaintext coefficients (any u64, reduced mod each q_i).
+ *   bfv_plain_mul     replaces bfv::eval::bfv_plain_mul      (src/bfv/eval.rs:468-486)
+ *   bfv_plain_add     replaces bfv::eval::bfv_plain_add      (src/bfv/eval.rs:489-503), c0 + Delta m
+ *   bfv_inner_product replaces bfv::eval::bfv_inner_product  (src/bfv/eval.rs:588-606):
+ *                     cts [K][polys][L][n], pts [K][n] -> out [polys][L][n]; K == 0 is InvalidParam
+ *   bfv_monomial_mul  replaces bfv::eval::bfv_monomial_mul   (src/bfv/eval.rs:613-652), X^j, j mod 2n
+ *   bfv_trace         replaces bfv::eval::bfv_trace          (src/bfv/eval.rs:572-586): elements is a
+ *                     HOST array [E]; gks [E][num_keys][2][L][n] holds the key of elements[e] at e. */
+int exacto_bfv_plain_mul(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* pt, uint64_t* out,
+                         size_t batch);
+int exacto_bfv_plain_mul_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* pt, uint64_t* out,
+                             size_t batch);
+int exacto_bfv_plain_add(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* pt, uint64_t* out,
+                         size_t batch);
+int exacto_bfv_plain_add_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* pt, uint64_t* out,
+                             size_t batch);
+int exacto_bfv_inner_product(exacto_ctx* ctx, const uint64_t* cts, const uint64_t* pts, size_t K, size_t polys,
+                             uint64_t* out);
+int exacto_bfv_inner_product_dev(exacto_ctx* ctx, const uint64_t* cts, const uint64_t* pts, size_t K, size_t polys,
+                                 uint64_t* out);
+int exacto_bfv_monomial_mul(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t j, uint64_t* out,
+                            size_t batch);
+int exacto_bfv_monomial_mul_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t j, uint64_t* out,
+                                size_t batch);
+int exacto_bfv_trace(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* elements, size_t E,
+                     const uint64_t* gks, size_t num_keys, uint64_t* out, size_t batch);
+int exacto_bfv_trace_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* elements, size_t E,
+                         const uint64_t* gks, size_t num_keys, uint64_t* out, size_t batch);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic

@@ -427,6 +427,61 @@ def bfv_apply_automorphism(ct, gk):
     return BfvCiphertext([c0f, c1f], params)
 
 
+def bfv_trace(ct, elements, galois_keys):
+    """eval.rs:572-586: result <- result + sigma_k(result) for each element k, in order."""
+    result = ct.clone()
+    for k in elements:
+        if k not in galois_keys:
+            raise ExactoError.invalid_param(f"missing Galois key for element {k}")
+        rot = bfv_apply_automorphism(result, galois_keys[k])
+        result = bfv_add(result, rot)
+    return result
+
+
+def monomial_mul_poly(poly: CoeffPoly, j: int, n: int) -> CoeffPoly:
+    """eval.rs:634-652."""
+    q = poly.modulus
+    res = [0] * n
+    for i, c in enumerate(poly.coeffs):
+        if c == 0:
+            continue
+        e = (i + j) % (2 * n)
+        if e < n:
+            res[e] = (res[e] + c) % q
+        else:
+            res[e - n] = (res[e - n] - c) % q
+    return CoeffPoly(res, q)
+
+
+def bfv_monomial_mul(ct, j: int):
+    """eval.rs:613-632 (to_coeff_poly under extension semantics for Q >= 2^64)."""
+    params = ct.params
+    basis = params.ct_basis
+    n = params.ring_degree
+    j %= 2 * n
+    if j == 0:
+        return ct.clone()
+    return BfvCiphertext([RnsPoly.from_coeff_poly(monomial_mul_poly(c.to_coeff_poly(basis), j, n), basis)
+                          for c in ct.c], params)
+
+
+def bfv_plain_mul(ct, pt: CoeffPoly):
+    """eval.rs:468-486: every component times the raw plaintext (no Delta)."""
+    ptr = RnsPoly.from_coeff_poly(pt, ct.params.ct_basis)
+    return BfvCiphertext([c.mul(ptr) for c in ct.c], ct.params)
+
+
+def bfv_plain_add(ct, pt: CoeffPoly):
+    """eval.rs:489-503: c0 + Delta m."""
+    params = ct.params
+    basis = params.ct_basis
+    dr = delta_residues(params)
+    dm = RnsPoly.from_limb_coeffs([[(m % q) * d % q for m in pt.coeffs] for q, d in zip(basis.moduli, dr)], basis)
+    c = [x.clone() for x in ct.c]
+    c[0] = c[0].add(dm)
+    return BfvCiphertext(c, params)
+
+
 def galois_s_auto(sk_poly: RnsPoly, k: int, basis) -> RnsPoly:
     """keygen.rs:179-182: limb 0 of s in the coefficient domain (mod q0), permuted, lifted to every limb."""
     s0 = sk_poly.components[0].to_coeff_poly()

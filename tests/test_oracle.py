@@ -306,3 +306,12 @@ def test_apply_automorphism_kat():
     # sigma_k then sigma_k^-1 is the identity (odd k)
     p = CoeffPoly([5, 0, 7, 1, 0, 0, 3, 2], 97)
     assert obfv.apply_automorphism(obfv.apply_automorphism(p, 3), 11).coeffs == p.coeffs  # 3 * 11 = 33 = 1 mod 16
+
+
+def test_monomial_mul_poly_kat():
+    """eval.rs:634-652: X^3 (1 + 2X + 3X^2) in Z_17[X]/(X^4 + 1) = -2 - 3X + X^3; X^(2n) is 1."""
+    from oracle import bfv as obfv
+    from oracle.ring import CoeffPoly
+    assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 3, 4).coeffs == [15, 14, 0, 1]
+    assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 4, 4).coeffs == [16, 15, 14, 0]
+    assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 8, 4).coeffs == [1, 2, 3, 0]
