@@ -107,6 +107,11 @@ _SIGS = [
     ("exacto_bfv_monomial_mul_dev", [_P, _P, _SZ, _U64, _P, _SZ], C.c_int),
     ("exacto_bfv_trace", [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_trace_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_required_trace_elements", [_SZ, _P, _SZ], _SZ),
+    ("exacto_extract_coefficients", [_P, _P, _U64, _SZ, _P, _SZ, _P, _SZ, _P], C.c_int),
+    ("exacto_extract_coefficients_dev", [_P, _P, _U64, _SZ, _P, _SZ, _P, _SZ, _P], C.c_int),
+    ("exacto_slots_to_coeffs", [_P, _P, _SZ, _SZ, _P], C.c_int),
+    ("exacto_slots_to_coeffs_dev", [_P, _P, _SZ, _SZ, _P], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -146,6 +151,15 @@ def last_error() -> str:
 def check(rc: int):
     if rc != 0:
         raise ExactoError(rc, last_error())
+
+
+def required_trace_elements(n: int) -> list[int]:
+    """coeffs_to_slots.rs:168-183 (host-only entry point of the library; no GPU needed)."""
+    lib = load()
+    count = lib.exacto_required_trace_elements(n, None, 0)
+    out = (C.c_uint64 * max(count, 1))()
+    lib.exacto_required_trace_elements(n, out, count)
+    return [int(v) for v in out[:count]]
 
 
 def _ptr(a) -> int | None:
@@ -375,6 +389,44 @@ class HipContext:
         check(self._lib.exacto_bfv_apply_automorphism(self._h, ct.ctypes.data, ct.shape[1], element,
                                                       gk.ctypes.data if gk.size else None, gk.shape[0],
                                                       out.ctypes.data, ct.shape[0]))
+        return out
+
+    def required_trace_elements(self, n=None) -> list[int]:
+        return required_trace_elements(self.n if n is None else n)
+
+    def gen_trace_galois_keys(self, sk, key, stream=0, elements=None, sigma=3.2):
+        """gen_trace_galois_keys / gen_all_galois_keys (coeffs_to_slots.rs:151-197): one key per element,
+        element e on ChaCha stream `stream + e`.  Returns (elements, gks [E][G][2][L][n])."""
+        els = self.required_trace_elements() if elements is None else list(elements)
+        gks = np.stack([self.gen_galois_key(sk, k, key, stream=stream + e, sigma=sigma) for e, k in enumerate(els)])
+        return els, gks
+
+    def extract_coefficients(self, ct, j0, count, elements, gks) -> np.ndarray:
+        """coeffs_to_slots.rs:21-49 for j0 .. j0+count-1: ct [2][L][n] -> [count][2][L][n]."""
+        ct = _u64(ct)
+        el = np.ascontiguousarray(np.asarray(elements, dtype=np.uint64))
+        gks = _u64(gks)
+        E = el.shape[0]
+        out = np.zeros((count, 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_extract_coefficients(self._h, ct.ctypes.data, j0, count, el.ctypes.data if E else None,
+                                                    E, gks.ctypes.data if E else None, gks.shape[1] if E else 0,
+                                                    out.ctypes.data))
+        return out
+
+    def extract_coefficient(self, ct, j, elements, gks) -> np.ndarray:
+        return self.extract_coefficients(ct, j, 1, elements, gks)[0]
+
+    def coeffs_to_slots(self, ct, elements, gks) -> np.ndarray:
+        """coeffs_to_slots.rs:103-115: all n coefficients, the n shifted copies traced together."""
+        return self.extract_coefficients(ct, 0, self.n, elements, gks)
+
+    def slots_to_coeffs(self, slots) -> np.ndarray:
+        """coeffs_to_slots.rs:121-145: slots [S][polys][L][n] -> [polys][L][n]."""
+        slots = _u64(slots)
+        S = slots.shape[0]
+        polys = slots.shape[1] if S else 2
+        out = np.zeros((polys, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_slots_to_coeffs(self._h, slots.ctypes.data, S, polys, out.ctypes.data))
         return out
 
     def _pt(self, pt, rows):

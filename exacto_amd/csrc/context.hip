@@ -1702,8 +1702,9 @@ extern "C" int exacto_bfv_plain_mul_dev(exacto_ctx* c, const uint64_t* ct, size_
     if (polys == 0) return invalid_param("ciphertext has no components");
     if (B == 0) return 0;
     if (int e = lift_plain(c, pt, (long)B, false)) return e;
-    launch_plain_apply(PLAIN_MUL, ct, out, (long)B, (int)polys, c->pl_buf, (long)c->L * c->n, c->n, c->L,
-                       c->d_primes, c->stream);
+    const long Ln = (long)c->L * c->n;
+    launch_plain_apply(PLAIN_MUL, ct, (long)polys * Ln, out, (long)B, (int)polys, c->pl_buf, Ln, c->n, c->L, c->d_primes,
+                       c->stream);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1715,8 +1716,9 @@ extern "C" int exacto_bfv_plain_add_dev(exacto_ctx* c, const uint64_t* ct, size_
     if (polys == 0) return invalid_param("ciphertext has no components");
     if (B == 0) return 0;
     if (int e = lift_plain(c, pt, (long)B, true)) return e;
-    launch_plain_apply(PLAIN_ADD, ct, out, (long)B, (int)polys, c->pl_buf, (long)c->L * c->n, c->n, c->L,
-                       c->d_primes, c->stream);
+    const long Ln = (long)c->L * c->n;
+    launch_plain_apply(PLAIN_ADD, ct, (long)polys * Ln, out, (long)B, (int)polys, c->pl_buf, Ln, c->n, c->L, c->d_primes,
+                       c->stream);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1746,12 +1748,35 @@ extern "C" int exacto_bfv_monomial_mul_dev(exacto_ctx* c, const uint64_t* ct, si
         return 0;
     }
     if (int e = pl_scratch(c, (size_t)Ln)) return e;
-    launch_monomial(c->pl_buf, j, c->n, c->L, c->d_primes, c->stream);
+    launch_monomials(c->pl_buf, 1, j, false, c->n, c->L, c->d_primes, c->stream);
     CHECK_LAUNCH();
     if (int e = ntt_items(c, c->pl_buf, 1, 0, c->L)) return e;
-    launch_plain_apply(PLAIN_MUL, ct, out, (long)B, (int)polys, c->pl_buf, 0, c->n, c->L, c->d_primes, c->stream);
+    launch_plain_apply(PLAIN_MUL, ct, polys * Ln, out, (long)B, (int)polys, c->pl_buf, 0, c->n, c->L, c->d_primes,
+                       c->stream);
     CHECK_LAUNCH();
     return 0;
+}
+
+// Trace accumulation over [B][2][L][n] in r: chain (src == nullptr): r += sigma_k(r) for each k in
+// order (eval.rs:572-586, coeffs_to_slots.rs:65-75); naive: r += sigma_k(src) (coeffs_to_slots.rs:79-95).
+// key e of ks lives at gks + kidx[e] * num_keys * 2Ln.
+static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u64>& ks,
+                      const std::vector<size_t>& kidx, const u64* gks, size_t num_keys, size_t B) {
+    if (ks.empty()) return 0;
+    const long Ln = (long)c->L * c->n;
+    u64* rot = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&rot, B * 2 * Ln * sizeof(u64), c->stream));
+    int rc = 0;
+    for (size_t e = 0; e < ks.size() && rc == 0; ++e) {
+        rc = exacto_bfv_apply_automorphism_dev(c, src ? src : r, 2, ks[e], gks + kidx[e] * num_keys * 2 * Ln,
+                                               num_keys, rot, B);
+        if (rc == 0) {
+            launch_pointwise(PwOp::Add, r, rot, r, (long)B * 2 * c->L, c->n, c->L, nullptr, c->d_primes, c->stream);
+            if (hipGetLastError() != hipSuccess) rc = fail(EXACTO_ERR_HIP, "HIP error: trace add launch");
+        }
+    }
+    HIP_TRY(hipFreeAsync(rot, c->stream));
+    return rc;
 }
 
 // eval.rs:572-586 batched: result = ct; for k in elements: result += sigma_k(result).
@@ -1762,23 +1787,106 @@ extern "C" int exacto_bfv_trace_dev(exacto_ctx* c, const uint64_t* ct, size_t po
     if (!ct || !out || (E && (!elements || !gks))) return invalid_param("null argument");
     if (B == 0) return 0;
     const long Ln = (long)c->L * c->n;
-    const size_t words = B * polys * Ln;
-    if (out != ct) HIP_TRY(hipMemcpyAsync(out, ct, words * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    if (out != ct) HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
     if (E == 0) return 0;
     if (polys != 2) return invalid_param("automorphism requires degree-1 ciphertext");
-    u64* rot = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&rot, words * sizeof(u64), c->stream));
-    int rc = 0;
-    for (size_t e = 0; e < E && rc == 0; ++e) {
-        rc = exacto_bfv_apply_automorphism_dev(c, out, 2, elements[e], gks + e * num_keys * 2 * Ln, num_keys, rot, B);
-        if (rc == 0) {
-            launch_pointwise(PwOp::Add, out, rot, out, (long)B * 2 * c->L, c->n, c->L, nullptr, c->d_primes,
-                             c->stream);
-            if (hipGetLastError() != hipSuccess) rc = EXACTO_ERR_HIP;
-        }
+    std::vector<u64> ks(elements, elements + E);
+    std::vector<size_t> kidx(E);
+    for (size_t e = 0; e < E; ++e) kidx[e] = e;
+    return trace_core(c, nullptr, out, ks, kidx, gks, num_keys, B);
+}
+
+// coeffs_to_slots.rs:168-183
+extern "C" size_t exacto_required_trace_elements(size_t n, uint64_t* out, size_t cap) {
+    std::vector<u64> v;
+    if (n <= 32 || (n & (n - 1))) {
+        for (u64 k = 3; k < 2 * (u64)n; k += 2) v.push_back(k);
+    } else {
+        for (u64 step = n; step >= 2; step >>= 1) v.push_back(step + 1);
     }
-    HIP_TRY(hipFreeAsync(rot, c->stream));
-    return rc;
+    for (size_t i = 0; i < v.size() && i < cap && out; ++i) out[i] = v[i];
+    return v.size();
+}
+
+// coeffs_to_slots.rs:21-49 for the coefficients j0 .. j0+J-1 of one ciphertext at once:
+// out[t] = n^-1 * Tr(X^(2n-j) ct), j = j0 + t; the J shifted copies share every trace step.
+extern "C" int exacto_extract_coefficients_dev(exacto_ctx* c, const uint64_t* ct, uint64_t j0, size_t J,
+                                               const uint64_t* elements, size_t E, const uint64_t* gks,
+                                               size_t num_keys, uint64_t* out) {
+    if (int e = check_ctx(c)) return e;
+    if (!ct || !out || (E && (!elements || !gks))) return invalid_param("null argument");
+    if (J == 0) return 0;
+    const int n = c->n;
+    if (j0 + J - 1 > 2 * (u64)n) return invalid_param("coefficient index out of range");
+    // resolve every key the trace needs first (HashMap lookups, coeffs_to_slots.rs:67-69, 87-89)
+    std::vector<u64> ks(exacto_required_trace_elements(n, nullptr, 0));
+    exacto_required_trace_elements(n, ks.data(), ks.size());
+    std::vector<size_t> kidx(ks.size());
+    for (size_t e = 0; e < ks.size(); ++e) {
+        size_t f = 0;
+        while (f < E && elements[f] != ks[e]) ++f;
+        if (f == E) return invalid_param("missing Galois key for element " + std::to_string(ks[e]));
+        kidx[e] = f;
+    }
+    // n^-1 mod t (coeffs_to_slots.rs:40-42)
+    const u64 n_inv = invmod_h((u64)n % c->plain, c->plain);
+    if (!n_inv) return invalid_param("n not invertible mod t");
+    const long Ln = (long)c->L * n;
+    const bool naive = n <= 32 || (n & (n - 1));
+    // shifted copies X^(2n-j) ct: the monomial table [J][L][n] in the NTT domain, one broadcast product
+    if (int e = pl_scratch(c, J * Ln)) return e;
+    launch_monomials(c->pl_buf, (long)J, j0, true, n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = ntt_items(c, c->pl_buf, (long)J, Ln, c->L)) return e;
+    u64* shifted = out;
+    if (naive) HIP_TRY(hipMallocAsync((void**)&shifted, J * 2 * Ln * sizeof(u64), c->stream));
+    launch_plain_apply(PLAIN_MUL, ct, 0, shifted, (long)J, 2, c->pl_buf, Ln, n, c->L, c->d_primes, c->stream);
+    int rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: monomial launch");
+    if (rc == 0 && naive)
+        rc = hipMemcpyAsync(out, shifted, J * 2 * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream) == hipSuccess
+                 ? 0 : fail(EXACTO_ERR_HIP, "HIP error: copy");
+    if (rc == 0) rc = trace_core(c, naive ? shifted : nullptr, out, ks, kidx, gks, num_keys, J);
+    if (naive) HIP_TRY(hipFreeAsync(shifted, c->stream));
+    if (rc) return rc;
+    // times the constant plaintext n^-1: NTT(constant) is that constant in every slot
+    return exacto_rns_scalar_mul_dev(c, out, n_inv, out, J * 2);
+}
+
+// coeffs_to_slots.rs:121-145: sum_j X^j slots[j], as one inner product against the monomial table
+extern "C" int exacto_slots_to_coeffs_dev(exacto_ctx* c, const uint64_t* slots, size_t S, size_t polys,
+                                          uint64_t* out) {
+    if (int e = check_ctx(c)) return e;
+    if (S == 0) return invalid_param("empty slots");
+    if (S != (size_t)c->n)
+        return invalid_param("expected " + std::to_string(c->n) + " slots, got " + std::to_string(S));
+    if (!slots || !out) return invalid_param("null argument");
+    if (polys == 0) return invalid_param("ciphertext has no components");
+    const long Ln = (long)c->L * c->n;
+    if (int e = pl_scratch(c, S * Ln)) return e;
+    launch_monomials(c->pl_buf, (long)S, 0, false, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    if (int e = ntt_items(c, c->pl_buf, (long)S, Ln, c->L)) return e;
+    launch_inner_product(slots, c->pl_buf, out, (int)S, (int)polys, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int exacto_extract_coefficients(exacto_ctx* c, const uint64_t* ct, uint64_t j0, size_t J,
+                                           const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys,
+                                           uint64_t* out) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = 2 * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}, {gks, E * num_keys * ctb}}, J * ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_extract_coefficients_dev(c, d[0], j0, J, elements, E, d[1], num_keys, o);
+    });
+}
+
+extern "C" int exacto_slots_to_coeffs(exacto_ctx* c, const uint64_t* slots, size_t S, size_t polys, uint64_t* out) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = polys * c->L * poly_bytes(c);
+    return host_call(c, {{slots, S * ctb}}, ctb, out, [&](std::vector<u64*>& d, u64* o) {
+        return exacto_slots_to_coeffs_dev(c, d[0], S, polys, o);
+    });
 }
 
 extern "C" int exacto_bfv_plain_mul(exacto_ctx* c, const uint64_t* ct, size_t polys, const uint64_t* pt,

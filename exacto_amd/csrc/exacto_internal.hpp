@@ -170,9 +170,9 @@ void launch_combine(int op, u64* x, long items, long item_stride, long x1_off, c
 
 // ---- plaintext-ciphertext operations (plain.hip) ----
 enum { PLAIN_MUL = 0, PLAIN_ADD = 1 };
-void launch_plain_apply(int op, const u64* x, u64* out, long items, int polys, const u64* pt, long pt_item_stride,
-                        int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_plain_apply(int op, const u64* x, long x_item_stride, u64* out, long items, int polys, const u64* pt,
+                        long pt_item_stride, int n, int L, const PrimeConst* primes, hipStream_t s);
 void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int polys, int n, int L,
                           const PrimeConst* primes, hipStream_t s);
-void launch_monomial(u64* out, u64 j, int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const PrimeConst* primes, hipStream_t s);
 }  // namespace exacto

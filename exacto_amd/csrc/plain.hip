@@ -15,12 +15,13 @@ namespace exacto {
 
 static constexpr int PL_TPB = 256;
 
-// rows [item][poly][limb][n]; plaintext rows [item (or 0 when pt_item_stride == 0)][limb][n]
+// rows [item][poly][limb][n] (x items x_item_stride apart, 0 = one ciphertext for every item);
+// plaintext rows [item (or 0 when pt_item_stride == 0)][limb][n]
 //   op PLAIN_MUL: out = x * pt      (every poly)
 //   op PLAIN_ADD: out = x + pt on poly 0, x elsewhere
 __global__ void __launch_bounds__(PL_TPB)
-plain_apply_kernel(int op, const u64* __restrict__ x, u64* __restrict__ out, int polys, const u64* __restrict__ pt,
-                   long pt_item_stride, int n, int L, const PrimeConst* __restrict__ primes) {
+plain_apply_kernel(int op, const u64* __restrict__ x, long x_item_stride, u64* __restrict__ out, int polys,
+                   const u64* __restrict__ pt, long pt_item_stride, int n, int L, const PrimeConst* __restrict__ primes) {
     const int nblk = (n + PL_TPB - 1) / PL_TPB;
     const long row = blockIdx.x / nblk;
     const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
@@ -32,7 +33,7 @@ plain_apply_kernel(int op, const u64* __restrict__ x, u64* __restrict__ out, int
     const int poly = (int)(r / L);
     const PrimeConst& P = primes[i];
     const long idx = row * n + j;
-    const u64 v = x[idx];
+    const u64 v = x[item * x_item_stride + r * n + j];
     const u64 m = pt[item * pt_item_stride + (long)i * n + j];
     u64 res;
     if (op == PLAIN_MUL) res = mul_mod(v, m, P);
@@ -40,12 +41,12 @@ plain_apply_kernel(int op, const u64* __restrict__ x, u64* __restrict__ out, int
     out[idx] = res;
 }
 
-void launch_plain_apply(int op, const u64* x, u64* out, long items, int polys, const u64* pt, long pt_item_stride,
-                        int n, int L, const PrimeConst* primes, hipStream_t s) {
+void launch_plain_apply(int op, const u64* x, long x_item_stride, u64* out, long items, int polys, const u64* pt,
+                        long pt_item_stride, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = items * polys * L * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(plain_apply_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, op, x, out, polys, pt,
-                       pt_item_stride, n, L, primes);
+    hipLaunchKernelGGL(plain_apply_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, op, x, x_item_stride, out, polys,
+                       pt, pt_item_stride, n, L, primes);
 }
 
 // out[poly][limb][j] = sum_k cts[k][poly][limb][j] * pts[k][limb][j]  (accumulated in the
@@ -75,22 +76,27 @@ void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int p
                        L, primes);
 }
 
-// X^j mod (X^n + 1) as coefficient rows [limb][n]: +1 at j (j < n) or q_i - 1 at j - n.
+// Monomials X^e mod (X^n + 1) as coefficient rows [J][L][n], item t: e = j mod 2n, or
+// e = (2n - j) mod 2n (X^-j) when neg, with j = j0 + t: +1 at e (e < n) or q_i - 1 at e - n.
 __global__ void __launch_bounds__(PL_TPB)
-monomial_kernel(u64* __restrict__ out, u64 jj, int n, int L, const PrimeConst* __restrict__ primes) {
+monomial_kernel(u64* __restrict__ out, u64 j0, int neg, int n, int L, const PrimeConst* __restrict__ primes) {
     const int nblk = (n + PL_TPB - 1) / PL_TPB;
-    const long row = blockIdx.x / nblk;
+    const long row = blockIdx.x / nblk;  // row = t * L + i
     const int c = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
     if (c >= n) return;
-    const u64 pos = jj < (u64)n ? jj : jj - n;
+    const u64 two_n = 2 * (u64)n;
+    const u64 j = (j0 + (u64)(row / L)) % two_n;
+    const u64 e = neg ? (two_n - j) % two_n : j;
+    const u64 pos = e < (u64)n ? e : e - n;
     u64 v = 0;
-    if ((u64)c == pos) v = jj < (u64)n ? 1 : primes[row].q - 1;
+    if ((u64)c == pos) v = e < (u64)n ? 1 : primes[row % L].q - 1;
     out[row * n + c] = v;
 }
 
-void launch_monomial(u64* out, u64 j, int n, int L, const PrimeConst* primes, hipStream_t s) {
-    const long blocks = (long)L * ((n + PL_TPB - 1) / PL_TPB);
-    hipLaunchKernelGGL(monomial_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, j, n, L, primes);
+void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = J * L * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(monomial_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, j0, (int)neg, n, L, primes);
 }
 
 }  // namespace exacto

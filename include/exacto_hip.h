@@ -279,6 +279,25 @@ int exacto_bfv_trace(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const ui
 int exacto_bfv_trace_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, const uint64_t* elements, size_t E,
                          const uint64_t* gks, size_t num_keys, uint64_t* out, size_t batch);
 
+/* CoeffsToSlots / SlotsToCoeffs (src/bootstrap/coeffs_to_slots.rs).
+ *   exacto_required_trace_elements replaces required_trace_elements (coeffs_to_slots.rs:168-183):
+ *     pure host function, writes up to cap elements and returns how many there are.
+ *   exacto_extract_coefficients replaces extract_coefficient (coeffs_to_slots.rs:21-49) for the J
+ *     indices j0 .. j0+J-1 of one ciphertext ct [2][L][n] -> out [J][2][L][n] (coeffs_to_slots,
+ *     coeffs_to_slots.rs:103-115, is j0 = 0, J = n).  (elements [E] host, gks [E][num_keys][2][L][n])
+ *     is the reference's HashMap<element, GaloisKey>; a required element missing from it is
+ *     InvalidParam "missing Galois key for element k"; n not invertible mod t is InvalidParam.
+ *   exacto_slots_to_coeffs replaces slots_to_coeffs (coeffs_to_slots.rs:121-145): slots
+ *     [S][polys][L][n] -> out [polys][L][n]; S == 0 "empty slots", S != n "expected n slots, got S". */
+size_t exacto_required_trace_elements(size_t n, uint64_t* out, size_t cap);
+int exacto_extract_coefficients(exacto_ctx* ctx, const uint64_t* ct, uint64_t j0, size_t J, const uint64_t* elements,
+                                size_t E, const uint64_t* gks, size_t num_keys, uint64_t* out);
+int exacto_extract_coefficients_dev(exacto_ctx* ctx, const uint64_t* ct, uint64_t j0, size_t J,
+                                    const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys,
+                                    uint64_t* out);
+int exacto_slots_to_coeffs(exacto_ctx* ctx, const uint64_t* slots, size_t S, size_t polys, uint64_t* out);
+int exacto_slots_to_coeffs_dev(exacto_ctx* ctx, const uint64_t* slots, size_t S, size_t polys, uint64_t* out);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic

@@ -52,3 +52,12 @@ def test_no_silent_fallback(monkeypatch, tmp_path):
     monkeypatch.setattr(_ffi, "_lib", None)
     with pytest.raises(RuntimeError):
         _ffi.load()
+
+
+def test_required_trace_elements_host_entry():
+    """coeffs_to_slots.rs:390-396 (the reference's own vectors) and the oracle restatement."""
+    from oracle import bootstrap as ob
+    assert _ffi.required_trace_elements(8) == [3, 5, 7, 9, 11, 13, 15]
+    assert _ffi.required_trace_elements(64) == [65, 33, 17, 9, 5, 3]
+    for n in (16, 32, 48, 64, 1024, 4096, 8192):
+        assert _ffi.required_trace_elements(n) == ob.required_trace_elements(n)
