@@ -112,6 +112,12 @@ _SIGS = [
     ("exacto_extract_coefficients_dev", [_P, _P, _U64, _SZ, _P, _SZ, _P, _SZ, _P], C.c_int),
     ("exacto_slots_to_coeffs", [_P, _P, _SZ, _SZ, _P], C.c_int),
     ("exacto_slots_to_coeffs_dev", [_P, _P, _SZ, _SZ, _P], C.c_int),
+    ("exacto_lagrange_interpolate", [_P, _SZ, _U64, _P], C.c_int),
+    ("exacto_compute_rounding_poly", [_U64, _U64, _U64, _P], C.c_int),
+    ("exacto_trivial_encrypt", [_P, _P, _P, _SZ], C.c_int),
+    ("exacto_trivial_encrypt_dev", [_P, _P, _P, _SZ], C.c_int),
+    ("exacto_eval_poly", [_P, _P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_eval_poly_dev", [_P, _P, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -151,6 +157,21 @@ def last_error() -> str:
 def check(rc: int):
     if rc != 0:
         raise ExactoError(rc, last_error())
+
+
+def lagrange_interpolate(values, p: int) -> list[int]:
+    """digit_extract.rs:37-90 (host-only entry point)."""
+    v = np.ascontiguousarray(np.asarray(values, dtype=np.uint64))
+    out = np.zeros(max(v.size, 1), dtype=np.uint64)
+    check(load().exacto_lagrange_interpolate(v.ctypes.data, v.size, p, out.ctypes.data))
+    return [int(x) for x in out[:v.size]]
+
+
+def compute_rounding_poly(t_orig: int, q_prime: int, t_boot: int) -> list[int]:
+    """digit_extract.rs:19-30 (host-only entry point)."""
+    out = np.zeros(max(t_boot, 1), dtype=np.uint64)
+    check(load().exacto_compute_rounding_poly(t_orig, q_prime, t_boot, out.ctypes.data))
+    return [int(x) for x in out[:t_boot]]
 
 
 def required_trace_elements(n: int) -> list[int]:
@@ -200,6 +221,7 @@ class HipContext:
         self.path = info.mul_path
         self.num_internal_aux = info.num_internal_aux
         self.ct_moduli = [int(q) for q in ct_moduli]
+        self.plain_modulus = int(info.plain_modulus)
 
     @classmethod
     def from_params(cls, params, device=0):
@@ -427,6 +449,30 @@ class HipContext:
         polys = slots.shape[1] if S else 2
         out = np.zeros((polys, self.L, self.n), dtype=np.uint64)
         check(self._lib.exacto_slots_to_coeffs(self._h, slots.ctypes.data, S, polys, out.ctypes.data))
+        return out
+
+    def trivial_encrypt_poly(self, pt) -> np.ndarray:
+        """digit_extract.rs:179-189 batched: pt [B][n] -> (Delta m, 0) [B][2][L][n]."""
+        pt = _u64(pt)
+        pt = pt.reshape(-1, self.n)
+        out = np.zeros((pt.shape[0], 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_trivial_encrypt(self._h, pt.ctypes.data, out.ctypes.data, pt.shape[0]))
+        return out
+
+    def trivial_encrypt(self, values) -> np.ndarray:
+        """digit_extract.rs:160-176 for each scalar m of `values`: (Delta (m mod t), 0)."""
+        vals = [int(v) for v in np.atleast_1d(values)]
+        pt = np.zeros((len(vals), self.n), dtype=np.uint64)
+        pt[:, 0] = [v % self.plain_modulus for v in vals]
+        return self.trivial_encrypt_poly(pt)
+
+    def eval_poly(self, ct, coeffs) -> np.ndarray:
+        """digit_extract.rs:101-157 on a batch ct [B][2][L][n]; needs the resident relin key."""
+        ct = _u64(ct)
+        cf = np.ascontiguousarray(np.asarray(coeffs, dtype=np.uint64))
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_eval_poly(self._h, ct.ctypes.data, cf.ctypes.data if cf.size else None, cf.size,
+                                         out.ctypes.data, ct.shape[0]))
         return out
 
     def _pt(self, pt, rows):

@@ -1936,6 +1936,162 @@ extern "C" int exacto_bfv_trace(exacto_ctx* c, const uint64_t* ct, size_t polys,
                      });
 }
 
+// ---- digit extraction pieces (bootstrap/digit_extract.rs) ----
+
+// lagrange_interpolate (digit_extract.rs:37-90): the Lagrange formula at the points 0..n-1 over Z_p.
+// The numerator prod_{k != j} (x - k) is the master polynomial prod_k (x - k) divided by the monic
+// (x - j) -- exact over Z, so reducing mod p commutes -- which makes it O(n^2) instead of O(n^3)
+// with the same coefficients; the denominators prod_{k != j} (j - k) are the reference's.
+extern "C" int exacto_lagrange_interpolate(const uint64_t* values, size_t n, uint64_t p, uint64_t* out) {
+    if (n == 0) return 0;
+    if (!values || !out) return invalid_param("null argument");
+    if (p == 0) return invalid_param("modulus must be nonzero");
+    if (n == 1) { out[0] = values[0] % p; return 0; }
+    auto mulm = [p](u64 a, u64 b) { return (u64)((u128)a * b % p); };
+    auto addm = [p](u64 a, u64 b) { return (u64)(((u128)a + b) % p); };
+    // master[d], degree n: prod_{k=0}^{n-1} (x - k)
+    std::vector<u64> master(n + 1, 0), num(n), res(n, 0);
+    master[0] = 1 % p;
+    for (size_t k = 0; k < n; ++k) {
+        const u64 neg_k = (p - (u64)k % p) % p;
+        for (size_t d = k + 2; d-- > 0;) {  // d = k+1 .. 0
+            const u64 lower = d ? master[d - 1] : 0;
+            master[d] = addm(lower, mulm(master[d], neg_k));
+        }
+    }
+    for (size_t j = 0; j < n; ++j) {
+        if (values[j] % p == 0) continue;
+        // synthetic division of master by (x - j): num[n-1] = master[n], num[d-1] = master[d] + j num[d]
+        const u64 jm = (u64)j % p;
+        num[n - 1] = master[n];
+        for (size_t d = n - 1; d >= 1; --d) num[d - 1] = addm(master[d], mulm(jm, num[d]));
+        u64 denom = 1 % p;
+        for (size_t k = 0; k < n; ++k) {
+            if (k == j) continue;
+            const u64 diff = j >= k ? (u64)(j - k) % p : (p - (u64)(k - j) % p) % p;
+            denom = mulm(denom, diff);
+        }
+        const u64 dinv = invmod_h(denom, p);
+        if (!dinv) return invalid_param("points must be distinct mod p");
+        const u64 scale = mulm(values[j] % p, dinv);
+        for (size_t d = 0; d < n; ++d) res[d] = addm(res[d], mulm(num[d], scale));
+    }
+    std::copy(res.begin(), res.end(), out);
+    return 0;
+}
+
+// compute_rounding_poly (digit_extract.rs:19-30): g(x) = round(t_orig (x mod q') / q') mod t_orig
+// on x in [0, t_boot), interpolated over Z_{t_boot}; out has t_boot coefficients.
+extern "C" int exacto_compute_rounding_poly(uint64_t t_orig, uint64_t q_prime, uint64_t t_boot, uint64_t* out) {
+    if (!out) return invalid_param("null argument");
+    if (q_prime == 0 || t_orig == 0) return invalid_param("moduli must be nonzero");
+    std::vector<u64> v(t_boot);
+    for (u64 x = 0; x < t_boot; ++x) {
+        const u128 reduced = x % q_prime;
+        v[x] = (u64)(((u128)t_orig * reduced + q_prime / 2) / q_prime % t_orig);
+    }
+    return exacto_lagrange_interpolate(v.data(), t_boot, t_boot, out);
+}
+
+// trivial_encrypt_poly (digit_extract.rs:179-189): (Delta m, 0), m = pt [B][n] as given
+extern "C" int exacto_trivial_encrypt_dev(exacto_ctx* c, const uint64_t* pt, uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!pt || !out) return invalid_param("null argument");
+    if (B == 0) return 0;
+    const long Ln = (long)c->L * c->n;
+    if (int e = lift_plain(c, pt, (long)B, true)) return e;
+    HIP_TRY(hipMemcpy2DAsync(out, 2 * Ln * sizeof(u64), c->pl_buf, Ln * sizeof(u64), Ln * sizeof(u64), B,
+                             hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemset2DAsync(out + Ln, 2 * Ln * sizeof(u64), 0, Ln * sizeof(u64), B, c->stream));
+    return 0;
+}
+
+// eval_poly_homomorphic (digit_extract.rs:101-157), batched: the same polynomial on B ciphertexts.
+// Paterson-Stockmeyer with the reference's schedule: baby steps x^i = x^(i/2) * x^(i - i/2) for
+// i = 2..k, k = max(2, ceil(sqrt(d + 1))); groups g_i = sum_j a_{ik+j} x^j (trivial(0) + scalar
+// multiples, coefficients reduced mod t as bfv_scalar_mul does); Horner in x^k.  Uses the context's
+// resident relinearisation key for every bfv_mul_and_relin.
+extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uint64_t* coeffs, size_t m,
+                                    uint64_t* out, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (m == 0) return invalid_param("empty polynomial");
+    if (!ct || !out || !coeffs) return invalid_param("null argument");
+    if (B == 0) return 0;
+    if (int e = delta_residues(c)) return e;
+    const long Ln = (long)c->L * c->n;
+    const size_t words = B * 2 * Ln;
+    const size_t d = m - 1;
+    const u64 t = c->plain;
+    if (d == 0) {  // digit_extract.rs:109-111: trivial_encrypt(a_0)
+        launch_trivial_const(out, (long)B, coeffs[0] % t, c->d_delta, c->n, c->L, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+        return 0;
+    }
+    if (!c->rlk_loaded) return fail(EXACTO_ERR_MISSING_KEY, "key not available: relinearization key not loaded");
+    const size_t k = std::max<size_t>(2, (size_t)std::ceil(std::sqrt((double)d + 1.0)));
+    const size_t groups = (d + k) / k;
+    // workspace: baby[0], baby[2..k] (baby[1] is ct), one group accumulator, a Horner ping buffer
+    const size_t nbuf = k + 3;
+    u64* ws = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&ws, nbuf * words * sizeof(u64), c->stream));
+    std::vector<const u64*> baby(k + 1);
+    auto slot = [&](size_t i) { return ws + i * words; };
+    baby[0] = slot(0);
+    baby[1] = ct;
+    u64* acc = slot(k + 1);
+    u64* ping = slot(k + 2);
+    int rc = 0;
+    launch_trivial_const(slot(0), (long)B, 1 % t, c->d_delta, c->n, c->L, c->d_primes, c->stream);
+    if (hipGetLastError() != hipSuccess) rc = fail(EXACTO_ERR_HIP, "HIP error: trivial launch");
+    for (size_t i = 2; i <= k && rc == 0; ++i) {
+        const size_t half = i / 2;
+        rc = exacto_bfv_mul_and_relin_dev(c, baby[half], baby[i - half], slot(i), B);
+        baby[i] = slot(i);
+    }
+    // group g_i into `dst`: trivial(0) + sum_j (a mod t) x^j
+    auto group = [&](size_t gi, u64* dst) -> int {
+        HIP_TRY(hipMemsetAsync(dst, 0, words * sizeof(u64), c->stream));
+        for (size_t j = 0; j < k; ++j) {
+            const size_t idx = gi * k + j;
+            if (idx >= m) break;
+            if (coeffs[idx] == 0) continue;
+            launch_axpy(dst, baby[j], coeffs[idx] % t, (long)B * 2 * c->L, c->n, c->L, c->d_primes, c->stream);
+            CHECK_LAUNCH();
+        }
+        return 0;
+    };
+    // Horner from the last group; the running result alternates between out and ping
+    u64* res = ((groups - 1) % 2 == 0) ? out : ping;  // so that the final result lands in out
+    u64* other = res == out ? ping : out;
+    if (rc == 0) rc = group(groups - 1, res);
+    for (size_t gi = groups - 1; gi-- > 0 && rc == 0;) {
+        rc = exacto_bfv_mul_and_relin_dev(c, res, baby[k], other, B);
+        if (rc == 0) rc = group(gi, acc);
+        if (rc == 0) {
+            launch_pointwise(PwOp::Add, other, acc, other, (long)B * 2 * c->L, c->n, c->L, nullptr, c->d_primes,
+                             c->stream);
+            if (hipGetLastError() != hipSuccess) rc = fail(EXACTO_ERR_HIP, "HIP error: add launch");
+        }
+        std::swap(res, other);
+    }
+    HIP_TRY(hipFreeAsync(ws, c->stream));
+    return rc;
+}
+
+extern "C" int exacto_trivial_encrypt(exacto_ctx* c, const uint64_t* pt, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    return host_call(c, {{pt, B * poly_bytes(c)}}, B * 2 * c->L * poly_bytes(c), out,
+                     [&](std::vector<u64*>& d, u64* o) { return exacto_trivial_encrypt_dev(c, d[0], o, B); });
+}
+
+extern "C" int exacto_eval_poly(exacto_ctx* c, const uint64_t* ct, const uint64_t* coeffs, size_t m, uint64_t* out,
+                                size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{ct, ctb}}, ctb, out,
+                     [&](std::vector<u64*>& d, u64* o) { return exacto_eval_poly_dev(c, d[0], coeffs, m, o, B); });
+}
+
 // Host-pointer variants (synchronous); `key` is always a host pointer to 4 words.
 extern "C" int exacto_gen_secret_key(exacto_ctx* c, const uint64_t* key, uint64_t stream, uint64_t* sk) {
     if (!c) return invalid_param("null context");

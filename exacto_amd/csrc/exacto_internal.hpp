@@ -175,4 +175,7 @@ void launch_plain_apply(int op, const u64* x, long x_item_stride, u64* out, long
 void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int polys, int n, int L,
                           const PrimeConst* primes, hipStream_t s);
 void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_axpy(u64* out, const u64* x, u64 a, long rows, int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, int L, const PrimeConst* primes,
+                          hipStream_t s);
 }  // namespace exacto

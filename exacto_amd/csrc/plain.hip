@@ -100,3 +100,49 @@ void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const Pr
 }
 
 }  // namespace exacto
+
+namespace exacto {
+
+// out[row] += (a mod q_i) * x[row] over contiguous rows [rows][n], limb = row % L
+// (bfv_scalar_mul + bfv_add, digit_extract.rs:131-140, 191-196)
+__global__ void __launch_bounds__(PL_TPB)
+axpy_kernel(u64* __restrict__ out, const u64* __restrict__ x, u64 a, int n, int L,
+            const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;
+    const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (j >= n) return;
+    const PrimeConst& P = primes[row % L];
+    const long idx = row * n + j;
+    out[idx] = add_mod(out[idx], mul_mod(x[idx], reduce64(a, P.q, P.mu64), P), P.q);
+}
+
+void launch_axpy(u64* out, const u64* x, u64 a, long rows, int n, int L, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = rows * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(axpy_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, x, a, n, L, primes);
+}
+
+// trivial encryptions of the constant m (digit_extract.rs:160-176): (Delta m, 0) per item, where the
+// NTT of the constant polynomial Delta_i m is that constant in every slot.  out [items][2][L][n].
+__global__ void __launch_bounds__(PL_TPB)
+trivial_const_kernel(u64* __restrict__ out, u64 m, const u64* __restrict__ delta, int n, int L,
+                     const PrimeConst* __restrict__ primes) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;  // row = (item * 2 + poly) * L + limb
+    const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (j >= n) return;
+    const int i = (int)(row % L);
+    const int poly = (int)((row / L) % 2);
+    const PrimeConst& P = primes[i];
+    out[row * n + j] = poly == 0 ? mul_mod(reduce64(m, P.q, P.mu64), delta[i], P) : 0;
+}
+
+void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, int L, const PrimeConst* primes,
+                          hipStream_t s) {
+    const long blocks = items * 2 * L * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(trivial_const_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, m, delta, n, L, primes);
+}
+
+}  // namespace exacto

@@ -298,6 +298,25 @@ int exacto_extract_coefficients_dev(exacto_ctx* ctx, const uint64_t* ct, uint64_
 int exacto_slots_to_coeffs(exacto_ctx* ctx, const uint64_t* slots, size_t S, size_t polys, uint64_t* out);
 int exacto_slots_to_coeffs_dev(exacto_ctx* ctx, const uint64_t* slots, size_t S, size_t polys, uint64_t* out);
 
+/* Digit extraction (src/bootstrap/digit_extract.rs).
+ *   exacto_lagrange_interpolate replaces lagrange_interpolate (digit_extract.rs:37-90): host only,
+ *     out [n]; a zero denominator (points not distinct mod p) is InvalidParam (the reference panics).
+ *   exacto_compute_rounding_poly replaces compute_rounding_poly (digit_extract.rs:19-30): host only,
+ *     out [t_boot].
+ *   exacto_trivial_encrypt replaces trivial_encrypt_poly (digit_extract.rs:179-189): pt [B][n] ->
+ *     (Delta m, 0) [B][2][L][n]; trivial_encrypt(m) is pt = (m mod t, 0, ..., 0).
+ *   exacto_eval_poly replaces eval_poly_homomorphic (digit_extract.rs:101-157) on B ciphertexts at
+ *     once with the reference's Paterson-Stockmeyer schedule; coeffs is a HOST array [m], m >= 1;
+ *     the relinearisation key is the context's resident one (MissingKey if none). */
+int exacto_lagrange_interpolate(const uint64_t* values, size_t n, uint64_t p, uint64_t* out);
+int exacto_compute_rounding_poly(uint64_t t_orig, uint64_t q_prime, uint64_t t_boot, uint64_t* out);
+int exacto_trivial_encrypt(exacto_ctx* ctx, const uint64_t* pt, uint64_t* out, size_t batch);
+int exacto_trivial_encrypt_dev(exacto_ctx* ctx, const uint64_t* pt, uint64_t* out, size_t batch);
+int exacto_eval_poly(exacto_ctx* ctx, const uint64_t* ct, const uint64_t* coeffs, size_t m, uint64_t* out,
+                     size_t batch);
+int exacto_eval_poly_dev(exacto_ctx* ctx, const uint64_t* ct, const uint64_t* coeffs, size_t m, uint64_t* out,
+                         size_t batch);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic

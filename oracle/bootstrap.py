@@ -77,3 +77,107 @@ def slots_to_coeffs(slots: list[BfvCiphertext]) -> BfvCiphertext:
     for j in range(1, n):
         result = bfv_add(result, bfv_monomial_mul(slots[j], j))
     return result
+
+
+# ---- digit extraction (bootstrap/digit_extract.rs) ----
+
+def lagrange_interpolate(values: list[int], p: int) -> list[int]:
+    """digit_extract.rs:37-90, literally (O(n^3)); small n only."""
+    n = len(values)
+    if n == 0:
+        return []
+    if n == 1:
+        return [values[0] % p]
+    result = [0] * n
+    for j in range(n):
+        if values[j] % p == 0:
+            continue
+        num, deg = [0] * n, 0
+        num[0] = 1
+        for k in range(n):
+            if k == j:
+                continue
+            neg_k = (-(k % p)) % p
+            new = [0] * n
+            for d in range(deg + 1):
+                if d + 1 < n:
+                    new[d + 1] = (new[d + 1] + num[d]) % p
+                new[d] = (new[d] + num[d] * neg_k) % p
+            num, deg = new, deg + 1
+        denom = 1
+        for k in range(n):
+            if k != j:
+                denom = denom * ((j - k) % p) % p
+        inv = mod_inv(denom, p)
+        if inv is None:
+            raise ExactoError.invalid_param("points must be distinct mod p")
+        scale = values[j] % p * inv % p
+        for d in range(n):
+            result[d] = (result[d] + num[d] * scale) % p
+    return result
+
+
+def rounding_values(t_orig: int, q_prime: int, t_boot: int) -> list[int]:
+    """digit_extract.rs:20-27."""
+    return [(t_orig * (x % q_prime) + q_prime // 2) // q_prime % t_orig for x in range(t_boot)]
+
+
+def compute_rounding_poly(t_orig: int, q_prime: int, t_boot: int) -> list[int]:
+    """digit_extract.rs:19-30."""
+    return lagrange_interpolate(rounding_values(t_orig, q_prime, t_boot), t_boot)
+
+
+def trivial_encrypt_poly(pt: CoeffPoly, params) -> BfvCiphertext:
+    """digit_extract.rs:179-189: (Delta m, 0)."""
+    from .bfv import delta_residues
+    from .ring import RnsPoly
+    basis = params.ct_basis
+    dr = delta_residues(params)
+    c0 = RnsPoly.from_limb_coeffs([[(m % q) * d % q for m in pt.coeffs] for q, d in zip(basis.moduli, dr)], basis)
+    c1 = RnsPoly.from_limb_coeffs([[0] * params.ring_degree for _ in basis.moduli], basis)
+    return BfvCiphertext([c0, c1], params)
+
+
+def trivial_encrypt(m: int, params) -> BfvCiphertext:
+    """digit_extract.rs:160-176."""
+    coeffs = [0] * params.ring_degree
+    coeffs[0] = m % params.plain_modulus
+    return trivial_encrypt_poly(CoeffPoly(coeffs, params.plain_modulus), params)
+
+
+def bfv_scalar_mul(ct: BfvCiphertext, scalar: int) -> BfvCiphertext:
+    """digit_extract.rs:192-197."""
+    params = ct.params
+    coeffs = [0] * params.ring_degree
+    coeffs[0] = scalar % params.plain_modulus
+    return bfv_plain_mul(ct, CoeffPoly(coeffs, params.plain_modulus))
+
+
+def eval_poly_homomorphic(ct_x: BfvCiphertext, coeffs: list[int], rlk) -> BfvCiphertext:
+    """digit_extract.rs:101-157 (Paterson-Stockmeyer with the reference's schedule)."""
+    import math
+    from .bfv import bfv_mul_and_relin
+    params = ct_x.params
+    d = max(len(coeffs) - 1, 0)
+    if d == 0:
+        return trivial_encrypt(coeffs[0], params)
+    k = max(math.ceil(math.sqrt(d + 1.0)), 2)
+    baby = [trivial_encrypt(1, params), ct_x.clone()]
+    for i in range(2, k + 1):
+        half = i // 2
+        baby.append(bfv_mul_and_relin(baby[half], baby[i - half], rlk))
+    groups = []
+    for gi in range((d + k) // k):
+        g = trivial_encrypt(0, params)
+        for j in range(k):
+            idx = gi * k + j
+            if idx >= len(coeffs):
+                break
+            if coeffs[idx] == 0:
+                continue
+            g = bfv_add(g, bfv_scalar_mul(baby[j], coeffs[idx]))
+        groups.append(g)
+    result = groups.pop()
+    while groups:
+        result = bfv_add(bfv_mul_and_relin(result, baby[k], rlk), groups.pop())
+    return result

@@ -61,3 +61,27 @@ def test_required_trace_elements_host_entry():
     assert _ffi.required_trace_elements(64) == [65, 33, 17, 9, 5, 3]
     for n in (16, 32, 48, 64, 1024, 4096, 8192):
         assert _ffi.required_trace_elements(n) == ob.required_trace_elements(n)
+
+
+def test_digit_extract_host_entries():
+    """digit_extract.rs:204-267 (the reference's Lagrange / rounding-polynomial tests) and the
+    literal O(n^3) oracle restatement."""
+    from oracle import bootstrap as ob
+    assert _ffi.lagrange_interpolate([0, 1, 2], 7) == [0, 1, 0]
+    assert _ffi.lagrange_interpolate([0, 1, 4, 2], 7) == [0, 0, 1, 0]
+    vals = [(i * i + 3 * i + 7) % 29 for i in range(10)]
+    coeffs = _ffi.lagrange_interpolate(vals, 29)
+    for x, want in enumerate(vals):
+        assert sum(c * pow(x, k, 29) for k, c in enumerate(coeffs)) % 29 == want
+    assert coeffs == ob.lagrange_interpolate(vals, 29)
+    for t, qp, tb in ((5, 25, 29), (16, 64, 257), (3, 10, 11)):
+        poly = _ffi.compute_rounding_poly(t, qp, tb)
+        assert poly == ob.compute_rounding_poly(t, qp, tb)
+        for x in range(tb):
+            want = (t * (x % qp) + qp // 2) // qp % t
+            assert sum(c * pow(x, k, tb) for k, c in enumerate(poly)) % tb % t == want
+    assert _ffi.lagrange_interpolate([], 7) == []
+    assert _ffi.lagrange_interpolate([9], 7) == [2]
+    with pytest.raises(_ffi.ExactoError) as e:
+        _ffi.lagrange_interpolate(list(range(9)), 7)  # 9 points mod 7 are not distinct
+    assert e.value.variant == "InvalidParam" and "points must be distinct mod p" in str(e.value)
