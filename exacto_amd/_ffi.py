@@ -118,6 +118,10 @@ _SIGS = [
     ("exacto_trivial_encrypt_dev", [_P, _P, _P, _SZ], C.c_int),
     ("exacto_eval_poly", [_P, _P, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_eval_poly_dev", [_P, _P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bootstrap_key_material", [_P, _P, _P, _P, _P], C.c_int),
+    ("exacto_bootstrap_key_material_dev", [_P, _P, _P, _P, _P], C.c_int),
+    ("exacto_bfv_bootstrap", [_P, _P, _P, _SZ, _P, _P, _SZ, _U64, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_bootstrap_dev", [_P, _P, _P, _SZ, _P, _P, _SZ, _U64, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -172,6 +176,30 @@ def compute_rounding_poly(t_orig: int, q_prime: int, t_boot: int) -> list[int]:
     out = np.zeros(max(t_boot, 1), dtype=np.uint64)
     check(load().exacto_compute_rounding_poly(t_orig, q_prime, t_boot, out.ctypes.data))
     return [int(x) for x in out[:t_boot]]
+
+
+def bootstrap_key_material(orig: "HipContext", boot: "HipContext", sk):
+    """bfv_host.rs:57-100, 289-330: (boot_sk [Lb][n] NTT domain, s_pt [n]) from sk [1][n]."""
+    sk = _u64(sk)
+    boot_sk = np.zeros((boot.L, boot.n), dtype=np.uint64)
+    s_pt = np.zeros(boot.n, dtype=np.uint64)
+    check(load().exacto_bootstrap_key_material(orig._h, boot._h, sk.ctypes.data, boot_sk.ctypes.data,
+                                               s_pt.ctypes.data))
+    return boot_sk, s_pt
+
+
+def bfv_bootstrap_raw(orig: "HipContext", boot: "HipContext", ct, bsk, rpoly, q_prime, elements, gks):
+    """bfv_host.rs:131-205 batched: ct [B][2][1][n] (orig) -> [B][2][Lb][n] (boot)."""
+    ct, bsk, gks = _u64(ct), _u64(bsk), _u64(gks)
+    rp = np.ascontiguousarray(np.asarray(rpoly, dtype=np.uint64))
+    el = np.ascontiguousarray(np.asarray(elements, dtype=np.uint64))
+    E = el.shape[0]
+    out = np.zeros((ct.shape[0], 2, boot.L, boot.n), dtype=np.uint64)
+    check(load().exacto_bfv_bootstrap(orig._h, boot._h, ct.ctypes.data, ct.shape[1], bsk.ctypes.data,
+                                      rp.ctypes.data, rp.size, q_prime, el.ctypes.data if E else None, E,
+                                      gks.ctypes.data if E else None, gks.shape[1] if E else 0, out.ctypes.data,
+                                      ct.shape[0]))
+    return out
 
 
 def required_trace_elements(n: int) -> list[int]:

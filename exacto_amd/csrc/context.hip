@@ -2078,6 +2078,157 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
     return rc;
 }
 
+// ---- bootstrap composition (bootstrap/bfv_host.rs) ----
+
+static int boot_pair_check(exacto_ctx* o, exacto_ctx* b) {
+    if (int e = check_ctx(o)) return e;
+    if (int e = check_ctx(b)) return e;
+    if (o->n != b->n) return invalid_param("boot params must have same ring degree");
+    if (o->device != b->device) return invalid_param("both contexts must be on one device");
+    // the reference switches from q = moduli[0] after to_coeff_poly, which only holds one residue
+    // system when L = 1 (bfv_host.rs:149-157): multi-prime originals are not supported
+    if (o->L != 1) return invalid_param("bootstrap requires a single-prime ciphertext modulus");
+    return 0;
+}
+
+// gen_bootstrap_key's key material (bfv_host.rs:57-100, 289-330): the boot scheme's secret key
+// boot_sk [Lb][n] (NTT domain, create_boot_sk) and the plaintext s_pt [n] that bsk encrypts.
+extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, const uint64_t* sk, uint64_t* boot_sk,
+                                                 uint64_t* s_pt) {
+    if (int e = boot_pair_check(o, b)) return e;
+    if (!sk || !boot_sk || !s_pt) return invalid_param("null argument");
+    const int n = o->n;
+    u64* tmp = nullptr;
+    HIP_TRY(hipMalloc((void**)&tmp, 2 * n * sizeof(u64)));
+    HIP_TRY(hipMemcpyAsync(tmp, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream));
+    int rc = run_ntt(o, contiguous(tmp, 1, 1, 0, 1, n), 1, true);  // sk.poly.components[0].to_coeff_poly()
+    if (rc == 0) {
+        launch_boot_key_map(tmp, tmp + n, s_pt, n, o->primes[0], b->primes[0], b->plain, o->stream);
+        rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: key map launch");
+    }
+    if (rc == 0) rc = hipStreamSynchronize(o->stream) == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: sync");
+    if (rc == 0) {  // RnsPoly::from_coeff_poly over the boot basis, then its NTT
+        launch_scale_plain(tmp + n, nullptr, boot_sk, 1, n, b->L, b->d_primes, b->stream);
+        rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: lift launch");
+    }
+    if (rc == 0) rc = ntt_items(b, boot_sk, 1, 0, b->L);
+    if (rc == 0) rc = hipStreamSynchronize(b->stream) == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: sync");
+    HIP_TRY(hipFree(tmp));
+    return rc;
+}
+
+// bfv_bootstrap (bfv_host.rs:131-205) on B ciphertexts of the original scheme (ct [B][2][1][n] on
+// o) -> out [B][2][Lb][n] on b.  bsk [2][Lb][n] is the encryption of s under b; the boot
+// relinearisation key must be resident in b; (elements, gks) are the trace keys as in
+// exacto_extract_coefficients; rpoly [m] (host) the rounding polynomial.  Items whose c1 is zero
+// take the reference's trivial fast path, the others the full ring path.
+extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint64_t* ct, size_t polys,
+                                        const uint64_t* bsk, const uint64_t* rpoly, size_t m, uint64_t q_prime,
+                                        const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys,
+                                        uint64_t* out, size_t B) {
+    if (int e = boot_pair_check(o, b)) return e;
+    if (polys != 2) return invalid_param("bootstrap requires degree-1 ciphertext");
+    if (!ct || !bsk || !out || !rpoly) return invalid_param("null argument");
+    if (q_prime == 0) return invalid_param("q_prime must be nonzero");
+    if (B == 0) return 0;
+    const int n = o->n;
+    const long Lbn = (long)b->L * n;
+    // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
+    u64* coef = nullptr;
+    int* flags = nullptr;
+    HIP_TRY(hipMalloc((void**)&coef, 2 * B * 2 * n * sizeof(u64)));
+    HIP_TRY(hipMalloc((void**)&flags, B * sizeof(int)));
+    u64* small = coef + B * 2 * n;
+    int rc = 0;
+    auto ok = [&](hipError_t e, const char* what) {
+        if (rc == 0 && e != hipSuccess) rc = fail(EXACTO_ERR_HIP, std::string("HIP error: ") + what);
+    };
+    ok(hipMemcpyAsync(coef, ct, B * 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream), "copy");
+    ok(hipMemsetAsync(flags, 0, B * sizeof(int), o->stream), "memset");
+    if (rc == 0) rc = exacto_rns_inv_dev(o, coef, B * 2);
+    if (rc == 0) {
+        launch_modswitch(coef, small, flags, (long)B, n, o->primes[0], q_prime, b->plain, o->stream);
+        ok(hipGetLastError(), "modswitch launch");
+    }
+    std::vector<int> hflags(B);
+    if (rc == 0) ok(hipMemcpyAsync(hflags.data(), flags, B * sizeof(int), hipMemcpyDeviceToHost, o->stream), "flags");
+    if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
+    // 2. phase = TrivialEnc(c0') + bsk * c1' (b), written into out
+    u64* c0pt = nullptr;  // [B][n] copies of c0' and c1' rows in the plaintext layout
+    if (rc == 0) ok(hipMalloc((void**)&c0pt, 2 * B * n * sizeof(u64)), "alloc");
+    u64* c1pt = c0pt + B * n;
+    if (rc == 0) ok(hipMemcpy2DAsync(c0pt, n * sizeof(u64), small, 2 * n * sizeof(u64), n * sizeof(u64), B,
+                                     hipMemcpyDeviceToDevice, b->stream), "copy c0");
+    if (rc == 0) ok(hipMemcpy2DAsync(c1pt, n * sizeof(u64), small + n, 2 * n * sizeof(u64), n * sizeof(u64), B,
+                                     hipMemcpyDeviceToDevice, b->stream), "copy c1");
+    if (rc == 0) rc = lift_plain(b, c1pt, (long)B, false);
+    if (rc == 0) {
+        launch_plain_apply(PLAIN_MUL, bsk, 0, out, (long)B, 2, b->pl_buf, Lbn, n, b->L, b->d_primes, b->stream);
+        ok(hipGetLastError(), "plain_mul launch");
+    }
+    if (rc == 0) rc = lift_plain(b, c0pt, (long)B, true);
+    if (rc == 0) {
+        launch_plain_apply(PLAIN_ADD, out, 2 * Lbn, out, (long)B, 2, b->pl_buf, Lbn, n, b->L, b->d_primes,
+                           b->stream);
+        ok(hipGetLastError(), "plain_add launch");
+    }
+    // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
+    u64 *slots = nullptr, *rounded = nullptr, *phase = nullptr;
+    const size_t ctw = 2 * Lbn;
+    if (rc == 0) ok(hipMalloc((void**)&phase, ctw * sizeof(u64)), "alloc");
+    for (size_t i = 0; i < B && rc == 0; ++i) {
+        u64* oi = out + i * ctw;
+        ok(hipMemcpyAsync(phase, oi, ctw * sizeof(u64), hipMemcpyDeviceToDevice, b->stream), "copy");
+        if (rc) break;
+        if (!hflags[i]) {  // bfv_host.rs:180-186
+            rc = exacto_eval_poly_dev(b, phase, rpoly, m, oi, 1);
+            continue;
+        }
+        if (!slots) {
+            ok(hipMalloc((void**)&slots, 2 * (size_t)n * ctw * sizeof(u64)), "alloc");
+            rounded = slots + (size_t)n * ctw;
+            if (rc) break;
+        }
+        rc = exacto_extract_coefficients_dev(b, phase, 0, n, elements, E, gks, num_keys, slots);
+        if (rc == 0) rc = exacto_eval_poly_dev(b, slots, rpoly, m, rounded, n);
+        if (rc == 0) rc = exacto_slots_to_coeffs_dev(b, rounded, n, 2, oi);
+    }
+    hipStreamSynchronize(b->stream);
+    hipFree(slots); hipFree(phase); hipFree(c0pt); hipFree(coef); hipFree(flags);
+    return rc;
+}
+
+extern "C" int exacto_bootstrap_key_material(exacto_ctx* o, exacto_ctx* b, const uint64_t* sk, uint64_t* boot_sk,
+                                             uint64_t* s_pt) {
+    if (!o || !b) return invalid_param("null context");
+    if (int e = boot_pair_check(o, b)) return e;
+    const size_t n = o->n;
+    u64* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, (n + b->L * n + n) * sizeof(u64)));
+    int rc = hipMemcpy(d, sk, n * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess ? 0 : EXACTO_ERR_HIP;
+    if (rc == 0) rc = exacto_bootstrap_key_material_dev(o, b, d, d + n, d + n + b->L * n);
+    if (rc == 0 && (hipMemcpy(boot_sk, d + n, b->L * n * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess ||
+                    hipMemcpy(s_pt, d + n + b->L * n, n * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = fail(EXACTO_ERR_HIP, "HIP error: copy back");
+    hipFree(d);
+    return rc;
+}
+
+extern "C" int exacto_bfv_bootstrap(exacto_ctx* o, exacto_ctx* b, const uint64_t* ct, size_t polys,
+                                    const uint64_t* bsk, const uint64_t* rpoly, size_t m, uint64_t q_prime,
+                                    const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys,
+                                    uint64_t* out, size_t B) {
+    if (!o || !b) return invalid_param("null context");
+    if (int e = boot_pair_check(o, b)) return e;
+    if (polys != 2) return invalid_param("bootstrap requires degree-1 ciphertext");
+    const size_t ctb = 2 * b->L * poly_bytes(b);
+    return host_call(b, {{ct, B * 2 * o->L * poly_bytes(o)}, {bsk, ctb}, {gks, E * num_keys * ctb}}, B * ctb, out,
+                     [&](std::vector<u64*>& d, u64* dout) {
+                         return exacto_bfv_bootstrap_dev(o, b, d[0], polys, d[1], rpoly, m, q_prime, elements, E,
+                                                         d[2], num_keys, dout, B);
+                     });
+}
+
 extern "C" int exacto_trivial_encrypt(exacto_ctx* c, const uint64_t* pt, uint64_t* out, size_t B) {
     if (!c) return invalid_param("null context");
     return host_call(c, {{pt, B * poly_bytes(c)}}, B * 2 * c->L * poly_bytes(c), out,

@@ -176,6 +176,8 @@ void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int p
                           const PrimeConst* primes, hipStream_t s);
 void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const PrimeConst* primes, hipStream_t s);
 void launch_axpy(u64* out, const u64* x, u64 a, long rows, int n, int L, const PrimeConst* primes, hipStream_t s);
+void launch_modswitch(const u64* coef, u64* out, int* flags, long items, int n, u64 q, u64 qp, u64 tb, hipStream_t s);
+void launch_boot_key_map(const u64* s, u64* boot_coef, u64* s_pt, int n, u64 q, u64 qb, u64 tb, hipStream_t st);
 void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, int L, const PrimeConst* primes,
                           hipStream_t s);
 }  // namespace exacto

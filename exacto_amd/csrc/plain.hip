@@ -146,3 +146,57 @@ void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, 
 }
 
 }  // namespace exacto
+
+namespace exacto {
+
+// bfv_host.rs:149-170: modulus switch of coefficient rows [items][2][n] (mod q) to
+// ((q' c + q/2) / q) mod q' mod t_boot; flags[item] = 1 when c1 has a nonzero coefficient (the
+// reference's is_trivial test, bfv_host.rs:180).
+__global__ void __launch_bounds__(PL_TPB)
+modswitch_kernel(const u64* __restrict__ coef, u64* __restrict__ out, int* __restrict__ flags, int n, u64 q, u64 qp,
+                 u64 tb) {
+    const int nblk = (n + PL_TPB - 1) / PL_TPB;
+    const long row = blockIdx.x / nblk;  // row = item * 2 + poly
+    const int j = (blockIdx.x - row * nblk) * PL_TPB + threadIdx.x;
+    if (j >= n) return;
+    const u64 c = coef[row * n + j];
+    const u64 v = (u64)(((u128)qp * c + q / 2) / q);
+    out[row * n + j] = v % qp % tb;
+    if ((row & 1) && c != 0) atomicOr(&flags[row >> 1], 1);
+}
+
+void launch_modswitch(const u64* coef, u64* out, int* flags, long items, int n, u64 q, u64 qp, u64 tb, hipStream_t s) {
+    const long blocks = items * 2 * ((n + PL_TPB - 1) / PL_TPB);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(modswitch_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, coef, out, flags, n, q, qp, tb);
+}
+
+// gen_bootstrap_key's two images of the ternary secret s (coefficients mod q_orig):
+//   boot_coef: create_boot_sk's map into Z_{q_boot}    (bfv_host.rs:296-315)
+//   s_pt     : the plaintext encrypted as the key      (bfv_host.rs:68-86)
+__global__ void __launch_bounds__(PL_TPB)
+boot_key_map_kernel(const u64* __restrict__ s, u64* __restrict__ boot_coef, u64* __restrict__ s_pt, int n, u64 q,
+                    u64 qb, u64 tb) {
+    const int i = blockIdx.x * PL_TPB + threadIdx.x;
+    if (i >= n) return;
+    const u64 c = s[i];
+    u64 b;
+    if (c == 0) b = 0;
+    else if (c <= q / 2) b = c % qb;
+    else b = qb - (q - c) % qb;
+    boot_coef[i] = b;
+    u64 p;
+    if (c == 0) p = 0;
+    else if (c == 1) p = 1;
+    else if (c == q - 1) p = tb - 1;
+    else if (c > q / 2) p = tb - (q - c) % tb;
+    else p = c % tb;
+    s_pt[i] = p;
+}
+
+void launch_boot_key_map(const u64* s, u64* boot_coef, u64* s_pt, int n, u64 q, u64 qb, u64 tb, hipStream_t st) {
+    hipLaunchKernelGGL(boot_key_map_kernel, dim3((unsigned)((n + PL_TPB - 1) / PL_TPB)), dim3(PL_TPB), 0, st, s,
+                       boot_coef, s_pt, n, q, qb, tb);
+}
+
+}  // namespace exacto

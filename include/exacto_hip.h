@@ -317,6 +317,30 @@ int exacto_eval_poly(exacto_ctx* ctx, const uint64_t* ct, const uint64_t* coeffs
 int exacto_eval_poly_dev(exacto_ctx* ctx, const uint64_t* ct, const uint64_t* coeffs, size_t m, uint64_t* out,
                          size_t batch);
 
+/* Bootstrapping (src/bootstrap/bfv_host.rs), over two contexts on one device: `orig` (the scheme
+ * being refreshed; ONE ciphertext prime, because the reference switches from moduli[0] after
+ * to_coeff_poly, bfv_host.rs:149-157) and `boot` (same n).
+ *   exacto_bootstrap_key_material replaces the key-material half of gen_bootstrap_key and
+ *     create_boot_sk (bfv_host.rs:57-100, 289-330): sk [1][n] (NTT) -> boot_sk [Lb][n] (NTT) and the
+ *     plaintext s_pt [n] that bsk encrypts.  bsk, boot_rlk and the trace keys are then made with
+ *     exacto_encrypt_sk / exacto_gen_relin_key / exacto_gen_galois_key on `boot`.
+ *   exacto_bfv_bootstrap replaces bfv_bootstrap (bfv_host.rs:131-205) for B ciphertexts:
+ *     ct [B][2][1][n] -> out [B][2][Lb][n]; bsk [2][Lb][n]; rpoly [m] HOST (compute_rounding_poly);
+ *     (elements [E] HOST, gks [E][num_keys][2][Lb][n]) the trace keys; boot's resident relin key is
+ *     boot_rlk.  Items with c1 = 0 take the trivial path (bfv_host.rs:180-186), the rest the full
+ *     ring path (CoeffsToSlots -> rounding polynomial on the n slots at once -> SlotsToCoeffs). */
+int exacto_bootstrap_key_material(exacto_ctx* orig, exacto_ctx* boot, const uint64_t* sk, uint64_t* boot_sk,
+                                  uint64_t* s_pt);
+int exacto_bootstrap_key_material_dev(exacto_ctx* orig, exacto_ctx* boot, const uint64_t* sk, uint64_t* boot_sk,
+                                      uint64_t* s_pt);
+int exacto_bfv_bootstrap(exacto_ctx* orig, exacto_ctx* boot, const uint64_t* ct, size_t polys, const uint64_t* bsk,
+                         const uint64_t* rpoly, size_t m, uint64_t q_prime, const uint64_t* elements, size_t E,
+                         const uint64_t* gks, size_t num_keys, uint64_t* out, size_t batch);
+int exacto_bfv_bootstrap_dev(exacto_ctx* orig, exacto_ctx* boot, const uint64_t* ct, size_t polys,
+                             const uint64_t* bsk, const uint64_t* rpoly, size_t m, uint64_t q_prime,
+                             const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys, uint64_t* out,
+                             size_t batch);
+
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
  * (kind 0 = forward NTT, 1 = inverse NTT): launches, summed device ms, summed algorithmic

