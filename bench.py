@@ -231,14 +231,15 @@ def main():
         "polys_per_step": dom["polys"],
         "ntt_share_of_step": round((fwd["ms"] + inv["ms"]) / ms_per_step, 3),
     }
-    # HBM bytes per launch from the committed PMC pass over this same bench configuration
-    # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch, gfx950 corrections), as
-    # its measured traffic/algorithmic ratio applied to this run's algorithmic bytes per launch
+    # HBM bytes per launch from the committed PMC passes over this same bench configuration
+    # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch, gfx950 corrections, averaged
+    # over every forward-NTT dispatch: the same launch mix per step as the timed one)
     tfile = os.path.join(ROOT, "profiles", f"r1_{args.config}_fwd_traffic.json")
     if dom_name.startswith("ntt_fwd") and os.path.exists(tfile):
         with open(tfile) as f:
             tr = json.load(f)
-        roofline["traffic"] = round(tr["traffic_over_algorithmic"] * roofline["bytes_per_launch"], 1)
+        roofline["traffic"] = round(tr["traffic_bytes_avg"], 1)
+        roofline["traffic_over_algorithmic"] = round(tr["traffic_bytes_avg"] / roofline["bytes_per_launch"], 4)
         roofline["traffic_source"] = os.path.relpath(tfile, ROOT)
 
     cpu = None
@@ -247,7 +248,8 @@ def main():
         # whole machine), one product per thread; the single-thread figure rides along
         threads = min(16, os.cpu_count() or 1)
         try:
-            cpu = cpu_baseline(n, moduli, plain, gbase, args.cpu_sample or threads, threads)
+            # about 10-15 s of CPU work: 8 products per thread
+            cpu = cpu_baseline(n, moduli, plain, gbase, args.cpu_sample or 8 * threads, threads)
             one = cpu_baseline(n, moduli, plain, gbase, 2, 1)
             cpu["single_thread"] = {"value": one["value"], "sample": one["sample"]}
         except Exception as e:  # the baseline is informative; never fail the bench on it

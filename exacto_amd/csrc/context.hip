@@ -626,7 +626,9 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
         HIP_TRY(hipEventRecord(rec.b, c->stream));
         rec.kind = inverse ? 1 : 0;
         rec.polys = (u64)count;
-        rec.bytes = 16.0 * c->n * (double)count;
+        // algorithmic bytes: one read of the source (int16 digits: 2 B per coefficient) + one
+        // 8 B write per coefficient
+        rec.bytes = ((nb.src16 ? 2.0 : 8.0) + 8.0) * c->n * (double)count;
         c->recs.push_back(rec);
     }
     return 0;

@@ -5,7 +5,8 @@ gfx950 corrections (MI355X_MICROARCH.md, HBM section, and our own calibration on
 count: tools/ntt_bench.py over 16384 polys reads exactly 16384 * 8n bytes): FETCH_SIZE is in KiB
 and counts half of the bytes of these coalesced streaming reads, so read bytes = 2 * FETCH_SIZE;
 WRITE_SIZE (KiB) is exact.  Output: averages over every ntt_fwd_kernel dispatch of the run, and
-the ratio to the algorithmic bytes (16 n per transformed polynomial) of the same dispatches.
+bench.py divides by its own algorithmic bytes per launch (8 n written per polynomial, 8 n read, or
+2 n for the int16 digit sources) over the same launch mix.
 """
 import csv
 import glob
@@ -31,19 +32,13 @@ def per_dispatch(path, counter):
 out = sys.argv[1]
 fetch = per_dispatch(os.path.join(out, "fetch"), "FETCH_SIZE")
 write = per_dispatch(os.path.join(out, "write"), "WRITE_SIZE")
-n = 4096
 rd = [2 * 1024 * v[0] for v in fetch.values()]
 wr = [1024 * v[0] for v in write.values()]
-# polys per dispatch = grid / workgroup (one polynomial per workgroup)
-polys = [v[1] // max(v[2], 1) for v in fetch.values()]
-alg = [16.0 * n * p for p in polys]
 res = {
-    "kernel": "ntt_fwd_asm_kernel<12> (hand-scheduled forward NTT)",
+    "kernel": "ntt_fwd_asm_kernel (hand-scheduled forward NTT)",
     "dispatches": len(rd),
     "read_bytes_avg": sum(rd) / len(rd),
     "write_bytes_avg": sum(wr) / len(wr),
     "traffic_bytes_avg": sum(rd) / len(rd) + sum(wr) / len(wr),
-    "algorithmic_bytes_avg": sum(alg) / len(alg),
 }
-res["traffic_over_algorithmic"] = res["traffic_bytes_avg"] / res["algorithmic_bytes_avg"]
 print(json.dumps(res, indent=1))
