@@ -5,12 +5,16 @@
 //   exacto::bfv::eval::{bfv_mul_and_relin, bfv_mul_no_relin, bfv_add, bfv_sub, bfv_neg}
 //   exacto::bfv::keyswitch::relinearize
 //   exacto::dbfv::{DbfvCiphertext, eval::dbfv_mul}
+//   exacto::bfv::keygen / encrypt (device samplers), eval::{bfv_plain_mul, bfv_plain_add,
+//     bfv_inner_product, bfv_monomial_mul, bfv_trace, bfv_apply_automorphism}
+//   exacto::bootstrap::{coeffs_to_slots, digit_extract, bfv_host}  (src/bootstrap/*.rs)
 // Errors: Rust's Result<T, ExactoError> becomes a thrown exacto::ExactoError carrying the
 // variant (src/error.rs:4-31) and the reference's Display text.
 // Ciphertexts are host-resident here (one H2D/D2H per call); the batched overloads amortise it.
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -390,6 +394,228 @@ inline CoeffPoly encode_scalar(uint64_t m, const BfvParamsPtr& prm) {
     return p;
 }
 inline uint64_t decode_scalar(const CoeffPoly& p) { return p.coeffs.empty() ? 0 : p.coeffs[0]; }
+
+// ---- plaintext operations and the trace (src/bfv/eval.rs:468-652)
+namespace detail {
+inline std::vector<uint64_t> flatten_pts(const std::vector<CoeffPoly>& pts, size_t n) {
+    std::vector<uint64_t> out;
+    for (auto& p : pts) {
+        if (p.coeffs.size() != n) throw ExactoError(2, "dimension mismatch: expected " + std::to_string(n) +
+                                                           ", got " + std::to_string(p.coeffs.size()));
+        out.insert(out.end(), p.coeffs.begin(), p.coeffs.end());
+    }
+    return out;
+}
+inline BfvCiphertext one_ct(const std::vector<uint64_t>& flat, size_t polys, const BfvParamsPtr& prm) {
+    return unflatten(flat, 1, polys, prm)[0];
+}
+}  // namespace detail
+
+inline BfvCiphertext bfv_plain_mul(const BfvCiphertext& ct, const CoeffPoly& pt) {
+    const BfvParams& prm = *ct.params;
+    auto flat = detail::flatten({ct}, ct.c.size());
+    auto p = detail::flatten_pts({pt}, prm.ring_degree);
+    std::vector<uint64_t> out(flat.size());
+    detail::check(exacto_bfv_plain_mul(prm.ctx(), flat.data(), ct.c.size(), p.data(), out.data(), 1));
+    return detail::one_ct(out, ct.c.size(), ct.params);
+}
+inline BfvCiphertext bfv_plain_add(const BfvCiphertext& ct, const CoeffPoly& pt) {
+    const BfvParams& prm = *ct.params;
+    auto flat = detail::flatten({ct}, ct.c.size());
+    auto p = detail::flatten_pts({pt}, prm.ring_degree);
+    std::vector<uint64_t> out(flat.size());
+    detail::check(exacto_bfv_plain_add(prm.ctx(), flat.data(), ct.c.size(), p.data(), out.data(), 1));
+    return detail::one_ct(out, ct.c.size(), ct.params);
+}
+inline BfvCiphertext bfv_monomial_mul(const BfvCiphertext& ct, size_t j) {
+    const BfvParams& prm = *ct.params;
+    auto flat = detail::flatten({ct}, ct.c.size());
+    std::vector<uint64_t> out(flat.size());
+    detail::check(exacto_bfv_monomial_mul(prm.ctx(), flat.data(), ct.c.size(), j, out.data(), 1));
+    return detail::one_ct(out, ct.c.size(), ct.params);
+}
+inline BfvCiphertext bfv_inner_product(const std::vector<BfvCiphertext>& cts, const std::vector<CoeffPoly>& pts) {
+    if (cts.empty() || cts.size() != pts.size()) throw ExactoError(1, "invalid parameter: mismatched ct/pt lengths");
+    const BfvParams& prm = *cts[0].params;
+    const size_t polys = cts[0].c.size();
+    auto flat = detail::flatten(cts, polys);
+    auto p = detail::flatten_pts(pts, prm.ring_degree);
+    std::vector<uint64_t> out(polys * prm.num_limbs() * prm.ring_degree);
+    detail::check(exacto_bfv_inner_product(prm.ctx(), flat.data(), p.data(), cts.size(), polys, out.data()));
+    return detail::one_ct(out, polys, cts[0].params);
+}
+
+// HashMap<usize, GaloisKey> of the reference
+using GaloisKeys = std::map<size_t, GaloisKey>;
+namespace detail {
+// the map as (elements, keys stacked in that order); every key must carry the same digit count
+inline size_t pack_keys(const GaloisKeys& keys, std::vector<uint64_t>& els, std::vector<uint64_t>& flat) {
+    size_t nk = 0;
+    for (auto& kv : keys) {
+        if (nk == 0) nk = kv.second.keys.size();
+        if (kv.second.keys.size() != nk) throw ExactoError(1, "invalid parameter: Galois keys differ in digit count");
+        els.push_back(kv.first);
+        for (auto& k : kv.second.keys) {
+            flat.insert(flat.end(), k.first.data.begin(), k.first.data.end());
+            flat.insert(flat.end(), k.second.data.begin(), k.second.data.end());
+        }
+    }
+    return nk;
+}
+}  // namespace detail
+
+// bfv_trace (eval.rs:572-586)
+inline BfvCiphertext bfv_trace(const BfvCiphertext& ct, const std::vector<size_t>& elements, const GaloisKeys& keys) {
+    const BfvParams& prm = *ct.params;
+    std::vector<uint64_t> els, flat;
+    size_t nk = 0;
+    for (size_t k : elements) {
+        auto it = keys.find(k);
+        if (it == keys.end()) throw ExactoError(1, "invalid parameter: missing Galois key for element " + std::to_string(k));
+        if (nk == 0) nk = it->second.keys.size();
+        els.push_back(k);
+        for (auto& kp : it->second.keys) {
+            flat.insert(flat.end(), kp.first.data.begin(), kp.first.data.end());
+            flat.insert(flat.end(), kp.second.data.begin(), kp.second.data.end());
+        }
+    }
+    auto c = detail::flatten({ct}, ct.c.size());
+    std::vector<uint64_t> out(c.size());
+    detail::check(exacto_bfv_trace(prm.ctx(), c.data(), ct.c.size(), els.data(), els.size(),
+                                   flat.empty() ? nullptr : flat.data(), nk, out.data(), 1));
+    return detail::one_ct(out, ct.c.size(), ct.params);
+}
+
+// ---- exacto::bootstrap::coeffs_to_slots (src/bootstrap/coeffs_to_slots.rs)
+inline std::vector<size_t> required_trace_elements(size_t n) {
+    std::vector<uint64_t> v(exacto_required_trace_elements(n, nullptr, 0));
+    exacto_required_trace_elements(n, v.data(), v.size());
+    return std::vector<size_t>(v.begin(), v.end());
+}
+inline GaloisKeys gen_trace_galois_keys(const SecretKey& sk, ChaChaRng& rng) {
+    GaloisKeys keys;
+    for (size_t k : required_trace_elements(sk.params->ring_degree)) keys[k] = gen_galois_key_with_rng(sk, k, rng);
+    return keys;
+}
+inline GaloisKeys gen_all_galois_keys(const SecretKey& sk, ChaChaRng& rng) {
+    GaloisKeys keys;
+    for (size_t k = 3; k < 2 * sk.params->ring_degree; k += 2) keys[k] = gen_galois_key_with_rng(sk, k, rng);
+    return keys;
+}
+namespace detail {
+inline std::vector<BfvCiphertext> extract_range(const BfvCiphertext& ct, size_t j0, size_t count,
+                                                const GaloisKeys& keys) {
+    const BfvParams& prm = *ct.params;
+    if (ct.c.size() != 2) throw ExactoError(1, "invalid parameter: automorphism requires degree-1 ciphertext");
+    std::vector<uint64_t> els, flat;
+    const size_t nk = pack_keys(keys, els, flat);
+    auto c = flatten({ct}, 2);
+    std::vector<uint64_t> out(count * c.size());
+    check(exacto_extract_coefficients(prm.ctx(), c.data(), j0, count, els.data(), els.size(),
+                                      flat.empty() ? nullptr : flat.data(), nk, out.data()));
+    return unflatten(out, count, 2, ct.params);
+}
+}  // namespace detail
+inline BfvCiphertext extract_coefficient(const BfvCiphertext& ct, size_t j, const GaloisKeys& keys) {
+    return detail::extract_range(ct, j, 1, keys)[0];
+}
+inline std::vector<BfvCiphertext> coeffs_to_slots(const BfvCiphertext& ct, const GaloisKeys& keys) {
+    return detail::extract_range(ct, 0, ct.params->ring_degree, keys);
+}
+inline BfvCiphertext slots_to_coeffs(const std::vector<BfvCiphertext>& slots) {
+    if (slots.empty()) throw ExactoError(1, "invalid parameter: empty slots");
+    const BfvParams& prm = *slots[0].params;
+    const size_t polys = slots[0].c.size();
+    auto flat = detail::flatten(slots, polys);
+    std::vector<uint64_t> out(polys * prm.num_limbs() * prm.ring_degree);
+    detail::check(exacto_slots_to_coeffs(prm.ctx(), flat.data(), slots.size(), polys, out.data()));
+    return detail::one_ct(out, polys, slots[0].params);
+}
+
+// ---- exacto::bootstrap::digit_extract (src/bootstrap/digit_extract.rs)
+inline std::vector<uint64_t> lagrange_interpolate(const std::vector<uint64_t>& values, uint64_t p) {
+    std::vector<uint64_t> out(values.size());
+    if (!values.empty()) detail::check(exacto_lagrange_interpolate(values.data(), values.size(), p, out.data()));
+    return out;
+}
+inline std::vector<uint64_t> compute_rounding_poly(uint64_t t_orig, uint64_t q_prime, uint64_t t_boot) {
+    std::vector<uint64_t> out(t_boot);
+    detail::check(exacto_compute_rounding_poly(t_orig, q_prime, t_boot, out.data()));
+    return out;
+}
+inline BfvCiphertext trivial_encrypt_poly(const CoeffPoly& pt, const BfvParamsPtr& prm) {
+    auto p = detail::flatten_pts({pt}, prm->ring_degree);
+    std::vector<uint64_t> out(2 * prm->num_limbs() * prm->ring_degree);
+    detail::check(exacto_trivial_encrypt(prm->ctx(), p.data(), out.data(), 1));
+    return detail::one_ct(out, 2, prm);
+}
+inline BfvCiphertext trivial_encrypt(uint64_t m, const BfvParamsPtr& prm) {
+    CoeffPoly p;
+    p.coeffs.assign(prm->ring_degree, 0);
+    p.coeffs[0] = m % prm->plain_modulus;
+    p.modulus = prm->plain_modulus;
+    return trivial_encrypt_poly(p, prm);
+}
+inline BfvCiphertext eval_poly_homomorphic(const BfvCiphertext& ct, const std::vector<uint64_t>& coeffs,
+                                           const RelinKey& rlk) {
+    const BfvParams& prm = *ct.params;
+    if (coeffs.size() > 1) detail::load_key(rlk);
+    auto c = detail::flatten({ct}, 2);
+    std::vector<uint64_t> out(c.size());
+    detail::check(exacto_eval_poly(prm.ctx(), c.data(), coeffs.data(), coeffs.size(), out.data(), 1));
+    return detail::one_ct(out, 2, ct.params);
+}
+
+// ---- exacto::bootstrap::bfv_host (src/bootstrap/bfv_host.rs)
+struct BootstrapKey {
+    BfvCiphertext bsk;
+    BfvParamsPtr boot_params;
+    RelinKey boot_rlk;
+    GaloisKeys galois_keys;
+    std::vector<uint64_t> rounding_poly;
+    uint64_t t_orig = 0, q_prime = 0;
+    SecretKey boot_sk;  // create_boot_sk's key (the reference recomputes it in its tests)
+};
+
+inline BootstrapKey gen_bootstrap_key(const SecretKey& sk, const BfvParamsPtr& boot_params, uint64_t q_prime,
+                                      uint64_t t_orig, ChaChaRng& rng) {
+    const BfvParams& o = *sk.params;
+    const size_t n = o.ring_degree;
+    std::vector<uint64_t> boot_sk(boot_params->num_limbs() * n), s_pt(n);
+    detail::check(exacto_bootstrap_key_material(o.ctx(), boot_params->ctx(), sk.poly.data.data(), boot_sk.data(),
+                                                s_pt.data()));
+    BootstrapKey k;
+    k.boot_params = boot_params;
+    k.boot_sk = SecretKey{detail::make_poly(*boot_params, boot_sk.data()), boot_params};
+    CoeffPoly spt{s_pt, boot_params->plain_modulus};
+    k.bsk = encrypt_sk_with_rng(spt, k.boot_sk, boot_params, rng);
+    k.boot_rlk = gen_relin_key_with_rng(k.boot_sk, rng);
+    k.galois_keys = gen_trace_galois_keys(k.boot_sk, rng);
+    k.rounding_poly = compute_rounding_poly(t_orig, q_prime, boot_params->plain_modulus);
+    k.t_orig = t_orig;
+    k.q_prime = q_prime;
+    return k;
+}
+
+inline std::vector<BfvCiphertext> bfv_bootstrap(const std::vector<BfvCiphertext>& cts, const BootstrapKey& bsk) {
+    if (cts.empty()) return {};
+    const BfvParams& o = *cts[0].params;
+    const BfvParams& b = *bsk.boot_params;
+    if (cts[0].c.size() != 2) throw ExactoError(1, "invalid parameter: bootstrap requires degree-1 ciphertext");
+    detail::load_key(bsk.boot_rlk);
+    auto flat = detail::flatten(cts, 2);
+    auto key = detail::flatten({bsk.bsk}, 2);
+    std::vector<uint64_t> els, gks;
+    const size_t nk = detail::pack_keys(bsk.galois_keys, els, gks);
+    std::vector<uint64_t> out(cts.size() * 2 * b.num_limbs() * b.ring_degree);
+    detail::check(exacto_bfv_bootstrap(o.ctx(), b.ctx(), flat.data(), 2, key.data(), bsk.rounding_poly.data(),
+                                       bsk.rounding_poly.size(), bsk.q_prime, els.data(), els.size(),
+                                       gks.empty() ? nullptr : gks.data(), nk, out.data(), cts.size()));
+    return detail::unflatten(out, cts.size(), 2, bsk.boot_params);
+}
+inline BfvCiphertext bfv_bootstrap(const BfvCiphertext& ct, const BootstrapKey& bsk) {
+    return bfv_bootstrap(std::vector<BfvCiphertext>{ct}, bsk)[0];
+}
 
 // ---- exacto::dbfv
 struct DbfvParams {

@@ -198,6 +198,45 @@ static int keygen_case() {
     return 0;
 }
 
+// coeffs_to_slots.rs:221-318, digit_extract.rs:270-288, eval.rs:978-994, bfv_host.rs:430-476
+// through the C++ mirror of the bootstrap API
+static int bootstrap_case() {
+    auto small = BfvParamsBuilder().ring_degree(16).plain_modulus(97).ct_moduli({1125899906842817ull}).sigma(3.2)
+                     .gadget_base(8).build();
+    ChaChaRng rng(42);
+    auto sk = gen_secret_key_with_rng(small, rng);
+    auto keys = gen_all_galois_keys(sk, rng);
+    CoeffPoly m;
+    m.modulus = 97;
+    for (uint64_t i = 1; i <= 16; ++i) m.coeffs.push_back(i % 97);
+    auto ct = encrypt_sk_with_rng(m, sk, small, rng);
+    auto slots = coeffs_to_slots(ct, keys);
+    for (size_t j = 0; j < 16; ++j)
+        if (decode_scalar(decrypt(slots[j], sk)) != m.coeffs[j]) return 30;
+    auto back = decrypt(slots_to_coeffs(slots), sk);
+    if (back.coeffs != m.coeffs) return 31;
+    if (decode_scalar(decrypt(extract_coefficient(ct, 2, keys), sk)) != 3) return 32;
+    if (required_trace_elements(64) != std::vector<size_t>{65, 33, 17, 9, 5, 3}) return 33;
+    auto compact = BfvParamsBuilder().ring_degree(1024).plain_modulus(257).ct_moduli({1099509805057ull})
+                       .aux_moduli({562949953443841ull}).sigma(3.2).build();
+    auto skc = gen_secret_key_with_rng(compact, rng);
+    for (uint64_t v : {0ull, 1ull, 42ull, 100ull, 256ull})
+        if (decode_scalar(decrypt(trivial_encrypt(v, compact), skc)) != v) return 34;
+    auto c10 = encrypt_sk_with_rng(encode_scalar(10, compact), skc, compact, rng);
+    if (decode_scalar(decrypt(bfv_plain_add(c10, encode_scalar(5, compact)), skc)) != 15) return 35;
+    if (decode_scalar(decrypt(bfv_plain_mul(c10, encode_scalar(7, compact)), skc)) != 70) return 36;
+    // bfv_host.rs:430-476: trivial ciphertexts of m = 0..4 refreshed into the boot scheme
+    auto orig = BfvParamsBuilder().ring_degree(16).plain_modulus(5).ct_moduli({65537ull}).sigma(3.2).build();
+    auto boot = BfvParamsBuilder().ring_degree(16).plain_modulus(29).ct_moduli({1125899906842817ull}).sigma(3.2)
+                    .gadget_base(8).build();
+    auto sko = gen_secret_key_with_rng(orig, rng);
+    auto bsk = gen_bootstrap_key(sko, boot, 25, 5, rng);
+    for (uint64_t v = 0; v < 5; ++v)
+        if (decode_scalar(decrypt(bfv_bootstrap(trivial_encrypt(v, orig), bsk), bsk.boot_sk)) % 5 != v) return 37;
+    if (lagrange_interpolate({0, 1, 4, 2}, 7) != std::vector<uint64_t>{0, 0, 1, 0}) return 38;
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <fixture-dir> <case>...\n", argv[0]);
@@ -226,6 +265,14 @@ int main(int argc, char** argv) {
         k = 99;
     }
     std::printf("%s keygen (%d)\n", k ? "FAIL" : "PASS", k);
+    bad |= k != 0;
+    try {
+        k = bootstrap_case();
+    } catch (const std::exception& ex) {
+        std::printf("ERROR bootstrap: %s\n", ex.what());
+        k = 99;
+    }
+    std::printf("%s bootstrap (%d)\n", k ? "FAIL" : "PASS", k);
     bad |= k != 0;
     if (!bad) std::printf("ALL OK\n");
     return bad;
