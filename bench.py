@@ -47,8 +47,11 @@ CONFIGS = {
     "cfg3": (4096, Q3, [], 65537, 1 << 16, None, 0),                      # bfv_mul_and_relin
     "cfg4": (4096, Q3, [], 260111, 1 << 16, (2, 256, 65536), 1),          # dbfv_mul
     "cfg5": (8192, Q4, [], 1040407, 256, (8, 256, 0), 4),                 # dbfv_mul chain depth 4
+    # SURVEY 8(f) rank 4 (widened row, not a BASELINE config): Galois key switching
+    # bfv_apply_automorphism (eval.rs:512-561) on cfg3's parameters, element 5
+    "galois": (4096, Q3, [], 65537, 1 << 16, None, 0),
 }
-DEFAULT_BATCH = {"cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8}
+DEFAULT_BATCH = {"cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8, "galois": 1024}
 
 
 def parse():
@@ -153,7 +156,17 @@ def main():
             dist.broadcast(rlk, src=0)
         torch.cuda.synchronize(device)
         ctx.load_relin_key_dev(rlk, G)
-        if dbfv is None:
+        if args.config == "galois":
+            ct1 = uniform_dev((B, 2), moduli, n, gen, device)
+            gk = uniform_dev((G, 2), moduli, n, kgen, device)
+            out = torch.empty_like(ct1)
+
+            def step():
+                ctx.bfv_apply_automorphism_dev(ct1, 5, gk, G, out, B)
+            units_per_step = B
+            unit = "bfv_apply_automorphism/s"
+            metric = "Galois automorphisms/sec (bfv_apply_automorphism, key switched)"
+        elif dbfv is None:
             ct1 = uniform_dev((B, 2), moduli, n, gen, device)
             ct2 = uniform_dev((B, 2), moduli, n, gen, device)
             out = torch.empty_like(ct1)
@@ -259,7 +272,9 @@ def main():
         workload = {"cfg2": "batched fwd NTT + pointwise mul + inv NTT, BASELINE configs[1]",
                     "cfg3": "bfv_mul_and_relin, BASELINE configs[2]",
                     "cfg4": "dbfv_mul d=2 b=256 p=2^16, BASELINE configs[3]",
-                    "cfg5": "dbfv_mul chain depth 4, d=8 b=256 p=2^64, BASELINE configs[4]"}[args.config]
+                    "cfg5": "dbfv_mul chain depth 4, d=8 b=256 p=2^64, BASELINE configs[4]",
+                    "galois": "bfv_apply_automorphism (element 5, key switched) on cfg3 parameters, "
+                              "SURVEY 8(f) rank 4"}[args.config]
         line = {
             "metric": metric,
             "value": round(value, 1),

@@ -617,6 +617,10 @@ class HipContext:
         check(self._lib.exacto_bfv_mul_and_relin_dev(self._h, self._p(ct1), self._p(ct2),
                                                      self._p(out), batch))
 
+    def bfv_apply_automorphism_dev(self, ct, element, gk, num_keys, out, batch):
+        check(self._lib.exacto_bfv_apply_automorphism_dev(self._h, self._p(ct), 2, element, self._p(gk), num_keys,
+                                                          self._p(out), batch))
+
     def gadget_decompose_dev(self, coeffs, digits, batch, num_digits):
         check(self._lib.exacto_gadget_decompose_dev(self._h, self._p(coeffs), self._p(digits),
                                                     batch, num_digits))
