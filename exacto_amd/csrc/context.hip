@@ -983,9 +983,16 @@ extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t 
         nb.dst = c->ws_coefQ; nb.dst_item_stride = Ln;
         nb.ppi = c->L; nb.prime_base = 0; nb.period = c->L;
         if (int e = run_ntt(c, nb, (long)cnt * c->L, true)) return e;
-        launch_decompose(c->ws_coefQ, Ln, c->ws_D, guse, cnt, c->n, c->d_crt, c->d_primes, c->L, c->stream);
+        const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
+        launch_decompose(c->ws_coefQ, Ln, c->ws_D, guse, cnt, c->n, c->d_crt, c->d_primes, c->L, c->stream,
+                         d16 ? c->ws_D16 : nullptr);
         CHECK_LAUNCH();
-        if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * c->L, 0, c->L, c->n), (long)cnt * guse * c->L, false)) return e;
+        NttBatch db = contiguous(c->ws_D, cnt, (long)guse * c->L, 0, c->L, c->n);
+        if (d16) {
+            db.src16 = c->ws_D16;
+            db.src16_item_stride = (long)guse * c->n;
+        }
+        if (int e = run_ntt(c, db, (long)cnt * guse * c->L, false)) return e;
         if (int e = ensure_rlk_companions(c)) return e;
         launch_relin_mac(dst, 2 * Ln, c->ws_D, c->d_rlk, c->d_rlk_s, guse, dst, 2 * Ln, cnt, c->n, c->L,
                          c->d_primes, c->stream);
@@ -1648,10 +1655,16 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
         c0.ppi = L; c0.prime_base = 0; c0.period = L;
         if (int e = run_ntt(c, c0, (long)cnt * L, false)) return e;
         HIP_TRY(hipMemset2DAsync(dst + Ln, 2 * Ln * sizeof(u64), 0, Ln * sizeof(u64), cnt, c->stream));
-        launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream);
+        const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
+        launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream,
+                         d16 ? c->ws_D16 : nullptr);
         CHECK_LAUNCH();
-        if (int e = run_ntt(c, contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n), (long)cnt * guse * L, false))
-            return e;
+        NttBatch db = contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n);
+        if (d16) {
+            db.src16 = c->ws_D16;
+            db.src16_item_stride = (long)guse * n;
+        }
+        if (int e = run_ntt(c, db, (long)cnt * guse * L, false)) return e;
         launch_relin_mac(dst, 2 * Ln, c->ws_D, gk, c->gk_s, guse, dst, 2 * Ln, cnt, n, L, c->d_primes, c->stream);
         CHECK_LAUNCH();
     }

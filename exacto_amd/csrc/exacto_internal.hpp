@@ -127,8 +127,9 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);
+// D16 != nullptr (gadget base <= 2^16): signed int16 digits [item][g][n] instead of residues
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
-                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s);
+                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s, int16_t* D16 = nullptr);
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
                       hipStream_t s);

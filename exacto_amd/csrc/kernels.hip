@@ -637,21 +637,24 @@ void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, 
 // ---------------------------------------------------------------- standalone decomposition
 
 __global__ void __launch_bounds__(TPB)
-decompose_kernel(const u64* __restrict__ C2, long c2_stride, u64* __restrict__ D, int guse, int n,
-                 int L, const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+decompose_kernel(const u64* __restrict__ C2, long c2_stride, u64* __restrict__ D, int16_t* __restrict__ D16,
+                 int guse, int n, int L, const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
     u64 res[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L) res[i] = C2[row * c2_stride + (long)i * n + j];
-    gadget_digits<false>(res, L, C, primes, D + row * (long)guse * L * n + j, n, guse);
+    if (D16)
+        gadget_digits<false>(res, L, C, primes, nullptr, n, guse, D16 + row * (long)guse * n + j);
+    else
+        gadget_digits<false>(res, L, C, primes, D + row * (long)guse * L * n + j, n, guse);
 }
 
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,
-                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s) {
+                      const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s, int16_t* D16) {
     const long blocks = (long)items * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(decompose_kernel, dim3(blocks), dim3(TPB), 0, s, C2, c2_stride, D, guse, n, L,
+    hipLaunchKernelGGL(decompose_kernel, dim3(blocks), dim3(TPB), 0, s, C2, c2_stride, D, D16, guse, n, L,
                        ct, primes);
 }
 
