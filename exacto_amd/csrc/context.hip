@@ -975,8 +975,8 @@ extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t 
         const u64* src = ct + s * 3 * Ln;
         u64* dst = out + s * 2 * Ln;
         // c0, c1 copied, then accumulated in place
-        HIP_TRY(hipMemcpy2DAsync(dst, 2 * Ln * sizeof(u64), src, 3 * Ln * sizeof(u64), 2 * Ln * sizeof(u64), cnt,
-                                 hipMemcpyDeviceToDevice, c->stream));
+        launch_rows(dst, 2 * Ln, src, 3 * Ln, 2 * Ln, cnt, c->stream);
+        CHECK_LAUNCH();
         if (guse == 0) continue;
         NttBatch nb{};
         nb.src = src + 2 * Ln; nb.src_off = nullptr; nb.src_item_stride = 3 * Ln;
@@ -1654,7 +1654,7 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
         c0.dst = dst; c0.dst_item_stride = 2 * Ln;
         c0.ppi = L; c0.prime_base = 0; c0.period = L;
         if (int e = run_ntt(c, c0, (long)cnt * L, false)) return e;
-        HIP_TRY(hipMemset2DAsync(dst + Ln, 2 * Ln * sizeof(u64), 0, Ln * sizeof(u64), cnt, c->stream));
+        launch_rows(dst + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
         const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
         launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream,
                          d16 ? c->ws_D16 : nullptr);
@@ -1780,7 +1780,7 @@ static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u
     if (ks.empty()) return 0;
     const long Ln = (long)c->L * c->n;
     u64* rot = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&rot, B * 2 * Ln * sizeof(u64), c->stream));
+    HIP_TRY(hipMalloc((void**)&rot, B * 2 * Ln * sizeof(u64)));
     int rc = 0;
     for (size_t e = 0; e < ks.size() && rc == 0; ++e) {
         rc = exacto_bfv_apply_automorphism_dev(c, src ? src : r, 2, ks[e], gks + kidx[e] * num_keys * 2 * Ln,
@@ -1790,7 +1790,8 @@ static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u
             if (hipGetLastError() != hipSuccess) rc = fail(EXACTO_ERR_HIP, "HIP error: trace add launch");
         }
     }
-    HIP_TRY(hipFreeAsync(rot, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(rot));
     return rc;
 }
 
@@ -1854,14 +1855,17 @@ extern "C" int exacto_extract_coefficients_dev(exacto_ctx* c, const uint64_t* ct
     CHECK_LAUNCH();
     if (int e = ntt_items(c, c->pl_buf, (long)J, Ln, c->L)) return e;
     u64* shifted = out;
-    if (naive) HIP_TRY(hipMallocAsync((void**)&shifted, J * 2 * Ln * sizeof(u64), c->stream));
+    if (naive) HIP_TRY(hipMalloc((void**)&shifted, J * 2 * Ln * sizeof(u64)));
     launch_plain_apply(PLAIN_MUL, ct, 0, shifted, (long)J, 2, c->pl_buf, Ln, n, c->L, c->d_primes, c->stream);
     int rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: monomial launch");
     if (rc == 0 && naive)
         rc = hipMemcpyAsync(out, shifted, J * 2 * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream) == hipSuccess
                  ? 0 : fail(EXACTO_ERR_HIP, "HIP error: copy");
     if (rc == 0) rc = trace_core(c, naive ? shifted : nullptr, out, ks, kidx, gks, num_keys, J);
-    if (naive) HIP_TRY(hipFreeAsync(shifted, c->stream));
+    if (naive) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipFree(shifted));
+    }
     if (rc) return rc;
     // times the constant plaintext n^-1: NTT(constant) is that constant in every slot
     return exacto_rns_scalar_mul_dev(c, out, n_inv, out, J * 2);
@@ -2015,9 +2019,9 @@ extern "C" int exacto_trivial_encrypt_dev(exacto_ctx* c, const uint64_t* pt, uin
     if (B == 0) return 0;
     const long Ln = (long)c->L * c->n;
     if (int e = lift_plain(c, pt, (long)B, true)) return e;
-    HIP_TRY(hipMemcpy2DAsync(out, 2 * Ln * sizeof(u64), c->pl_buf, Ln * sizeof(u64), Ln * sizeof(u64), B,
-                             hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemset2DAsync(out + Ln, 2 * Ln * sizeof(u64), 0, Ln * sizeof(u64), B, c->stream));
+    launch_rows(out, 2 * Ln, c->pl_buf, Ln, Ln, (long)B, c->stream);
+    launch_rows(out + Ln, 2 * Ln, nullptr, 0, Ln, (long)B, c->stream);
+    CHECK_LAUNCH();
     return 0;
 }
 
@@ -2048,7 +2052,7 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
     // workspace: baby[0], baby[2..k] (baby[1] is ct), one group accumulator, a Horner ping buffer
     const size_t nbuf = k + 3;
     u64* ws = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&ws, nbuf * words * sizeof(u64), c->stream));
+    HIP_TRY(hipMalloc((void**)&ws, nbuf * words * sizeof(u64)));
     std::vector<const u64*> baby(k + 1);
     auto slot = [&](size_t i) { return ws + i * words; };
     baby[0] = slot(0);
@@ -2089,7 +2093,8 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
         }
         std::swap(res, other);
     }
-    HIP_TRY(hipFreeAsync(ws, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(ws));
     return rc;
 }
 
@@ -2172,10 +2177,11 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64* c0pt = nullptr;  // [B][n] copies of c0' and c1' rows in the plaintext layout
     if (rc == 0) ok(hipMalloc((void**)&c0pt, 2 * B * n * sizeof(u64)), "alloc");
     u64* c1pt = c0pt + B * n;
-    if (rc == 0) ok(hipMemcpy2DAsync(c0pt, n * sizeof(u64), small, 2 * n * sizeof(u64), n * sizeof(u64), B,
-                                     hipMemcpyDeviceToDevice, b->stream), "copy c0");
-    if (rc == 0) ok(hipMemcpy2DAsync(c1pt, n * sizeof(u64), small + n, 2 * n * sizeof(u64), n * sizeof(u64), B,
-                                     hipMemcpyDeviceToDevice, b->stream), "copy c1");
+    if (rc == 0) {
+        launch_rows(c0pt, n, small, 2 * n, n, (long)B, b->stream);
+        launch_rows(c1pt, n, small + n, 2 * n, n, (long)B, b->stream);
+        ok(hipGetLastError(), "copy c0/c1");
+    }
     if (rc == 0) rc = lift_plain(b, c1pt, (long)B, false);
     if (rc == 0) {
         launch_plain_apply(PLAIN_MUL, bsk, 0, out, (long)B, 2, b->pl_buf, Lbn, n, b->L, b->d_primes, b->stream);

@@ -767,6 +767,26 @@ relin_mac_lds_kernel(const u64* __restrict__ base, long base_stride, const u64* 
     }
 }
 
+// Strided row copy / zero fill: dst[r * dst_stride + k] = src ? src[r * src_stride + k] : 0 for
+// k < len, r < rows: the strided ciphertext-component fills and copies as one ordinary kernel on
+// the context stream (no 2D memset/memcpy engine path).
+__global__ void __launch_bounds__(TPB)
+rows_kernel(u64* __restrict__ dst, long dst_stride, const u64* __restrict__ src, long src_stride, long len,
+            long total) {
+    for (long t = (long)blockIdx.x * TPB + threadIdx.x; t < total; t += (long)gridDim.x * TPB) {
+        const long r = t / len, k = t - r * len;
+        dst[r * dst_stride + k] = src ? src[r * src_stride + k] : 0;
+    }
+}
+
+void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, long len, long rows, hipStream_t s) {
+    const long total = len * rows;
+    if (total <= 0) return;
+    const long blocks = std::min<long>((total + TPB - 1) / TPB, 65536);
+    hipLaunchKernelGGL(rows_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, dst, dst_stride, src, src_stride, len,
+                       total);
+}
+
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
                       hipStream_t s) {

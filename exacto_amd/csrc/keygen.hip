@@ -249,7 +249,7 @@ void launch_automorph(const u64* in, long in_stride, u64* out, long out_stride, 
         hipLaunchKernelGGL(automorph_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, in, in_stride, out,
                            out_stride, polys, n, L, kinv, primes, prime_fixed);
     } else {
-        (void)hipMemset2DAsync(out, out_stride * sizeof(u64), 0, (size_t)polys * L * n * sizeof(u64), items, s);
+        launch_rows(out, out_stride, nullptr, 0, (long)polys * L * n, items, s);
         hipLaunchKernelGGL(automorph_serial_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, in,
                            in_stride, out, out_stride, polys, n, L, k, rows, primes, prime_fixed);
     }
