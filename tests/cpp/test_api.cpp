@@ -216,6 +216,9 @@ static int bootstrap_case() {
     auto back = decrypt(slots_to_coeffs(slots), sk);
     if (back.coeffs != m.coeffs) return 31;
     if (decode_scalar(decrypt(extract_coefficient(ct, 2, keys), sk)) != 3) return 32;
+    // regression: a batched extraction after a single one (scratch reuse across calls) is exact
+    for (int rep = 0; rep < 3; ++rep)
+        if (decode_scalar(decrypt(coeffs_to_slots(ct, keys)[2], sk)) != 3) return 39;
     if (required_trace_elements(64) != std::vector<size_t>{65, 33, 17, 9, 5, 3}) return 33;
     auto compact = BfvParamsBuilder().ring_degree(1024).plain_modulus(257).ct_moduli({1099509805057ull})
                        .aux_moduli({562949953443841ull}).sigma(3.2).build();
