@@ -188,6 +188,7 @@ struct exacto_ctx {
     bool rlk_s_valid = false;
     bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
+    bool ntt_pipe = true;   // EXACTO_NTT_PIPE=0: one workgroup per polynomial instead of the persistent LDS-DMA kernel
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
@@ -507,6 +508,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     c->own_stream = true;
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
@@ -618,9 +620,9 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     bool lazy = true, near60 = c->ntt_asm;
     for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) {
         lazy &= c->primes[t] < (1ull << 60);
-        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 56);
+        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
     }
-    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60);
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, c->ntt_pipe);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));

@@ -65,10 +65,11 @@ struct CrtTables {
 };
 
 // lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)
-// asm_fwd: every prime of the batch is in (2^60 - 2^56, 2^60) and the hand-scheduled forward
+// asm_fwd: every prime of the batch is in (2^60 - 2^32, 2^60) and the hand-scheduled forward
 // kernel (ntt_asm.inc) may be used for n = 4096 / 8192
+// pipe: n = 4096 forward transforms run on the persistent LDS-DMA kernel (ntt_fwd_pipe_kernel)
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd = false);
+                hipStream_t s, bool asm_fwd = false, bool pipe = false);
 
 // Fused relinearisation: see keyswitch_kernel in ntt.hip.
 struct KsArgs {

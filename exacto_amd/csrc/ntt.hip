@@ -253,7 +253,7 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 
 // ---------------------------------------------------------------- forward, hand-scheduled rounds
 
-// n = 4096 / 8192 with every prime of the batch in (2^60 - 2^56, 2^60): the butterfly rounds are
+// n = 4096 / 8192 with every prime of the batch in (2^60 - 2^32, 2^60): the butterfly rounds are
 // the generated inline-asm statements of ntt_asm.inc (tools/gen_ntt_asm.py): two butterflies
 // interleaved so that the SGPR carry chains of the 64-bit arithmetic need no s_nop padding.
 // Same convention, same LDS exchanges and same output layout as ntt_fwd_kernel.
@@ -324,13 +324,7 @@ ntt_fwd_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64 x[16];
     load_coeffs<N>(x, nb, src, item, sub, q, tid);
 
-    AsmK K;
-    const u64 nq = (u64)0 - q, q2 = 2 * q, nq8 = (u64)0 - 8 * q;
-    K.n0 = (uint32_t)nq; K.n1 = (uint32_t)(nq >> 32);
-    K.q2l = (uint32_t)q2; K.q2h = (uint32_t)(q2 >> 32);
-    K.nq8l = (uint32_t)nq8; K.nq8h = (uint32_t)(nq8 >> 32);
-    K.nql = K.n0; K.nqh = K.n1;
-    K.q8 = 8 * q; K.q = q;
+    const AsmK K = make_asmk(q);
     fwd_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_fwd), K);
 
     // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
@@ -342,6 +336,229 @@ ntt_fwd_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     lds_load_x<LOGN - 4>(lds, x, t2);
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+}
+
+// ---------------------------------------------------------------- forward, persistent + LDS-DMA prefetch
+
+// The kernel above loads a polynomial, transforms it and stores it; its co-resident workgroups
+// start together and stay in phase, so the chip alternates between a memory phase and a compute
+// phase ("what bounds the forward transform").  This form keeps a fixed set of
+// workgroups resident (2 per CU, 64 KiB of LDS each) and streams polynomials through them:
+// while polynomial p is transformed in registers, polynomial p + grid is already on its way
+// from HBM into the other half of the workgroup's LDS by global_load_lds (LDS-DMA, no VGPRs).
+//
+// Every vector-memory operation inside the loop is an inline-asm statement (the DMA and the
+// output stores), so hipcc's waitcnt pass sees no loads to wait for and the counted
+// `s_waitcnt vmcnt(16)` at the top of each iteration (this wave's 16 output stores of the
+// previous polynomial may stay in flight) is the only wait on the DMA.  Twiddles: round 0 is
+// block-uniform (scalar loads, lgkmcnt); rounds 1 and 2 are per-thread and stay in VGPRs for
+// as long as the workgroup's prime does not change -- with the grid a multiple of the batch's
+// prime period, never.
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// one wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane gsrc to lds_dst + 16 * lane
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+
+// This wave's share of one polynomial's source bytes -> LDS image at lds_base (natural order).
+template <int BYTES, int WAVES>
+__device__ __forceinline__ void dma_share(const void* src, uint32_t lds_base, int wave, int lane) {
+    constexpr int PER = BYTES / WAVES;
+    static_assert(PER % 1024 == 0, "a wave moves whole 1 KiB pieces");
+    const char* s = (const char*)src + wave * PER + lane * 16;
+    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_base + wave * PER);
+#pragma unroll
+    for (int i = 0; i < PER / 1024; ++i) dma16(s + i * 1024, d + i * 1024);
+}
+
+__device__ __forceinline__ u64 sload_u64(const u64* p) {
+    u64 r;
+    asm volatile("s_load_dwordx2 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+    return r;
+}
+
+// Round-0 twiddles of an n = 4096 transform (indices 1..15, block-uniform) by scalar loads.
+__device__ __forceinline__ void sload_round0_tw(TwPair (&tw)[15], const TwPair* tab) {
+    u32x4 v[15];
+    asm volatile(
+        "s_load_dwordx4 %0, %15, 16\n\ts_load_dwordx4 %1, %15, 32\n\ts_load_dwordx4 %2, %15, 48\n\t"
+        "s_load_dwordx4 %3, %15, 64\n\ts_load_dwordx4 %4, %15, 80\n\ts_load_dwordx4 %5, %15, 96\n\t"
+        "s_load_dwordx4 %6, %15, 112\n\ts_load_dwordx4 %7, %15, 128\n\ts_load_dwordx4 %8, %15, 144\n\t"
+        "s_load_dwordx4 %9, %15, 160\n\ts_load_dwordx4 %10, %15, 176\n\ts_load_dwordx4 %11, %15, 192\n\t"
+        "s_load_dwordx4 %12, %15, 208\n\ts_load_dwordx4 %13, %15, 224\n\ts_load_dwordx4 %14, %15, 240\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=s"(v[0]), "=s"(v[1]), "=s"(v[2]), "=s"(v[3]), "=s"(v[4]), "=s"(v[5]), "=s"(v[6]), "=s"(v[7]),
+          "=s"(v[8]), "=s"(v[9]), "=s"(v[10]), "=s"(v[11]), "=s"(v[12]), "=s"(v[13]), "=s"(v[14])
+        : "s"(tab)
+        : "memory");
+#pragma unroll
+    for (int i = 0; i < 15; ++i) {
+        tw[i].w = (u64)v[i].x | ((u64)v[i].y << 32);
+        tw[i].ws = (u64)v[i].z | ((u64)v[i].w << 32);
+    }
+}
+
+// 16 coalesced 8-byte stores per thread: element tid + k*T of dst <- x[k] (byte offsets
+// off[j] = 8*tid + j*4096 with immediate 0 / 2048).  The trailing s_nop keeps hipcc from
+// reusing the data registers before the last store has read them.
+__device__ __forceinline__ void store_poly4096(u64* dst, const u64 (&x)[16], const uint32_t (&off)[8]) {
+    asm volatile(
+        "global_store_dwordx2 %16, %0, %24\n\tglobal_store_dwordx2 %16, %1, %24 offset:2048\n\t"
+        "global_store_dwordx2 %17, %2, %24\n\tglobal_store_dwordx2 %17, %3, %24 offset:2048\n\t"
+        "global_store_dwordx2 %18, %4, %24\n\tglobal_store_dwordx2 %18, %5, %24 offset:2048\n\t"
+        "global_store_dwordx2 %19, %6, %24\n\tglobal_store_dwordx2 %19, %7, %24 offset:2048\n\t"
+        "global_store_dwordx2 %20, %8, %24\n\tglobal_store_dwordx2 %20, %9, %24 offset:2048\n\t"
+        "global_store_dwordx2 %21, %10, %24\n\tglobal_store_dwordx2 %21, %11, %24 offset:2048\n\t"
+        "global_store_dwordx2 %22, %12, %24\n\tglobal_store_dwordx2 %22, %13, %24 offset:2048\n\t"
+        "global_store_dwordx2 %23, %14, %24\n\tglobal_store_dwordx2 %23, %15, %24 offset:2048\n\t"
+        "s_nop 1"
+        :
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]),
+          "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14]), "v"(x[15]), "v"(off[0]),
+          "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]), "s"(dst)
+        : "memory");
+}
+
+struct PipeSrc {
+    const void* src;  // u64 polynomial or int16 digit row
+    int prime;        // index into primes[]
+    u64* dst;
+};
+
+// Source / destination / prime of polynomial p (all block-uniform; src_off by a scalar load).
+__device__ __forceinline__ PipeSrc pipe_locate(const NttBatch& nb, int p, int N) {
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    PipeSrc r;
+    r.prime = nb.prime_base + sub % nb.period;
+    if (nb.src16) {
+        r.src = nb.src16 + (long)item * nb.src16_item_stride + (long)(sub / nb.period) * N;
+    } else {
+        const long base = nb.src_off ? (long)sload_u64(nb.src_off + item) : (long)item * nb.src_item_stride;
+        r.src = nb.src + base + (long)sub * N;
+    }
+    r.dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    return r;
+}
+
+template <int LOGN>
+__device__ __forceinline__ void pipe_issue(const NttBatch& nb, const PipeSrc& s, uint32_t lds_base, int wave,
+                                           int lane) {
+    constexpr int N = 1 << LOGN, WAVES = N / 16 / 64;
+    if (nb.src16) dma_share<N * 2, WAVES>(s.src, lds_base, wave, lane);
+    else dma_share<N * 8, WAVES>(s.src, lds_base, wave, lane);
+}
+
+// EXACTO_PIPE_PROBE (measurement builds only, wrong results): 1 = no DMA and no stores (compute
+// and LDS exchanges alone), 2 = no butterfly rounds (memory and LDS exchanges alone)
+#ifndef EXACTO_PIPE_PROBE
+#define EXACTO_PIPE_PROBE 0
+#endif
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+ntt_fwd_pipe_kernel(NttBatch nb, const PrimeConst* __restrict__ primes, int count) {
+    constexpr int LOGN = 12, N = 1 << LOGN, T = N / 16;
+    __shared__ u64 lds[2 * N];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int p = blockIdx.x;
+    if (p >= count) return;
+    const uint32_t lds0 = lds_u32(lds);
+
+    uint32_t off[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) off[j] = 8 * tid + 4096 * j;
+
+    PipeSrc cur = pipe_locate(nb, p, N);
+    if (EXACTO_PIPE_PROBE != 1) pipe_issue<LOGN>(nb, cur, lds0, wave, lane);
+
+    int have = -1;
+    AsmK K{};
+    TwPair tw1[15], tw2[15];
+    u64 q = 0;
+    const TwPair* tab = nullptr;
+    int buf = 0;
+    bool first = true;
+    for (;;) {
+        if (cur.prime != have) {
+            // (re)load the prime's constants and the per-thread twiddles of rounds 1 and 2; the
+            // empty asm consumes them so that hipcc waits for these loads here, before the next
+            // DMA is issued, not at their first use in the loop
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const PrimeConst& P = primes[cur.prime];
+            q = P.q;
+            tab = P.tw_fwd;
+            const TwTab tt = tw_table(tab);
+            load_round_tw<LOGN, 4, 7, 4>(tw1, tid, tt);
+            load_round_tw<LOGN, 0, 3, 0>(tw2, tid, tt);
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+                asm volatile("" ::"v"(tw1[i].w), "v"(tw1[i].ws), "v"(tw2[i].w), "v"(tw2[i].ws));
+            K = make_asmk(q);
+            have = cur.prime;
+        }
+        // this wave's DMA of polynomial p has landed (the 16 younger ops are the previous
+        // polynomial's stores); the barrier makes every wave's share visible
+        if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        first = false;
+        lds_barrier();
+        u64* L0 = lds + buf * N;
+        u64 x[16];
+        if (nb.src16) {
+            const int16_t* s16 = reinterpret_cast<const int16_t*>(L0);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const i64 d = s16[tid + k * T];
+                x[k] = d < 0 ? q + (u64)d : (u64)d;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = L0[tid + k * T];
+        }
+        TwPair tw0[15];
+        sload_round0_tw(tw0, tab);  // its lgkmcnt(0) also retires the reads above
+        // prefetch the next polynomial into the other half (free: its last reads were in the
+        // previous iteration, before the barrier above)
+        const int pn = p + (int)gridDim.x;
+        PipeSrc nxt{};
+        if (pn < count) {
+            nxt = pipe_locate(nb, pn, N);
+            if (EXACTO_PIPE_PROBE != 1) pipe_issue<LOGN>(nb, nxt, lds0 + (buf ^ 1) * N * 8, wave, lane);
+        }
+        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 0>::run(x, tw0, K);
+        int t2 = tid;
+        asm volatile("" : "+v"(t2));
+        lds_barrier();
+        lds_store_x<8>(L0, x, t2);
+        lds_barrier();
+        lds_load_x<4>(L0, x, t2);
+        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 1>::run(x, tw1, K);
+        lds_barrier();
+        lds_store_x<4>(L0, x, t2);
+        lds_barrier();
+        lds_load_x<0>(L0, x, t2);
+        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 2>::run(x, tw2, K);
+        // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
+        lds_barrier();
+        lds_store_x<0>(L0, x, t2);
+        lds_barrier();
+        lds_load_x<LOGN - 4>(L0, x, t2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (EXACTO_PIPE_PROBE != 1) store_poly4096(cur.dst, x, off);
+        if (pn >= count) break;
+        p = pn;
+        cur = nxt;
+        buf ^= 1;
+    }
 }
 
 // ---------------------------------------------------------------- inverse
@@ -722,9 +939,29 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
     }
 }
 
+static int cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd) {
+                hipStream_t s, bool asm_fwd, bool pipe) {
     if (count <= 0) return;
+    if (asm_fwd && pipe && !inverse && logn == 12) {
+        // two resident workgroups per CU; a grid that is a multiple of the prime period keeps
+        // every workgroup on one prime (twiddles loaded once)
+        const int slots = 2 * cu_count();
+        int grid = slots >= nb.period ? (slots / nb.period) * nb.period : slots;
+        if (grid > count) grid = count;
+        hipLaunchKernelGGL(ntt_fwd_pipe_kernel, dim3(grid), dim3(256), 0, s, nb, primes, count);
+        return;
+    }
     if (asm_fwd && !inverse && logn == 12) {
         hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
         return;

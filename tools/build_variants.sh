@@ -9,7 +9,8 @@ H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC"
 build() {  # name, flags...
   local name=$1; shift
   $H "$@" -c $R/exacto_amd/csrc/ntt.hip -o $OUT/ntt_$name.o
-  $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o $OUT/ntt_$name.o
+  $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o \
+    $R/build/obj/keygen.o $R/build/obj/plain.o $OUT/ntt_$name.o
 }
 for v in "$@"; do
   case $v in
@@ -27,8 +28,8 @@ for v in "$@"; do
     w5) build w5 -DEXACTO_NTT_WAVES=5 ;;
     ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
-    probe0) build probe0 -DEXACTO_ASM_PROBE=0 ;;
-    probe2) build probe2 -DEXACTO_ASM_PROBE=2 ;;
+    pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
+    pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
