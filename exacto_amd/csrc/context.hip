@@ -253,6 +253,33 @@ static void free_dev(void* p) {
     if (p) (void)hipFree(p);
 }
 
+// Per-call scratch from the stream-ordered pool (hipMallocAsync / hipFreeAsync on the stream that
+// uses it; no device-wide synchronisation).  EXACTO_DEBUG_SCRATCH=1 fills every block with 0xFF
+// when it is handed out, so a kernel that reads scratch it never wrote gives wrong results at once
+// instead of whatever the previous owner of the block left there.
+static const bool g_debug_scratch = [] {
+    const char* e = getenv("EXACTO_DEBUG_SCRATCH");
+    return e && atoi(e) != 0;
+}();
+
+struct Scratch {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    Scratch() = default;
+    Scratch(const Scratch&) = delete;
+    Scratch& operator=(const Scratch&) = delete;
+    ~Scratch() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+    hipError_t alloc(size_t bytes, hipStream_t st) {
+        s = st;
+        hipError_t e = hipMallocAsync(&p, std::max<size_t>(bytes, 8), st);
+        if (e == hipSuccess && g_debug_scratch) e = hipMemsetAsync(p, 0xFF, std::max<size_t>(bytes, 8), st);
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 static int grow(u64** buf, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
     free_dev(*buf);
@@ -260,6 +287,17 @@ static int grow(u64** buf, size_t* cap, size_t bytes) {
     *cap = 0;
     HIP_TRY(hipMalloc((void**)buf, bytes));
     *cap = bytes;
+    return 0;
+}
+
+// Host -> device copy ordered on the context stream.  The stream is non-blocking, so it does not
+// wait for the legacy null stream that a plain hipMemcpy runs on: a kernel enqueued on it right
+// after such a copy may read the destination before the copy has landed.  Returns once the copy
+// is complete, so `src` may be reused at once.
+static int upload(exacto_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return 0;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
 
@@ -307,13 +345,13 @@ static int build_tables(exacto_ctx* c) {
         pc[t] = make_prime_const(c->primes[t], c->n, c->logn, &tw[(size_t)t * 2 * c->n],
                                  &tw[(size_t)t * 2 * c->n + c->n]);
     HIP_TRY(hipMalloc((void**)&c->d_tw, tw.size() * sizeof(TwPair)));
-    HIP_TRY(hipMemcpy(c->d_tw, tw.data(), tw.size() * sizeof(TwPair), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_tw, tw.data(), tw.size() * sizeof(TwPair))) return e_;
     for (int t = 0; t < NP; ++t) {
         pc[t].tw_fwd = c->d_tw + (size_t)t * 2 * c->n;
         pc[t].tw_inv = c->d_tw + (size_t)t * 2 * c->n + c->n;
     }
     HIP_TRY(hipMalloc((void**)&c->d_primes, NP * sizeof(PrimeConst)));
-    HIP_TRY(hipMemcpy(c->d_primes, pc.data(), NP * sizeof(PrimeConst), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_primes, pc.data(), NP * sizeof(PrimeConst))) return e_;
 
     // ---- CRT tables
     CrtTables& C = c->h_crt;
@@ -393,7 +431,7 @@ static int build_tables(exacto_ctx* c) {
     }
     HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
     HIP_TRY(hipMalloc((void**)&c->d_crt, sizeof(CrtTables)));
-    HIP_TRY(hipMemcpy(c->d_crt, &C, sizeof(CrtTables), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_crt, &C, sizeof(CrtTables))) return e_;
     return 0;
 }
 
@@ -506,6 +544,18 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
     c->own_stream = true;
+    {
+        // Per-call scratch (Scratch) comes from the device's default stream-ordered pool.  Keep its
+        // freed blocks mapped for reuse instead of returning them to the driver at every
+        // synchronisation (release threshold 0, the default): no map/unmap per call, and on this
+        // ROCm 7.2 stack blocks re-acquired after such a release gave wrong results at n = 16
+        // ("Scratch"), which keeping them mapped avoids.
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t thr = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+    }
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
@@ -603,7 +653,7 @@ extern "C" int exacto_ctx_load_relin_key(exacto_ctx* c, const uint64_t* rlk, siz
     if (num_keys && !rlk) return invalid_param("null relinearization key");
     u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
     if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
-    if (num_keys) HIP_TRY(hipMemcpy(dst, rlk, num_keys * 2 * c->L * poly_bytes(c), hipMemcpyHostToDevice));
+    if (num_keys) if (int e_ = upload(c, dst, rlk, num_keys * 2 * c->L * poly_bytes(c))) return e_;
     return 0;
 }
 
@@ -887,7 +937,7 @@ static int ntt_host(exacto_ctx* c, uint64_t* polys, size_t count, size_t limb, b
     if (int e = check_ctx(c)) return e;
     const size_t bytes = count * poly_bytes(c);
     if (int e = stage(c, std::max<size_t>(bytes, 8))) return e;
-    HIP_TRY(hipMemcpy(c->io, polys, bytes, hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->io, polys, bytes)) return e_;
     if (int e = ntt_dev(c, c->io, count, limb, inverse)) return e;
     HIP_TRY(hipMemcpyAsync(polys, c->io, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -921,7 +971,7 @@ extern "C" int exacto_rns_scalar_mul_dev(exacto_ctx* c, const uint64_t* a, uint6
     u64 sm[EXACTO_MAX_L];
     for (int i = 0; i < c->L; ++i) sm[i] = scalar % c->ctq[i];
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_scal, sm, c->L * sizeof(u64), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_scal, sm, c->L * sizeof(u64))) return e_;
     return pw(c, PwOp::ScalarMul, a, nullptr, o, (long)n * c->L, c->d_scal);
 }
 
@@ -961,10 +1011,9 @@ extern "C" int exacto_bfv_mul_and_relin_dev(exacto_ctx* c, const uint64_t* ct1, 
 extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t* out, size_t B) {
     if (int e = check_ctx(c)) return e;
     const long Ln = (long)c->L * c->n;
-    if (polys < 3) {  // keyswitch.rs:63-65: already degree-1, cloned
-        for (size_t b = 0; b < B; ++b)
-            HIP_TRY(hipMemcpyAsync(out + b * 2 * Ln, ct + b * polys * Ln, polys * Ln * sizeof(u64),
-                                   hipMemcpyDeviceToDevice, c->stream));
+    if (polys < 3) {  // keyswitch.rs:63-65: already degree-1, cloned: out = [B][polys][L][n]
+        if (B * polys)
+            HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
         return 0;
     }
     if (polys > 3) return invalid_param("relinearization only supports degree-2 ciphertexts");
@@ -1022,10 +1071,13 @@ static int host_call(exacto_ctx* c, const std::vector<std::pair<const void*, siz
     std::vector<u64*> dins;
     char* p = (char*)c->io;
     for (auto& in : ins) {
-        if (in.second) HIP_TRY(hipMemcpy(p, in.first, in.second, hipMemcpyHostToDevice));
+        // stream-ordered on the context stream (see upload)
+        if (in.second) HIP_TRY(hipMemcpyAsync(p, in.first, in.second, hipMemcpyHostToDevice, c->stream));
         dins.push_back((u64*)p);
         p += (in.second + 255) / 256 * 256;
     }
+    // landed before fn runs: fn may read the inputs on another context's stream (bootstrap)
+    HIP_TRY(hipStreamSynchronize(c->stream));
     u64* dout = (u64*)p;
     if (int e = fn(dins, dout)) return e;
     HIP_TRY(hipMemcpyAsync(host_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1120,14 +1172,14 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
     size_t cap = c->off_cap;
     if (grow(&c->d_off, &cap, off.size() * sizeof(u64) + 8)) return EXACTO_ERR_HIP;
     c->off_cap = cap;
-    HIP_TRY(hipMemcpy(c->d_off, off.data(), off.size() * sizeof(u64), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_off, off.data(), off.size() * sizeof(u64))) return e_;
     free_dev(c->d_term_start);
     free_dev(c->d_terms);
     HIP_TRY(hipMalloc((void**)&c->d_term_start, start.size() * sizeof(int)));
-    HIP_TRY(hipMemcpy(c->d_term_start, start.data(), start.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_term_start, start.data(), start.size() * sizeof(int))) return e_;
     HIP_TRY(hipMalloc((void**)&c->d_terms, std::max<size_t>(terms.size(), 1) * sizeof(CombineTerm)));
     if (!terms.empty())
-        HIP_TRY(hipMemcpy(c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm), hipMemcpyHostToDevice));
+        if (int e_ = upload(c, c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm))) return e_;
     c->cached_B = B; c->cached_d = d; c->cached_base = base; c->cached_p = plain;
     c->cached_npairs = npairs;
     return 0;
@@ -1378,7 +1430,7 @@ static int gaussian_table(exacto_ctx* c, double sigma, int* tail, int* len, doub
         if (grow((u64**)&c->d_cdt, &cap, cdf.size() * sizeof(double))) return EXACTO_ERR_HIP;
         c->cdt_cap = cap;
         HIP_TRY(hipStreamSynchronize(c->stream));  // in-flight samplers may still read the old table
-        HIP_TRY(hipMemcpy(c->d_cdt, cdf.data(), cdf.size() * sizeof(double), hipMemcpyHostToDevice));
+        if (int e_ = upload(c, c->d_cdt, cdf.data(), cdf.size() * sizeof(double))) return e_;
         c->cdt_sigma = sigma;
     }
     *tail = t;
@@ -1465,7 +1517,7 @@ extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, doubl
     c->gpow_cap = cap;
     // the table is host-pageable and d_gpow may still be read by a previous call's kernels
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_gpow, gpow.data(), gpow.size() * sizeof(u64))) return e_;
     const ChaChaKey k = chacha_key(key);
     // key i: a_i (index 2i) into the rlk1 slot, e_i (index 2i+1) into the rlk0 slot
     if (int e = sample_polys(c, KG_UNIFORM, k, stream, rlk + Ln, 2 * Ln, 0, 2, (long)num_keys, sigma)) return e;
@@ -1514,7 +1566,7 @@ static int delta_residues(exacto_ctx* c) {
         dr[i] = (u64)r;
     }
     if (!c->d_delta) HIP_TRY(hipMalloc((void**)&c->d_delta, EXACTO_MAX_L * sizeof(u64)));
-    HIP_TRY(hipMemcpy(c->d_delta, dr.data(), dr.size() * sizeof(u64), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_delta, dr.data(), dr.size() * sizeof(u64))) return e_;
     c->delta_ok = true;
     return 0;
 }
@@ -1608,7 +1660,7 @@ extern "C" int exacto_gen_galois_key_dev(exacto_ctx* c, const uint64_t* sk, uint
     c->gpow_cap = cap;
     // the table is host-pageable and d_gpow may still be read by a previous call's kernels
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_gpow, gpow.data(), gpow.size() * sizeof(u64), hipMemcpyHostToDevice));
+    if (int e_ = upload(c, c->d_gpow, gpow.data(), gpow.size() * sizeof(u64))) return e_;
     const ChaChaKey k = chacha_key(key);
     if (int e = sample_polys(c, KG_UNIFORM, k, stream, gk + Ln, 2 * Ln, 0, 2, (long)num_keys, sigma)) return e;
     if (int e = sample_polys(c, KG_GAUSSIAN, k, stream, gk, 2 * Ln, 1, 2, (long)num_keys, sigma)) return e;
@@ -1781,8 +1833,9 @@ static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u
                       const std::vector<size_t>& kidx, const u64* gks, size_t num_keys, size_t B) {
     if (ks.empty()) return 0;
     const long Ln = (long)c->L * c->n;
-    u64* rot = nullptr;
-    HIP_TRY(hipMalloc((void**)&rot, B * 2 * Ln * sizeof(u64)));
+    Scratch rs;
+    HIP_TRY(rs.alloc(B * 2 * Ln * sizeof(u64), c->stream));
+    u64* rot = rs.as<u64>();
     int rc = 0;
     for (size_t e = 0; e < ks.size() && rc == 0; ++e) {
         rc = exacto_bfv_apply_automorphism_dev(c, src ? src : r, 2, ks[e], gks + kidx[e] * num_keys * 2 * Ln,
@@ -1792,8 +1845,6 @@ static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u
             if (hipGetLastError() != hipSuccess) rc = fail(EXACTO_ERR_HIP, "HIP error: trace add launch");
         }
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipFree(rot));
     return rc;
 }
 
@@ -1856,18 +1907,15 @@ extern "C" int exacto_extract_coefficients_dev(exacto_ctx* c, const uint64_t* ct
     launch_monomials(c->pl_buf, (long)J, j0, true, n, c->L, c->d_primes, c->stream);
     CHECK_LAUNCH();
     if (int e = ntt_items(c, c->pl_buf, (long)J, Ln, c->L)) return e;
-    u64* shifted = out;
-    if (naive) HIP_TRY(hipMalloc((void**)&shifted, J * 2 * Ln * sizeof(u64)));
+    Scratch ss;
+    if (naive) HIP_TRY(ss.alloc(J * 2 * Ln * sizeof(u64), c->stream));
+    u64* shifted = naive ? ss.as<u64>() : out;
     launch_plain_apply(PLAIN_MUL, ct, 0, shifted, (long)J, 2, c->pl_buf, Ln, n, c->L, c->d_primes, c->stream);
     int rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: monomial launch");
     if (rc == 0 && naive)
         rc = hipMemcpyAsync(out, shifted, J * 2 * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream) == hipSuccess
                  ? 0 : fail(EXACTO_ERR_HIP, "HIP error: copy");
     if (rc == 0) rc = trace_core(c, naive ? shifted : nullptr, out, ks, kidx, gks, num_keys, J);
-    if (naive) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        HIP_TRY(hipFree(shifted));
-    }
     if (rc) return rc;
     // times the constant plaintext n^-1: NTT(constant) is that constant in every slot
     return exacto_rns_scalar_mul_dev(c, out, n_inv, out, J * 2);
@@ -2053,8 +2101,9 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
     const size_t groups = (d + k) / k;
     // workspace: baby[0], baby[2..k] (baby[1] is ct), one group accumulator, a Horner ping buffer
     const size_t nbuf = k + 3;
-    u64* ws = nullptr;
-    HIP_TRY(hipMalloc((void**)&ws, nbuf * words * sizeof(u64)));
+    Scratch wss;
+    HIP_TRY(wss.alloc(nbuf * words * sizeof(u64), c->stream));
+    u64* ws = wss.as<u64>();
     std::vector<const u64*> baby(k + 1);
     auto slot = [&](size_t i) { return ws + i * words; };
     baby[0] = slot(0);
@@ -2095,8 +2144,6 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
         }
         std::swap(res, other);
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipFree(ws));
     return rc;
 }
 
@@ -2120,8 +2167,9 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
     if (int e = boot_pair_check(o, b)) return e;
     if (!sk || !boot_sk || !s_pt) return invalid_param("null argument");
     const int n = o->n;
-    u64* tmp = nullptr;
-    HIP_TRY(hipMalloc((void**)&tmp, 2 * n * sizeof(u64)));
+    Scratch ts;
+    HIP_TRY(ts.alloc(2 * n * sizeof(u64), o->stream));
+    u64* tmp = ts.as<u64>();
     HIP_TRY(hipMemcpyAsync(tmp, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream));
     int rc = run_ntt(o, contiguous(tmp, 1, 1, 0, 1, n), 1, true);  // sk.poly.components[0].to_coeff_poly()
     if (rc == 0) {
@@ -2134,8 +2182,9 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
         rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: lift launch");
     }
     if (rc == 0) rc = ntt_items(b, boot_sk, 1, 0, b->L);
-    if (rc == 0) rc = hipStreamSynchronize(b->stream) == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: sync");
-    HIP_TRY(hipFree(tmp));
+    // tmp + n was read on b's stream: both streams drain before the block returns to o's pool
+    const hipError_t sb = hipStreamSynchronize(b->stream), so = hipStreamSynchronize(o->stream);
+    if (rc == 0 && (sb != hipSuccess || so != hipSuccess)) rc = fail(EXACTO_ERR_HIP, "HIP error: sync");
     return rc;
 }
 
@@ -2155,16 +2204,35 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (B == 0) return 0;
     const int n = o->n;
     const long Lbn = (long)b->L * n;
-    // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
-    u64* coef = nullptr;
-    int* flags = nullptr;
-    HIP_TRY(hipMalloc((void**)&coef, 2 * B * 2 * n * sizeof(u64)));
-    HIP_TRY(hipMalloc((void**)&flags, B * sizeof(int)));
-    u64* small = coef + B * 2 * n;
+    // Scratch of the whole call.  A block of o's stream is also read on b's stream (small), so
+    // both streams drain before any block goes back to its pool: `drain` is declared after the
+    // blocks, so its destructor runs first on every return path; the normal path calls finish()
+    // to fold a failed synchronisation (e.g. a kernel fault) into the return code.
+    Scratch coef_s, flags_s, c0pt_s, phase_s, slots_s;
     int rc = 0;
+    struct Drain {
+        exacto_ctx *o, *b;
+        bool done = false;
+        int finish(int code) {
+            done = true;
+            const hipError_t sb = hipStreamSynchronize(b->stream), so = hipStreamSynchronize(o->stream);
+            if (code == 0 && (sb != hipSuccess || so != hipSuccess)) return fail(EXACTO_ERR_HIP, "HIP error: sync");
+            return code;
+        }
+        ~Drain() {
+            if (!done) finish(1);
+        }
+    } drain{o, b};
     auto ok = [&](hipError_t e, const char* what) {
         if (rc == 0 && e != hipSuccess) rc = fail(EXACTO_ERR_HIP, std::string("HIP error: ") + what);
     };
+    // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
+    ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream), "alloc");
+    ok(flags_s.alloc(B * sizeof(int), o->stream), "alloc");
+    if (rc) return rc;
+    u64* coef = coef_s.as<u64>();
+    int* flags = flags_s.as<int>();
+    u64* small = coef + B * 2 * n;
     ok(hipMemcpyAsync(coef, ct, B * 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream), "copy");
     ok(hipMemsetAsync(flags, 0, B * sizeof(int), o->stream), "memset");
     if (rc == 0) rc = exacto_rns_inv_dev(o, coef, B * 2);
@@ -2176,8 +2244,9 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(hipMemcpyAsync(hflags.data(), flags, B * sizeof(int), hipMemcpyDeviceToHost, o->stream), "flags");
     if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
     // 2. phase = TrivialEnc(c0') + bsk * c1' (b), written into out
-    u64* c0pt = nullptr;  // [B][n] copies of c0' and c1' rows in the plaintext layout
-    if (rc == 0) ok(hipMalloc((void**)&c0pt, 2 * B * n * sizeof(u64)), "alloc");
+    // [B][n] copies of c0' and c1' rows in the plaintext layout
+    if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream), "alloc");
+    u64* c0pt = c0pt_s.as<u64>();
     u64* c1pt = c0pt + B * n;
     if (rc == 0) {
         launch_rows(c0pt, n, small, 2 * n, n, (long)B, b->stream);
@@ -2196,9 +2265,10 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         ok(hipGetLastError(), "plain_add launch");
     }
     // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
-    u64 *slots = nullptr, *rounded = nullptr, *phase = nullptr;
     const size_t ctw = 2 * Lbn;
-    if (rc == 0) ok(hipMalloc((void**)&phase, ctw * sizeof(u64)), "alloc");
+    if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream), "alloc");
+    u64* phase = phase_s.as<u64>();
+    u64 *slots = nullptr, *rounded = nullptr;
     for (size_t i = 0; i < B && rc == 0; ++i) {
         u64* oi = out + i * ctw;
         ok(hipMemcpyAsync(phase, oi, ctw * sizeof(u64), hipMemcpyDeviceToDevice, b->stream), "copy");
@@ -2207,18 +2277,17 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
             rc = exacto_eval_poly_dev(b, phase, rpoly, m, oi, 1);
             continue;
         }
-        if (!slots) {
-            ok(hipMalloc((void**)&slots, 2 * (size_t)n * ctw * sizeof(u64)), "alloc");
-            rounded = slots + (size_t)n * ctw;
+        if (!slots) {  // once per call, on the first item that takes the ring path
+            ok(slots_s.alloc(2 * (size_t)n * ctw * sizeof(u64), b->stream), "alloc");
             if (rc) break;
+            slots = slots_s.as<u64>();
+            rounded = slots + (size_t)n * ctw;
         }
         rc = exacto_extract_coefficients_dev(b, phase, 0, n, elements, E, gks, num_keys, slots);
         if (rc == 0) rc = exacto_eval_poly_dev(b, slots, rpoly, m, rounded, n);
         if (rc == 0) rc = exacto_slots_to_coeffs_dev(b, rounded, n, 2, oi);
     }
-    hipStreamSynchronize(b->stream);
-    hipFree(slots); hipFree(phase); hipFree(c0pt); hipFree(coef); hipFree(flags);
-    return rc;
+    return drain.finish(rc);
 }
 
 extern "C" int exacto_bootstrap_key_material(exacto_ctx* o, exacto_ctx* b, const uint64_t* sk, uint64_t* boot_sk,
@@ -2228,12 +2297,13 @@ extern "C" int exacto_bootstrap_key_material(exacto_ctx* o, exacto_ctx* b, const
     const size_t n = o->n;
     u64* d = nullptr;
     HIP_TRY(hipMalloc((void**)&d, (n + b->L * n + n) * sizeof(u64)));
-    int rc = hipMemcpy(d, sk, n * sizeof(u64), hipMemcpyHostToDevice) == hipSuccess ? 0 : EXACTO_ERR_HIP;
+    int rc = upload(o, d, sk, n * sizeof(u64));
     if (rc == 0) rc = exacto_bootstrap_key_material_dev(o, b, d, d + n, d + n + b->L * n);
-    if (rc == 0 && (hipMemcpy(boot_sk, d + n, b->L * n * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess ||
-                    hipMemcpy(s_pt, d + n + b->L * n, n * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess))
+    if (rc == 0 && (hipMemcpyAsync(boot_sk, d + n, b->L * n * sizeof(u64), hipMemcpyDeviceToHost, o->stream) != hipSuccess ||
+                    hipMemcpyAsync(s_pt, d + n + b->L * n, n * sizeof(u64), hipMemcpyDeviceToHost, o->stream) != hipSuccess ||
+                    hipStreamSynchronize(o->stream) != hipSuccess))
         rc = fail(EXACTO_ERR_HIP, "HIP error: copy back");
-    hipFree(d);
+    (void)hipFree(d);
     return rc;
 }
 

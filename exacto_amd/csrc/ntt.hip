@@ -64,6 +64,19 @@ __device__ __forceinline__ void lds_load(const u64* lds, u64 (&x)[16], int tid) 
     for (int k = 0; k < 16; ++k) x[k] = lds[swz(elem_index<LO>(tid, k))];
 }
 
+// Thread index that hipcc cannot prove wave-uniform (used when T < 64).  At n = 16 a polynomial has one thread
+// (T = 1): after `if (tid >= T) return` every address in the kernel is uniform and hipcc loaded the
+// polynomial with s_load_dwordx16, i.e. through the scalar data cache.  When a buffer was reused
+// (the stream-ordered pool hands the same block to the next call), those scalar loads returned the
+// block's previous contents instead of what the preceding kernel had just stored with vector
+// stores: wrong results at n = 16 only, changing from run to run (round-1 ADVICE item).  Keeping
+// the index in a VGPR makes every polynomial access a vector load.
+__device__ __forceinline__ int vtid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // ---------------------------------------------------------------- forward
 
 // Twiddles of one round: stage bit b uses (8 >> (b - LO)) groups; at most 1+2+4+8 = 15 pairs.
@@ -208,7 +221,7 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
+    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
     const int p = blockIdx.x;
     const int item = p / nb.ppi, sub = p - item * nb.ppi;
@@ -668,7 +681,7 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
+    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
     const int p = blockIdx.x;
     const int item = p / nb.ppi, sub = p - item * nb.ppi;
@@ -726,7 +739,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
+    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
     const int NP = L + K;
     const long p = blockIdx.x;
@@ -799,7 +812,7 @@ keyswitch_kernel(KsArgs a, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
+    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     const int L = a.L;
     const long item = blockIdx.x / L;
     const int i = (int)(blockIdx.x - item * L);

@@ -137,9 +137,9 @@ int exacto_bfv_mul_no_relin(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1,
 int exacto_bfv_mul_no_relin_dev(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2,
                                 size_t polys2, uint64_t* out, size_t batch);
 
-/* relinearize (bfv/keyswitch.rs:59-101): ct = [B][polys][L][n] -> out = [B][2][L][n].
- * polys < 3: copied; polys > 3: InvalidParam "relinearization only supports degree-2
- * ciphertexts". */
+/* relinearize (bfv/keyswitch.rs:59-101): ct = [B][3][L][n] -> out = [B][2][L][n].
+ * polys < 3: cloned, out = [B][polys][L][n] (keyswitch.rs:63-65); polys > 3: InvalidParam
+ * "relinearization only supports degree-2 ciphertexts". */
 int exacto_relinearize(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
 int exacto_relinearize_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
 

@@ -151,6 +151,19 @@ def test_degree_errors(gpu_available):
     assert "relinearization only supports degree-2 ciphertexts" in str(e.value)
     ct2 = uniform_residues(rng, (2, 2), prm.ct_basis.moduli, 16)
     assert np.array_equal(ctx.relinearize(ct2), ct2)
+    # keyswitch.rs:63-65 clones a ciphertext of fewer than 3 polys: one-poly items, batched,
+    # keep their own layout ([B][1][L][n]), on the host and the device entry points
+    ct1 = uniform_residues(rng, (3, 1), prm.ct_basis.moduli, 16)
+    assert np.array_equal(ctx.relinearize(ct1), ct1)
+    import torch
+    d_in = torch.from_numpy(ct1.view(np.int64)).cuda()
+    d_out = torch.full((3 + 2, 1, prm.ct_basis.num_moduli(), 16), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # the context's stream does not wait for torch's
+    ctx.relinearize_dev(d_in, 1, d_out, 3)
+    ctx.synchronize()
+    got = d_out.cpu().numpy()
+    assert np.array_equal(got[:3].view(np.uint64), ct1)
+    assert (got[3:] == -1).all()  # nothing written past the B*1*L*n output words
 
 
 def test_missing_key(gpu_available):

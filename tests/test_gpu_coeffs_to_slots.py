@@ -50,6 +50,30 @@ def test_extract_coefficients_match_oracle(gpu_available, which, j0, count):
 
 
 @pytest.mark.parametrize("which", ["small16", "cfg3_n64"])
+def test_batched_after_single_extraction(gpu_available, which):
+    """One context extracts J = 1 and then J = n coefficients, three times over: every result is
+    bit-exact against the oracle.  Regression for the round-1 fault where results changed from
+    call to call once scratch blocks were recycled (the key-switch workspace grows from 1 to n
+    items between the two calls, and the scratch comes from the stream-ordered pool)."""
+    prm = small_test_params() if which == "small16" else P.cfg3_params(64)
+    n, q = prm.ring_degree, prm.ct_basis.moduli
+    ctx = HipContext.from_params(prm)
+    rng = np.random.default_rng(47)
+    elements = ctx.required_trace_elements()
+    gks = uniform_residues(rng, (len(elements), 2, 2), q, n)
+    keys = _oracle_keys(prm, elements, gks)
+    cts = [uniform_residues(rng, (2,), q, n) for _ in range(2)]
+    want = [[ct_to_np(ob.extract_coefficient(np_to_ct(ct, prm), j, keys)) for j in range(n)] for ct in cts]
+    for rep in range(3):
+        for c, ct in enumerate(cts):
+            one = ctx.extract_coefficients(ct, 3, 1, elements, gks)
+            assert np.array_equal(one[0], want[c][3]), (which, rep, c, "J=1")
+            alln = ctx.extract_coefficients(ct, 0, n, elements, gks)
+            for j in range(n):
+                assert np.array_equal(alln[j], want[c][j]), (which, rep, c, j)
+
+
+@pytest.mark.parametrize("which", ["small16", "cfg3_n64"])
 def test_slots_to_coeffs_matches_oracle(gpu_available, which):
     prm = small_test_params() if which == "small16" else P.cfg3_params(64)
     n, q = prm.ring_degree, prm.ct_basis.moduli
