@@ -189,6 +189,7 @@ struct exacto_ctx {
     bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
     bool ntt_pipe = true;   // EXACTO_NTT_PIPE=0: one workgroup per polynomial instead of the persistent LDS-DMA kernel
+    bool ntt_asm_inv = true;  // EXACTO_NTT_ASM_INV=0: compiler-scheduled inverse NTT (A/B)
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
@@ -559,6 +560,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_NTT_ASM_INV")) c->ntt_asm_inv = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
@@ -672,7 +674,8 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
         lazy &= c->primes[t] < (1ull << 60);
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
     }
-    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, c->ntt_pipe);
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, c->ntt_pipe,
+               near60 && c->ntt_asm_inv);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));
@@ -694,9 +697,12 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt) {
         HIP_TRY(hipEventCreate(&rec.b));
         HIP_TRY(hipEventRecord(rec.a, c->stream));
     }
-    bool lazy = true;
-    for (int t = 0; t < NP; ++t) lazy &= c->primes[t] < (1ull << 60);
-    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream);
+    bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
+    for (int t = 0; t < NP; ++t) {
+        lazy &= c->primes[t] < (1ull << 60);
+        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
+    }
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));

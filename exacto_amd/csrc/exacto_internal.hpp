@@ -68,8 +68,10 @@ struct CrtTables {
 // asm_fwd: every prime of the batch is in (2^60 - 2^32, 2^60) and the hand-scheduled forward
 // kernel (ntt_asm.inc) may be used for n = 4096 / 8192
 // pipe: n = 4096 forward transforms run on the persistent LDS-DMA kernel (ntt_fwd_pipe_kernel)
+// asm_inv: same prime window as asm_fwd, inverse transforms at n = 4096 / 8192 run the generated
+// Gentleman-Sande rounds (ntt_inv_asm_kernel)
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd = false, bool pipe = false);
+                hipStream_t s, bool asm_fwd = false, bool pipe = false, bool asm_inv = false);
 
 // Fused relinearisation: see keyswitch_kernel in ntt.hip.
 struct KsArgs {
@@ -107,8 +109,9 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 };
 
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
+// asm_inv: every prime in (2^60 - 2^32, 2^60) and n = 4096 / 8192 (generated inverse rounds)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s);
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);

@@ -714,6 +714,59 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
+// ---------------------------------------------------------------- inverse, hand-scheduled rounds
+
+// n = 4096 / 8192 with every prime of the batch in (2^60 - 2^32, 2^60): the Gentleman-Sande rounds
+// are the generated statements of ntt_asm.inc (InvRoundAsm): bounds tracked per value at
+// generation time (inputs < 4q), special-prime reductions, n^-1 folded into the last stage.  Same
+// convention, twiddle layout and LDS exchanges as inv_rounds.
+template <int LOGN, int R>
+__device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
+    constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
+    constexpr int BLO = 4 * R;
+    constexpr int BHI = (4 * R + 3) < (LOGN - 1) ? 4 * R + 3 : LOGN - 1;
+    TwPair tw[15];
+    load_round_tw_inv<LOGN, LO, BLO, BHI>(tw, tid, tab);  // in flight across the exchange
+    if constexpr (R > 0) {
+        constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
+        int t2 = tid;
+        asm volatile("" : "+v"(t2));
+        lds_barrier();
+        lds_store_x<PLO>(lds, x, t2);
+        lds_barrier();
+        lds_load_x<LO>(lds, x, t2);
+    }
+    InvRoundAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(EXACTO_ASM_WAVES)))
+ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    u64 x[16];
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const ulonglong2 v = s2[k];
+        x[2 * k] = v.x;
+        x[2 * k + 1] = v.y;
+    }
+    const AsmK K = make_asmk_inv(P);
+    inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), K);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
 // ---------------------------------------------------------------- tensor product + inverse
 
 // Degree-2 tensor of two degree-1 ciphertexts fused into the inverse transform of its
@@ -731,8 +784,11 @@ __device__ __forceinline__ u64 barrett_mul_lazy(u64 a, u64 b, const PrimeConst& 
     return lo - qhat * P.q;  // < 3q
 }
 
-template <int LOGN, bool LAZY>
+// ASM (n = 4096 / 8192, every prime in (2^60 - 2^32, 2^60)): the inverse rounds are the generated
+// InvRoundAsm statements (inputs < 4q: products < 3q, c1 < 4q).
+template <int LOGN, bool LAZY, bool ASM = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+__attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
                       const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
@@ -792,7 +848,12 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
             x[k] = LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
         }
     }
-    inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
+    if constexpr (ASM) {
+        const AsmK AK = make_asmk_inv(P);
+        inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
+    } else {
+        inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
+    }
     u64* dst = Tout + p * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
@@ -922,8 +983,15 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
 
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false) {
     constexpr int threads = (1 << LOGN) / 16;
+    if constexpr (LOGN == 12 || LOGN == 13) {
+        if (asm_inv) {
+            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(blocks), dim3(threads), 0, s, op, extP,
+                               T, L, K, primes);
+            return;
+        }
+    }
     if (lazy)
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L, K,
                            primes);
@@ -933,7 +1001,7 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     switch (logn) {
@@ -945,8 +1013,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv); break;
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }
@@ -964,7 +1032,7 @@ static int cu_count() {
 }
 
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd, bool pipe) {
+                hipStream_t s, bool asm_fwd, bool pipe, bool asm_inv) {
     if (count <= 0) return;
     if (asm_fwd && pipe && !inverse && logn == 12) {
         // two resident workgroups per CU; a grid that is a multiple of the prime period keeps
@@ -977,6 +1045,14 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
     }
     if (asm_fwd && !inverse && logn == 12) {
         hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        return;
+    }
+    if (asm_inv && inverse && logn == 12) {
+        hipLaunchKernelGGL((ntt_inv_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        return;
+    }
+    if (asm_inv && inverse && logn == 13) {
+        hipLaunchKernelGGL((ntt_inv_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     if (asm_fwd && !inverse && logn == 13) {

@@ -1,7 +1,8 @@
-"""CPU check of the generated forward-NTT asm rounds (exacto_amd/csrc/ntt_asm.inc): a one-lane
-simulation of every round's instruction sequence against exact modular butterflies, at the
-input bounds the rounds assume (tools/asm_sim.py), and the committed .inc is what the generator
-emits today."""
+"""CPU check of the generated forward / inverse NTT asm rounds (exacto_amd/csrc/ntt_asm.inc): a
+one-lane simulation of every round's instruction sequence against exact modular butterflies
+(Cooley-Tukey forward, Gentleman-Sande inverse with n^-1 folded into the last stage), at the
+input bounds the rounds assume, for the approximate and the exact Shoup quotient
+(tools/asm_sim.py), and the committed .inc is what the generator emits today."""
 
 import os
 import random
@@ -16,12 +17,13 @@ import gen_ntt_asm  # noqa: E402
 
 def test_rounds_match_exact_arithmetic():
     rng = random.Random(7)
-    primes = [1152921504606830593, 1152921504606748673, 1152921504606683137, 1152921504606601217,
-              (1 << 60) - (1 << 32) + 3]
-    for logn in (12, 13):
-        for r in range((logn + 3) // 4):
-            for i in range(25):
-                asm_sim.check_round(logn, r, primes[i % len(primes)], rng)
+    for approx in (True, False):
+        for logn in (12, 13):
+            for r in range((logn + 3) // 4):
+                for i in range(15):
+                    q = asm_sim.PRIMES[i % len(asm_sim.PRIMES)]
+                    asm_sim.check_round(logn, r, q, rng, approx)
+                    asm_sim.check_inv_round(logn, r, q, rng, approx)
 
 
 def test_committed_inc_is_current(tmp_path):

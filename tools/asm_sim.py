@@ -3,7 +3,8 @@
 
 Runs each round's instruction sequence on random inputs at the bounds the round assumes and
 checks the results against exact modular arithmetic: every output is congruent mod q to the
-radix-2 Cooley-Tukey butterflies of the round, below the next round's input bound (16q), and
+radix-2 Cooley-Tukey (forward) or Gentleman-Sande (inverse, n^-1 folded into the last stage)
+butterflies of the round, below the bound the generator declares for the round's outputs, and
 canonical after the final round.  This catches register-reuse and sequencing mistakes before a
 GPU run (it does not model timing or hazards; pad_hazards() handles those).
 
@@ -122,32 +123,59 @@ def shoup(w, q):
     return (w << 64) // q
 
 
-def check_round(logn, r, q, rng):
-    rd = G.Round(logn, r)
-    seq = rd.gen()
-    first = r == 0
-    bound_in = q if first else 16 * q
+def _named(rd, x, tw, q, logn):
+    """Operand values of one statement for a lane holding x[0..15] with twiddles tw[slot]."""
+    n = 1 << logn
+    n_inv = pow(n, -1, q)
+    # psi_inv_rev[1] * n^-1: any constant below q exercises the same instructions
+    last_w = (q - 12345) * n_inv % q
+    K = dict(n0=((1 << 64) - q) & M32, n1=((1 << 64) - q) >> 32, ql=q & M32, qh=q >> 32, nq=(1 << 64) - q,
+             nil=n_inv & M32, nih=n_inv >> 32, nsl=shoup(n_inv, q) & M32, nsh=shoup(n_inv, q) >> 32,
+             lwl=last_w & M32, lwh=last_w >> 32, lsl=shoup(last_w, q) & M32, lsh=shoup(last_w, q) >> 32)
+    named = {}
+    for key, cons, expr in rd.ins:
+        m = re.fullmatch(r"x(\d+)([lh])", key)
+        if m:
+            k = int(m.group(1))
+            named[key] = [(x[k] if m.group(2) == "l" else x[k] >> 32) & M32, 32]
+            continue
+        m = re.fullmatch(r"t(\d+)(w0|w1|s0|s1)", key)
+        if m:
+            slot, part = int(m.group(1)), m.group(2)
+            w = tw[slot]
+            named[key] = [{"w0": w & M32, "w1": w >> 32, "s0": shoup(w, q) & M32,
+                           "s1": shoup(w, q) >> 32}[part], 32]
+            continue
+        m = re.fullmatch(r"mq(\d+)", key)
+        if m:
+            named[key] = [int(m.group(1)) * q, 64]
+            continue
+        m = re.fullmatch(r"q(\d+)([lh])", key)
+        if m:
+            cq = int(m.group(1)) * q
+            named[key] = [(cq if m.group(2) == "l" else cq >> 32) & M32, 32]
+            continue
+        named[key] = [K[key], 64 if key == "nq" else 32]
+    for k in range(16):
+        named[f"x{k}"] = [x[k], 64]
+    return named, n_inv, last_w
+
+
+def _inputs(rng, bound_in):
     x = [rng.randrange(bound_in) for _ in range(16)]
     if rng.random() < 0.3:   # extremes
         x = [bound_in - 1 - rng.randrange(3) for _ in range(16)]
+    return x
+
+
+def check_round(logn, r, q, rng, approx=True):
+    rd = G.Round(logn, r, approx)
+    seq = rd.gen()
+    first = r == 0
+    bound_in = q if first else 16 * q
+    x = _inputs(rng, bound_in)
     tw = [rng.randrange(q) for _ in range(15)]
-    K = dict(n0=((1 << 64) - q) & M32, n1=((1 << 64) - q) >> 32, q2l=(2 * q) & M32, q2h=(2 * q) >> 32,
-             ql=q & M32, qh=q >> 32, nq=(1 << 64) - q)
-    named = {}
-    for key, cons, expr in rd.ins:
-        if key.startswith("x") and key[-1] in "lh":
-            k = int(key[1:-1])
-            named[key] = [(x[k] if key.endswith("l") else x[k] >> 32) & M32, 32]
-        elif key.startswith("t"):
-            m = re.fullmatch(r"t(\d+)(w0|w1|s0|s1)", key)
-            slot, part = int(m.group(1)), m.group(2)
-            w = tw[slot]
-            val = {"w0": w & M32, "w1": w >> 32, "s0": shoup(w, q) & M32, "s1": shoup(w, q) >> 32}[part]
-            named[key] = [val, 32]
-        else:
-            named[key] = [K[key], 64 if key == "nq" else 32]
-    for k in range(16):
-        named[f"x{k}"] = [x[k], 64]
+    named, _, _ = _named(rd, x, tw, q, logn)
     lane = Lane(named)
     for ins in seq:
         lane.run(ins.text)
@@ -163,19 +191,48 @@ def check_round(logn, r, q, rng):
         if rd.last:
             assert got[k] < q, ("not canonical", logn, r, k, got[k])
         else:
-            assert got[k] < 10 * q if r > 0 else got[k] < 9 * q, ("bound", logn, r, k, got[k] / q)
+            assert got[k] < rd.bound_out * q, ("bound", logn, r, k, got[k] / q)
+
+
+def check_inv_round(logn, r, q, rng, approx=True):
+    rd = G.inv_rounds(logn, approx)[r]
+    rd = G.InvRound(logn, r, rd.bound_in, approx)
+    seq = rd.gen()
+    x = _inputs(rng, rd.bound_in * q)
+    tw = [rng.randrange(q) for _ in range(15)]
+    named, n_inv, last_w = _named(rd, x, tw, q, logn)
+    lane = Lane(named)
+    for ins in seq:
+        lane.run(ins.text)
+    got = [named[f"x{k}"][0] for k in range(16)]
+    want = [v % q for v in x]
+    for final, bfs in rd.stages():
+        for k0, k1, slot in bfs:
+            u, w_ = want[k0], want[k1]
+            if final:
+                want[k0], want[k1] = (u + w_) * n_inv % q, (u - w_) * last_w % q
+            else:
+                want[k0], want[k1] = (u + w_) % q, (u - w_) * tw[slot] % q
+    for k in range(16):
+        assert got[k] % q == want[k], ("inv", logn, r, k, got[k], want[k])
+        assert got[k] < rd.bound_out * q, ("inv bound", logn, r, k, got[k] / q, rd.bound_out)
+
+
+PRIMES = [1152921504606830593, 1152921504606748673, 1152921504606683137, 1152921504606601217,
+          (1 << 60) - (1 << 32) + 3]  # the last: d = 2^32 - 3, the edge of the path (primality irrelevant here)
 
 
 def main():
     trials = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     rng = random.Random(1)
-    primes = [1152921504606830593, 1152921504606748673, 1152921504606683137, 1152921504606601217,
-              (1 << 60) - (1 << 32) + 3]  # the last: d = 2^32 - 3, the edge of the path (primality irrelevant here)
-    for logn in (12, 13):
-        for r in range((logn + 3) // 4):
-            for i in range(trials):
-                check_round(logn, r, primes[i % len(primes)], rng)
-    print(f"asm_sim: all rounds of n=4096/8192 agree with exact arithmetic over {trials} trials each")
+    for approx in (True, False):
+        for logn in (12, 13):
+            for r in range((logn + 3) // 4):
+                for i in range(trials):
+                    check_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+                    check_inv_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+    print(f"asm_sim: all forward and inverse rounds of n=4096/8192 (approximate and exact Shoup "
+          f"quotients) agree with exact arithmetic over {trials} trials each")
 
 
 if __name__ == "__main__":

@@ -1,44 +1,53 @@
 #!/usr/bin/env python3
 """Generates exacto_amd/csrc/ntt_asm.inc: hand-scheduled gfx950 inline-asm rounds of the forward
-negacyclic NTT (Cooley-Tukey, Harvey lazy butterflies, Shoup twiddles) for primes q in
+(Cooley-Tukey) and inverse (Gentleman-Sande) negacyclic NTT with Shoup twiddles, for primes q in
 (2^60 - 2^32, 2^60).  Run it after editing; the output is committed.
 
 Why asm: gfx950 has no 64-bit add/sub/compare with carry-out to a VGPR, so every 64-bit
 subtraction and every 65-bit sum is a VALU carry chain through an SGPR pair, and a VALU that
 reads an SGPR written by a VALU needs 2 wait states.  hipcc schedules one butterfly at a time
-and pads each chain with s_nop.  Here W butterflies are interleaved with explicit carry pairs, so
-every carry read has its 2 wait states filled by independent work; pad_hazards() inserts s_nop
-only where a gap remains (and is the safety net for the rule).
+and pads each chain with s_nop (the compiler-scheduled inverse issued 12.9k VALU per 4096-point
+polynomial, the forward below 7.7k).  Here W butterflies are interleaved with explicit carry
+pairs, so every carry read has its 2 wait states filled by independent work; pad_hazards()
+inserts s_nop only where a gap remains (and is the safety net for the rule).
 
 Issue costs measured on MI355X (tools/op_rate.hip, cycles per wave-instruction per SIMD): v_add /
 v_sub / v_and / v_mov / v_lshrrev_b32 ~2.5; every multiply, mad, carry op, 64-bit op, add3,
-cndmask_e64, bfi, alignbit ~4.2-5.  The sequence below is written for that table.
+cndmask_e64, bfi, alignbit ~4.2-5.  The sequences below are written for that table.
 
-Register model: one asm statement per round keeps the 16 values of a thread in physical VGPR
-pairs (clobbered) between stages, with one temp set per butterfly stream.  The values enter and
-leave through "+v" u64 operands tied to x[k]; the first stage also takes the u32 halves of its
-Y operands (and the high halves of the X operands it reduces) as inputs.  Tied operands are
-written only by the round's last stage (or the final reduction), after every input was read.
-Hazard rule (LLVM GCNHazardRecognizer, gfx940+ VALUWriteSGPRVALURead): a VALU reading an SGPR
-written by a VALU (carry-in, cndmask mask) needs 2 wait states after the write.  gfx9 reads at
-most one SGPR (or literal) per VALU instruction, so the carry-in of v_subb takes 2q's high word
-from a VGPR.
-
-Per-butterfly sequence (Y any 64-bit value, X < bound, T = Shoup(Y, w) in [0, 2q)), 15 slow +
-2 fast instructions (the previous generator: 18 slow + 1 fast):
-  qh = hi64(Y * ws) exact:  Z = mulhi(y0,s0); A = y1*s0 + Z; B = y0*s1 + A with the carry-out of
-       v_mad_u64_u32 in an SGPR pair; D = (B.hi, carry) by v_mov + v_cndmask; qh = y1*s1 + D
+Shoup product T = Y*w mod q for any Y < 2^64 (w < q, ws = floor(w * 2^64 / q)), 10 or 11 slow +
+2 fast instructions:
+  qh = hi64(Y * ws):  A = y1*s0 + Z with Z = mulhi(y0,s0) (exact) or Z = 0 (APPROX); B = y0*s1 + A
+       with the carry-out of v_mad_u64_u32 in an SGPR pair; D = (B.hi, carry) by v_mov + v_cndmask;
+       qh = y1*s1 + D.  Dropping the low-low partial product lowers qh by at most 1, so T grows
+       from [0, 2q) to [0, 3q): one multiply less per butterfly for a wider bound.
   T  = lo64(Y*w + qh*(2^64-q)):  E = y0*w0; E += qh0*n0 (two mads); the high-word cross terms
        y0*w1 + y1*w0 + qh0*n1 + qh1*n0 as one mul_lo + three mads on a 32-bit chain (the high
-       word of a mad's 64-bit addend never reaches the low word of its result); T.hi += chain
-  out0 = X + T, out1 = X + (2q - T)        (v_lshl_add_u64, sub_co/subb)
+       word of a mad's 64-bit addend never reaches the low word of its result); T.hi += chain.
+Forward butterfly (X < bound, Y anything): out0 = X + T, out1 = X + (cq - T), c = 2 or 3.
+Inverse butterfly (U, V with bounds mu + mv <= 16): D = U + (mv*q - V) (sub_co/subb + one 64-bit
+add), U' = U + V, V' = T = Shoup(D, w).  Bounds are tracked per value at generation time; a value
+that would push a sum past 16q is first reduced.
 Reduction of a value x < 2^64 for q = 2^60 - d, d < 2^32 (so 2^64 - q = (0xF0000000, d)):
   t = x.hi >> 28; r = x + t*(2^64 - q) = x - t*q, by one mad (low word d) and a subtraction of
   t << 28 from the high word; r = (x mod 2^60) + t*d < 2q.
-Round-start reduction (rounds >= 1): only the 8 values that are X of the round's first stage are
-reduced (< 2q; a Shoup input may be anything below 2^64, and both butterfly outputs are bounded
-by X's bound + 2q per stage), so the round ends below 10q < 16q.
-Final round: the reduction above, then r - q, selected by the sign of r - q (and-mask + add).
+Forward round-start reduction (rounds >= 1): only the 8 values that are X of the round's first
+stage are reduced (< 2q; a Shoup input may be anything below 2^64, and both butterfly outputs are
+bounded by X's bound + cq per stage), so the round ends below 2q + 4cq <= 14q < 16q.
+Final forward round: the reduction above, then r - q, selected by the sign of r - q (and-mask + add).
+Final inverse stage: n^-1 folded in (x0 = (U+V)*n^-1, x1 = D*psi_inv_rev[1]*n^-1), exact Shoup,
+then the same canonical reduction.
+
+Register model: one asm statement per round.  The 16 values enter and leave through "+v" u64
+operands tied to x[k]; the first stage also takes u32 halves of its inputs.  Tied operands are
+written only once every input of the round has been read (the round's last stage, or the final
+reduction).  Forward: values live in fixed VGPR pairs between stages, one temp set per butterfly
+stream.  Inverse: values and temps share one pool of VGPR pairs with renaming (the sum overwrites
+U's pair, the Shoup result's temp pair becomes V's home and V's old pair becomes the next temp).
+Hazard rule (LLVM GCNHazardRecognizer, gfx940+ VALUWriteSGPRVALURead): a VALU reading an SGPR
+written by a VALU (carry-in, cndmask mask) needs 2 wait states after the write.  gfx9 reads at
+most one SGPR (or literal) per VALU instruction, so carry-in instructions take their other
+constant operand (2q, 3q, m*q high words) from a VGPR.
 """
 
 import os
@@ -50,6 +59,7 @@ VBASE = int(os.environ.get("EXACTO_ASM_VBASE", "104"))   # first physical VGPR o
 W = int(os.environ.get("EXACTO_ASM_STREAMS", "2"))       # butterflies interleaved per group
 SGPR_C = [80, 82, 84, 88, 90, 92][:max(W, 2)]            # carry pair of each stream
 SGPR_SD = 86                  # sink for the carry-out of v_mad_u64_u32 where it is not used
+INV_BOUND_IN = 4              # inverse round 0 input bound (the fused tensor's c1 < 4q)
 
 
 def v(i):
@@ -62,6 +72,15 @@ def vp(i):
 
 def sp(i):
     return f"s[{i}:{i + 1}]"
+
+
+def lo(pair):
+    """Low VGPR of a pair operand 'v[a:b]'."""
+    return "v" + pair[2:pair.index(":")]
+
+
+def hi(pair):
+    return "v" + pair[pair.index(":") + 1:-1]
 
 
 class Ins:
@@ -105,15 +124,10 @@ def pad_hazards(seq):
     return out
 
 
-class Round:
-    """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
+class Statement:
+    """Operand bookkeeping of one asm statement."""
 
-    def __init__(self, logn, r):
-        self.logn, self.r = logn, r
-        self.lo = max(logn - 4 * (r + 1), 0)
-        self.bhi = logn - 1 - 4 * r
-        self.last = self.lo == 0
-        self.uniform_tw = self.lo + 4 >= logn     # thigh == 0: twiddles are block-uniform (SGPR)
+    def __init__(self):
         self.ins = []                            # (name, constraint, expr)
         self.seen = set()
 
@@ -125,14 +139,105 @@ class Round:
 
     def n0(self): return self._in("n0", "s", "K.n0")
     def n1(self): return self._in("n1", "s", "K.n1")
-    def q2l(self): return self._in("q2l", "s", "K.q2l")
-    def q2h(self): return self._in("q2h", "v", "K.q2h")
     def ql(self): return self._in("ql", "s", "K.ql")
     def qh(self): return self._in("qh", "s", "K.qh")
     def nq(self): return self._in("nq", "s", "K.nq")
 
+    def mq(self, m): return self._in(f"mq{m}", "s", f"K.q * {m}u")
+    def cql(self, c): return self._in(f"q{c}l", "s", f"(uint32_t)(K.q * {c}u)")
+    def cqh(self, c): return self._in(f"q{c}h", "v", f"(uint32_t)((K.q * {c}u) >> 32)")
+
     def xh(self, k): return self._in(f"x{k}h", "v", f"(uint32_t)(x[{k}] >> 32)")
     def xl(self, k): return self._in(f"x{k}l", "v", f"(uint32_t)x[{k}]")
+
+
+def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True):
+    """Instructions computing T['E'] = Shoup(Y, w) (in [0, 2q) exact, [0, 3q) approx).
+    T: temp pairs Z (Z.hi == 0, exact only), A, B, E, F; c: this stream's carry SGPR pair.
+    fixup=False leaves out the last instruction (E.hi += F.lo) for the caller to place: E.lo is
+    final before it."""
+    SD = sp(SGPR_SD)
+    Z, A, B, E, F = (T.get(n) for n in "ZABEF")
+    seq = []
+    if approx:
+        seq.append(Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s0}, 0", wr=[SD]))
+    else:
+        seq.append(Ins(f"v_mul_hi_u32 {lo(Z)}, {yl}, {s0}"))
+        seq.append(Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s0}, {Z}", wr=[SD]))
+    seq += [
+        Ins(f"v_mad_u64_u32 {B}, {c}, {yl}, {s1}, {A}", wr=[c]),
+        Ins(f"v_mad_u64_u32 {E}, {SD}, {yl}, {w0}, 0", wr=[SD]),
+        Ins(f"v_mov_b32 {lo(A)}, {hi(B)}"),
+        Ins(f"v_mul_lo_u32 {lo(F)}, {yl}, {w1}"),
+        Ins(f"v_cndmask_b32_e64 {hi(A)}, 0, 1, {c}", rd=[c]),
+        Ins(f"v_mad_u64_u32 {F}, {SD}, {yh}, {w0}, {F}", wr=[SD]),
+        Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s1}, {A}", wr=[SD]),
+        Ins(f"v_mad_u64_u32 {E}, {SD}, {lo(A)}, {st.n0()}, {E}", wr=[SD]),
+        Ins(f"v_mad_u64_u32 {F}, {SD}, {lo(A)}, {st.n1()}, {F}", wr=[SD]),
+        Ins(f"v_mad_u64_u32 {F}, {SD}, {hi(A)}, {st.n0()}, {F}", wr=[SD]),
+    ]
+    if fixup:
+        seq.append(fix_seq(E, F))
+    return seq
+
+
+def fix_seq(E, F):
+    return Ins(f"v_add_u32 {hi(E)}, {hi(E)}, {lo(F)}")
+
+
+def reduce_seq(st, dst, src, src_hi, t, u):
+    """dst (pair) = src - floor(src / 2^60) * q  in [0, 2q).  t, u: temp VGPRs (32-bit names)."""
+    return [
+        Ins(f"v_lshrrev_b32 {t}, 28, {src_hi}"),
+        Ins(f"v_mad_u64_u32 {dst}, {sp(SGPR_SD)}, {t}, {st.n0()}, {src}", wr=[sp(SGPR_SD)]),
+        Ins(f"v_lshlrev_b32 {u}, 28, {t}"),
+        Ins(f"v_sub_u32 {hi(dst)}, {hi(dst)}, {u}"),
+    ]
+
+
+def canon_seq(st, dst, r, S, M):
+    """dst = r mod q for r < 2q: s = r - q, out = s + (q & sign(s)).  S, M: temp pairs."""
+    return [
+        Ins(f"v_lshl_add_u64 {S}, {r}, 0, {st.nq()}"),
+        Ins(f"v_ashrrev_i32 {lo(M)}, 31, {hi(S)}"),
+        Ins(f"v_and_b32 {hi(M)}, {st.qh()}, {lo(M)}"),
+        Ins(f"v_and_b32 {lo(M)}, {st.ql()}, {lo(M)}"),
+        Ins(f"v_lshl_add_u64 {dst}, {S}, 0, {M}"),
+    ]
+
+
+def emit_statement(struct, st, seq, vmax, comment, run_args):
+    seq = pad_hazards(seq)
+    body = "\\n\\t".join(i.text for i in seq)
+    clob = [f'"v{i}"' for i in range(VBASE, vmax)]
+    clob += [f'"s{i}"' for p in SGPR_C + [SGPR_SD] for i in (p, p + 1)]
+    clob.append('"memory"')   # keeps the next round's twiddle loads below the statement
+    outs = ", ".join(f'[x{k}] "+v"(x[{k}])' for k in range(16))
+    ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in st.ins)
+    nops = sum(1 for i in seq if i.text.startswith("s_nop"))
+    valu = sum(1 for i in seq if i.valu)
+    return (f"// {comment}, {valu} VALU, {nops} s_nop\n"
+            f"template <> struct {struct} {{\n"
+            f"    static __device__ __forceinline__ void run({run_args}) {{\n"
+            f"        asm volatile(\"{body}\"\n            : {outs}\n            : {ins}\n"
+            f"            : {', '.join(clob)});\n    }}\n}};\n")
+
+
+class Round(Statement):
+    """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
+
+    def __init__(self, logn, r, approx=True):
+        super().__init__()
+        self.logn, self.r, self.approx = logn, r, approx
+        self.c = 3 if approx else 2            # Shoup output bound (units of q)
+        self.lo = max(logn - 4 * (r + 1), 0)
+        self.bhi = logn - 1 - 4 * r
+        self.last = self.lo == 0
+        self.uniform_tw = self.lo + 4 >= logn     # thigh == 0: twiddles are block-uniform (SGPR)
+        nst = self.bhi - self.lo + 1
+        # bound of the round's outputs (units of q): X < 1 (round 0, canonical input) or < 2
+        # (reduced at round start), plus c per stage
+        self.bound_out = 1 if self.last else (1 if r == 0 else 2) + self.c * nst
 
     def tw(self, slot, part):
         c = "s" if self.uniform_tw else "v"
@@ -154,27 +259,18 @@ class Round:
             res.append((lb, bfs))
         return res
 
-    def reduce(self, dst, src_pair, src_hi, t, u):
-        """dst (pair) = src - floor(src / 2^60) * q  in [0, 2q).  t, u: temp VGPRs."""
-        return [
-            Ins(f"v_lshrrev_b32 {v(t)}, 28, {src_hi}"),
-            Ins(f"v_mad_u64_u32 {vp(dst)}, {sp(SGPR_SD)}, {v(t)}, {self.n0()}, {src_pair}", wr=[sp(SGPR_SD)]),
-            Ins(f"v_lshlrev_b32 {v(u)}, 28, {v(t)}"),
-            Ins(f"v_sub_u32 {v(dst + 1)}, {v(dst + 1)}, {v(u)}"),
-        ]
-
     def gen(self):
         P = [VBASE + 2 * k for k in range(16)]
         TB = VBASE + 32
-        # 10 VGPRs per stream: Z (Z.hi stays 0), A (= D = qh), B (then 2q - T), E (T), F (cross chain)
+        # 10 VGPRs per stream: Z (Z.hi stays 0), A (= D = qh), B (then cq - T), E (T), F (cross chain)
         temps = [dict(Z=TB + 10 * j, A=TB + 10 * j + 2, B=TB + 10 * j + 4, E=TB + 10 * j + 6,
                       F=TB + 10 * j + 8) for j in range(max(W, 2))]
         self.vmax = TB + 10 * len(temps)
         C = SGPR_C
-        SD = sp(SGPR_SD)
         seq = [Ins("s_nop 1", valu=False)]      # an "s" operand may come straight from a VALU
-        for t in temps:
-            seq.append(Ins(f"v_mov_b32 {v(t['Z'] + 1)}, 0"))
+        if not self.approx:
+            for t in temps:
+                seq.append(Ins(f"v_mov_b32 {v(t['Z'] + 1)}, 0"))
 
         st = self.stages()
         nstage = len(st)
@@ -190,7 +286,7 @@ class Round:
             for i, k in enumerate(red):
                 j = i % len(temps)
                 t = temps[j]
-                streams[j] += self.reduce(P[k], xop[k], self.xh(k), t["B"], t["B"] + 1)
+                streams[j] += reduce_seq(self, vp(P[k]), xop[k], self.xh(k), v(t["B"]), v(t["B"] + 1))
                 in_p[k] = True
             seq += interleave(streams)
 
@@ -201,103 +297,282 @@ class Round:
                 for j, (k0, k1, slot) in enumerate(bfs[pi:pi + W]):
                     t = temps[j]
                     c = sp(C[j])
-                    Z, A, B, E, F = (t[n] for n in "ZABEF")
+                    T = {n: vp(t[n]) for n in "ZABEF"}
                     if in_p[k1]:
                         yl, yh = v(P[k1]), v(P[k1] + 1)
                     else:
                         yl, yh = self.xl(k1), self.xh(k1)
                     X = vp(P[k0]) if in_p[k0] else xop[k0]
-                    w0, w1 = self.tw(slot, "w0"), self.tw(slot, "w1")
-                    s0, s1 = self.tw(slot, "s0"), self.tw(slot, "s1")
                     o0, o1 = (xop[k0], xop[k1]) if direct_out else (vp(P[k0]), vp(P[k1]))
-                    streams.append([
-                        Ins(f"v_mul_hi_u32 {v(Z)}, {yl}, {s0}"),
-                        Ins(f"v_mad_u64_u32 {vp(A)}, {SD}, {yh}, {s0}, {vp(Z)}", wr=[SD]),
-                        Ins(f"v_mad_u64_u32 {vp(B)}, {c}, {yl}, {s1}, {vp(A)}", wr=[c]),
-                        Ins(f"v_mad_u64_u32 {vp(E)}, {SD}, {yl}, {w0}, 0", wr=[SD]),
-                        Ins(f"v_mov_b32 {v(A)}, {v(B + 1)}"),
-                        Ins(f"v_mul_lo_u32 {v(F)}, {yl}, {w1}"),
-                        Ins(f"v_cndmask_b32_e64 {v(A + 1)}, 0, 1, {c}", rd=[c]),
-                        Ins(f"v_mad_u64_u32 {vp(F)}, {SD}, {yh}, {w0}, {vp(F)}", wr=[SD]),
-                        Ins(f"v_mad_u64_u32 {vp(A)}, {SD}, {yh}, {s1}, {vp(A)}", wr=[SD]),
-                        Ins(f"v_mad_u64_u32 {vp(E)}, {SD}, {v(A)}, {self.n0()}, {vp(E)}", wr=[SD]),
-                        Ins(f"v_mad_u64_u32 {vp(F)}, {SD}, {v(A)}, {self.n1()}, {vp(F)}", wr=[SD]),
-                        Ins(f"v_mad_u64_u32 {vp(F)}, {SD}, {v(A + 1)}, {self.n0()}, {vp(F)}", wr=[SD]),
-                        Ins(f"v_sub_co_u32_e64 {v(B)}, {c}, {self.q2l()}, {v(E)}", wr=[c]),
-                        Ins(f"v_add_u32 {v(E + 1)}, {v(E + 1)}, {v(F)}"),
-                        Ins(f"v_subb_co_u32_e64 {v(B + 1)}, {c}, {self.q2h()}, {v(E + 1)}, {c}", rd=[c], wr=[c]),
+                    s = shoup_seq(self, yl, yh, self.tw(slot, "w0"), self.tw(slot, "w1"),
+                                  self.tw(slot, "s0"), self.tw(slot, "s1"), T, c, self.approx, fixup=False)
+                    s += [
+                        # cq - T: the low word first, the E.hi fix-up fills the carry's wait states
+                        Ins(f"v_sub_co_u32_e64 {v(t['B'])}, {c}, {self.cql(self.c)}, {v(t['E'])}", wr=[c]),
+                        fix_seq(T["E"], T["F"]),
+                        Ins(f"v_subb_co_u32_e64 {v(t['B'] + 1)}, {c}, {self.cqh(self.c)}, {v(t['E'] + 1)}, {c}",
+                            rd=[c], wr=[c]),
                         # o1 first: o0 may be X's own register pair
-                        Ins(f"v_lshl_add_u64 {o1}, {vp(B)}, 0, {X}"),
-                        Ins(f"v_lshl_add_u64 {o0}, {vp(E)}, 0, {X}"),
-                    ])
+                        Ins(f"v_lshl_add_u64 {o1}, {T['B']}, 0, {X}"),
+                        Ins(f"v_lshl_add_u64 {o0}, {T['E']}, 0, {X}"),
+                    ]
+                    streams.append(s)
                     if not direct_out:
                         in_p[k0] = in_p[k1] = True
                 seq += interleave(streams)
 
         if self.last:
-            # canonical reduction of all 16 values (< 16q) into the tied operands:
-            # r = x - floor(x/2^60)*q in [0, 2q); s = r - q; out = s + (q & sign(s))
+            # canonical reduction of all 16 values (< 16q) into the tied operands
             streams = [[] for _ in range(len(temps))]
             for k in range(16):
                 j = k % len(temps)
                 t = temps[j]
-                R, S, M = P[k], t["E"], t["F"]
-                streams[j] += self.reduce(R, vp(R), v(R + 1), t["B"], t["B"] + 1) + [
-                    Ins(f"v_lshl_add_u64 {vp(S)}, {vp(R)}, 0, {self.nq()}"),
-                    Ins(f"v_ashrrev_i32 {v(M)}, 31, {v(S + 1)}"),
-                    Ins(f"v_and_b32 {v(M + 1)}, {self.qh()}, {v(M)}"),
-                    Ins(f"v_and_b32 {v(M)}, {self.ql()}, {v(M)}"),
-                    Ins(f"v_lshl_add_u64 {xop[k]}, {vp(S)}, 0, {vp(M)}"),
-                ]
+                R = vp(P[k])
+                streams[j] += reduce_seq(self, R, R, v(P[k] + 1), v(t["B"]), v(t["B"] + 1))
+                streams[j] += canon_seq(self, xop[k], R, vp(t["E"]), vp(t["F"]))
             seq += interleave(streams)
-
-        return pad_hazards(seq)
+        return seq
 
     def emit(self):
         seq = self.gen()
-        body = "\\n\\t".join(i.text for i in seq)
-        clob = [f'"v{i}"' for i in range(VBASE, self.vmax)]
-        clob += [f'"s{i}"' for p in SGPR_C + [SGPR_SD] for i in (p, p + 1)]
-        clob.append('"memory"')   # keeps the next round's twiddle loads below the statement
-        outs = ", ".join(f'[x{k}] "+v"(x[{k}])' for k in range(16))
-        ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in self.ins)
-        nops = sum(1 for i in seq if i.text.startswith("s_nop"))
-        valu = sum(1 for i in seq if i.valu)
-        return (f"// round {self.r} of the {1 << self.logn}-point forward NTT: stage bits {self.bhi}..{self.lo}, "
-                f"{valu} VALU, {nops} s_nop\n"
-                f"template <> struct FwdRoundAsm<{self.logn}, {self.r}> {{\n"
-                f"    static __device__ __forceinline__ void run(u64 (&x)[16], const TwPair (&tw)[15], "
-                f"const AsmK& K) {{\n"
-                f"        asm volatile(\"{body}\"\n            : {outs}\n            : {ins}\n"
-                f"            : {', '.join(clob)});\n    }}\n}};\n")
+        return emit_statement(f"FwdRoundAsm<{self.logn}, {self.r}>", self, seq, self.vmax,
+                              f"round {self.r} of the {1 << self.logn}-point forward NTT: stage bits "
+                              f"{self.bhi}..{self.lo}",
+                              "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
+
+
+class InvRound(Statement):
+    """One inverse round (Gentleman-Sande, stage bits BLO..BHI ascending) as one asm statement.
+    bound_in: every input value < bound_in * q."""
+
+    def __init__(self, logn, r, bound_in, approx=True):
+        super().__init__()
+        self.logn, self.r, self.approx = logn, r, approx
+        self.tb = 3 if approx else 2             # Shoup output bound (units of q)
+        self.lo = min(4 * r, logn - 4)
+        self.blo = 4 * r
+        self.bhi = min(4 * r + 3, logn - 1)
+        self.last = self.bhi == logn - 1
+        self.uniform_tw = self.lo + 4 >= logn
+        self.bound_in = bound_in
+        self.bound_out = None
+
+    def tw(self, slot, part):
+        c = "s" if self.uniform_tw else "v"
+        expr = {"w0": f"(uint32_t)tw[{slot}].w", "w1": f"(uint32_t)(tw[{slot}].w >> 32)",
+                "s0": f"(uint32_t)tw[{slot}].ws", "s1": f"(uint32_t)(tw[{slot}].ws >> 32)"}[part]
+        return self._in(f"t{slot}{part}", c, expr)
+
+    def kc(self, name):
+        """Final-stage constants (n^-1 and psi_inv_rev[1] * n^-1, Shoup form), block-uniform."""
+        return self._in(name, "s", "K." + name)
+
+    def stages(self):
+        res, slot = [], 0
+        for b in range(self.blo, self.bhi + 1):
+            lb = b - self.lo
+            half = 1 << lb
+            bfs = []
+            for g in range(8 >> lb):
+                for m in range(half):
+                    k0 = g * 2 * half + m
+                    bfs.append((k0, k0 + half, None if b == self.logn - 1 else slot + g))
+            if b != self.logn - 1:
+                slot += 8 >> lb
+            res.append((b == self.logn - 1, bfs))
+        return res
+
+    def gen(self):
+        # pool of VGPR pairs: 16 value homes (values enter in the tied x operands), plus per
+        # stream A, B, F, D (and Z when exact) fixed temps and a rotating E
+        nfixed = 4 if self.approx else 5
+        npairs = 16 + max(W, 2) * (nfixed + 1) + max(W, 2)
+        pool = [VBASE + 2 * i for i in range(npairs)]
+        self.vmax = VBASE + 2 * npairs
+        free = list(pool)
+
+        def alloc():
+            return vp(free.pop(0))
+
+        temps = []
+        seq = [Ins("s_nop 1", valu=False)]
+        for j in range(max(W, 2)):
+            t = {n: alloc() for n in ("ABFD" if self.approx else "ZABFD")}
+            t["E"] = alloc()
+            temps.append(t)
+            if not self.approx:
+                seq.append(Ins(f"v_mov_b32 {hi(t['Z'])}, 0"))
+        loc = {k: None for k in range(16)}      # None: still in the tied operand x[k]
+        bnd = {k: self.bound_in for k in range(16)}
+        st = self.stages()
+        nstage = len(st)
+        C = SGPR_C
+
+        def val64(k):
+            return f"%[x{k}]" if loc[k] is None else loc[k]
+
+        def halves(k):
+            if loc[k] is None:
+                return self.xl(k), self.xh(k)
+            return lo(loc[k]), hi(loc[k])
+
+        for si, (final, bfs) in enumerate(st):
+            direct = si == nstage - 1        # outputs into the tied operands
+            for pi in range(0, len(bfs), W):
+                streams = []
+                # pairs released by this batch's butterflies become allocatable only after the
+                # batch: its streams are interleaved, so a pair one stream frees may still be read
+                # by that stream after the other stream's instruction that would reuse it
+                released = []
+                for j, (k0, k1, slot) in enumerate(bfs[pi:pi + W]):
+                    t = temps[j]
+                    c = sp(C[j])
+                    s = []
+                    # keep the pair sum and the difference below 16q
+                    for _ in range(2):
+                        if bnd[k0] + bnd[k1] <= 16:
+                            break
+                        kr = k0 if bnd[k0] >= bnd[k1] else k1
+                        if loc[kr] is None:
+                            dst = alloc()
+                            s += reduce_seq(self, dst, val64(kr), self.xh(kr), lo(t["B"]), hi(t["B"]))
+                            loc[kr] = dst
+                        else:
+                            s += reduce_seq(self, loc[kr], loc[kr], hi(loc[kr]), lo(t["B"]), hi(t["B"]))
+                        bnd[kr] = 2
+                    m = bnd[k1]
+                    vl, vh = halves(k1)
+                    U, V = val64(k0), val64(k1)
+                    D = t["D"]
+                    # D = (U + m q) - V: the sum U + V goes between the two halves of the
+                    # subtraction (U's last read is the first add; V.hi is read after the sum)
+                    if final:
+                        s0 = loc[k0] if loc[k0] is not None else alloc()
+                    elif direct:
+                        s0 = f"%[x{k0}]"
+                    elif loc[k0] is None:
+                        s0 = alloc()
+                    else:
+                        s0 = loc[k0]
+                    s += [
+                        Ins(f"v_lshl_add_u64 {D}, {U}, 0, {self.mq(m)}"),
+                        Ins(f"v_sub_co_u32_e64 {lo(D)}, {c}, {lo(D)}, {vl}", wr=[c]),
+                        Ins(f"v_lshl_add_u64 {s0}, {U}, 0, {V}"),
+                        Ins(f"v_subb_co_u32_e64 {hi(D)}, {c}, {hi(D)}, {vh}, {c}", rd=[c], wr=[c]),
+                    ]
+                    if not final:
+                        s += shoup_seq(self, lo(D), hi(D), self.tw(slot, "w0"), self.tw(slot, "w1"),
+                                       self.tw(slot, "s0"), self.tw(slot, "s1"), t, c, self.approx)
+                        old_v = loc[k1]
+                        if direct:
+                            s.append(Ins(f"v_lshl_add_u64 %[x{k1}], {t['E']}, 0, 0"))
+                            released += [p for p in (loc[k0], old_v) if p is not None]
+                            loc[k0] = loc[k1] = None
+                        else:
+                            loc[k0] = s0
+                            loc[k1] = t["E"]                     # rename: E is V's new home
+                            t["E"] = old_v if old_v is not None else alloc()
+                        bnd[k0] = bnd[k0] + bnd[k1]
+                        bnd[k1] = self.tb
+                    else:
+                        # last stage: x0 = (U+V) n^-1, x1 = D psi_inv_rev[1] n^-1, canonical; two
+                        # exact Shoup products through the same temps, S in a spare pair
+                        S = s0
+                        ex = dict(t)
+                        if self.approx:   # exact Shoup here: B doubles as Z (B.hi = 0 first)
+                            ex["Z"] = t["B"]
+                        for dst, y, w in ((f"%[x{k1}]", D, "l"), (f"%[x{k0}]", S, "n")):
+                            if self.approx:
+                                s.append(Ins(f"v_mov_b32 {hi(t['B'])}, 0"))
+                            wn, sn = ("lw", "ls") if w == "l" else ("ni", "ns")
+                            s += shoup_seq(self, lo(y), hi(y), self.kc(wn + "l"), self.kc(wn + "h"),
+                                           self.kc(sn + "l"), self.kc(sn + "h"), ex, c, False)
+                            s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
+                        released += [p for p in {S, loc[k1]} if p is not None]
+                        loc[k0] = loc[k1] = None
+                        bnd[k0] = bnd[k1] = 1
+                    streams.append(s)
+                seq += interleave(streams)
+                free.extend(int(lo(p)[1:]) for p in released)
+        assert all(loc[k] is None for k in range(16))
+        self.bound_out = max(bnd.values())
+        return seq
+
+    def emit(self):
+        seq = self.gen()
+        return emit_statement(f"InvRoundAsm<{self.logn}, {self.r}>", self, seq, self.vmax,
+                              f"round {self.r} of the {1 << self.logn}-point inverse NTT: stage bits "
+                              f"{self.blo}..{self.bhi}, inputs < {self.bound_in}q, outputs < "
+                              f"{self.bound_out}q",
+                              "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
+
+
+def inv_rounds(logn, approx=True):
+    """The inverse rounds of one transform, each starting at the previous round's output bound."""
+    out, b = [], INV_BOUND_IN
+    for r in range((logn + 3) // 4):
+        rd = InvRound(logn, r, b, approx)
+        rd.gen()
+        out.append(rd)
+        b = rd.bound_out
+    return out
+
+
+HEADER = """// GENERATED by tools/gen_ntt_asm.py -- do not edit.
+// Hand-scheduled forward / inverse NTT rounds for primes in (2^60 - 2^32, 2^60); see the
+// generator's docstring.  Included inside namespace exacto by ntt.hip.
+#pragma once
+
+#ifndef EXACTO_ASM_APPROX
+#define EXACTO_ASM_APPROX 1   // Shoup quotient without the low-low partial product (T < 3q)
+#endif
+
+struct AsmK {
+    uint32_t n0, n1;      // 2^64 - q (n1 = 0xF0000000 for the primes of this path)
+    uint32_t ql, qh;      // q
+    u64 q, nq;            // q, 2^64 - q
+    // inverse last stage: n^-1 and psi_inv_rev[1] * n^-1 with their Shoup companions
+    uint32_t nil, nih, nsl, nsh, lwl, lwh, lsl, lsh;
+};
+
+__device__ __forceinline__ AsmK make_asmk(u64 q) {
+    AsmK K{};
+    const u64 nq = (u64)0 - q;
+    K.n0 = (uint32_t)nq; K.n1 = (uint32_t)(nq >> 32);
+    K.ql = (uint32_t)q; K.qh = (uint32_t)(q >> 32);
+    K.q = q; K.nq = nq;
+    return K;
+}
+
+__device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
+    AsmK K = make_asmk(P.q);
+    K.nil = (uint32_t)P.n_inv; K.nih = (uint32_t)(P.n_inv >> 32);
+    K.nsl = (uint32_t)P.n_inv_s; K.nsh = (uint32_t)(P.n_inv_s >> 32);
+    K.lwl = (uint32_t)P.last_w; K.lwh = (uint32_t)(P.last_w >> 32);
+    K.lsl = (uint32_t)P.last_ws; K.lsh = (uint32_t)(P.last_ws >> 32);
+    return K;
+}
+
+template <int LOGN, int R> struct FwdRoundAsm;
+template <int LOGN, int R> struct InvRoundAsm;
+
+"""
 
 
 def main():
-    parts = ["// GENERATED by tools/gen_ntt_asm.py -- do not edit.\n"
-             "// Hand-scheduled forward NTT rounds for primes in (2^60 - 2^32, 2^60); see the generator's docstring.\n"
-             "// Included inside namespace exacto by ntt.hip.\n#pragma once\n\n"
-             "struct AsmK {\n"
-             "    uint32_t n0, n1;      // 2^64 - q (n1 = 0xF0000000 for the primes of this path)\n"
-             "    uint32_t q2l, q2h;    // 2q\n"
-             "    uint32_t ql, qh;      // q\n"
-             "    u64 nq;               // 2^64 - q\n"
-             "};\n\n"
-             "__device__ __forceinline__ AsmK make_asmk(u64 q) {\n"
-             "    AsmK K;\n"
-             "    const u64 nq = (u64)0 - q, q2 = 2 * q;\n"
-             "    K.n0 = (uint32_t)nq; K.n1 = (uint32_t)(nq >> 32);\n"
-             "    K.q2l = (uint32_t)q2; K.q2h = (uint32_t)(q2 >> 32);\n"
-             "    K.ql = (uint32_t)q; K.qh = (uint32_t)(q >> 32);\n"
-             "    K.nq = nq;\n"
-             "    return K;\n"
-             "}\n\n"
-             "template <int LOGN, int R> struct FwdRoundAsm;\n\n"]
-    for logn in (12, 13):
-        for r in range((logn + 3) // 4):
-            parts.append(Round(logn, r).emit())
-            parts.append("\n")
+    parts = [HEADER]
+    for approx in (True, False):
+        parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
+        for logn in (12, 13):
+            for r in range((logn + 3) // 4):
+                parts.append(Round(logn, r, approx).emit())
+                parts.append("\n")
+            for rd in inv_rounds(logn, approx):
+                parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
+                parts.append("\n")
+        parts.append(f"#endif  // {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
     with open(OUT, "w") as f:
-        f.write("".join(parts))
+        f.write("".join(parts).rstrip("\n") + "\n")
     print("wrote", OUT)
 
 
