@@ -224,10 +224,14 @@ def main():
     inv = ctx.prof_read(1)
     ctx.prof_enable(False)
     logn = n.bit_length() - 1
-    # every BASELINE prime lies in (2^60 - 2^56, 2^60): n = 4096 / 8192 take the hand-scheduled kernel
-    fwd_name = ("ntt_fwd_asm_kernel" if logn in (12, 13) and os.environ.get("EXACTO_NTT_ASM", "1") != "0"
-                else "ntt_fwd_kernel")
-    dom, dom_name = (fwd, f"{fwd_name}<{logn}>") if fwd["ms"] >= inv["ms"] else (inv, f"ntt_inv_kernel<{logn}>")
+    # every BASELINE prime lies in (2^60 - 2^32, 2^60): n = 4096 / 8192 take the hand-scheduled
+    # kernels (n = 4096 forward: the persistent LDS-DMA form)
+    on = lambda k: os.environ.get(k, "1") != "0"
+    asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
+    fwd_name = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and on("EXACTO_NTT_PIPE")
+                else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}>")
+    inv_name = f"ntt_inv_asm_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}>"
+    dom, dom_name = (fwd, fwd_name) if fwd["ms"] >= inv["ms"] else (inv, inv_name)
     achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9 if dom["ms"] > 0 else 0.0
     per_launch_ms = dom["ms"] / max(dom["launches"], 1)
     roofline = {
@@ -247,7 +251,7 @@ def main():
     # HBM bytes per launch from the committed PMC passes over this same bench configuration
     # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch, gfx950 corrections, averaged
     # over every forward-NTT dispatch: the same launch mix per step as the timed one)
-    tfile = os.path.join(ROOT, "profiles", f"r1_{args.config}_fwd_traffic.json")
+    tfile = os.path.join(ROOT, "profiles", f"r2_{args.config}_fwd_traffic.json")
     if dom_name.startswith("ntt_fwd") and os.path.exists(tfile):
         with open(tfile) as f:
             tr = json.load(f)
