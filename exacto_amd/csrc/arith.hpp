@@ -86,6 +86,14 @@ __device__ __forceinline__ u64 reduce64(u64 x, u64 q, u64 mu64) {
     return r;
 }
 
+// x mod q for any x < 2^64 and q = 2^60 - d, d < 2^24: (x mod 2^60) + floor(x / 2^60) d < 2q,
+// then one conditional subtraction (reduce64's quotient estimate costs a 64x64 high product).
+__device__ __forceinline__ u64 reduce_near60(u64 x, u64 q) {
+    const uint32_t d = (uint32_t)((1ull << 60) - q);
+    const u64 r = (x & ((1ull << 60) - 1)) + (u64)(uint32_t)(x >> 60) * d;
+    return r >= q ? r - q : r;
+}
+
 __device__ __forceinline__ u64 barrett128(u64 hi, u64 lo, u64 q, u64 mu, int s) {
     // x = hi:lo < 2^(2s) -> x mod q
     u64 xs = (lo >> (s - 1)) | (hi << (65 - s));

@@ -428,6 +428,7 @@ static int build_tables(exacto_ctx* c) {
         const u64 mn = *std::min_element(c->primes.begin(), c->primes.end());
         C.near = (u128)mx < 2 * (u128)mn;
         C.fast = C.near && mx < (1ull << 60);
+        C.special = C.fast && mn > (1ull << 60) - (1ull << 24);
         C.digit_small = c->gbase <= *std::min_element(qv.begin(), qv.end());
     }
     HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
@@ -700,7 +701,8 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt) {
     bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
     for (int t = 0; t < NP; ++t) {
         lazy &= c->primes[t] < (1ull << 60);
-        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
+        // the fused product (mulmod_near60) needs d = 2^60 - q < 2^24; the asm rounds d < 2^32
+        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
     }
     launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60);
     CHECK_LAUNCH();
@@ -792,6 +794,11 @@ static int ensure_rlk_companions(exacto_ctx* c) {
     return 0;
 }
 
+// CRT kernel variant: 3 special-prime reductions, 2 lazy (fast), 1 near primes, 0 generic
+static int crt_mode(const exacto_ctx* c) {
+    return c->h_crt.special ? 3 : c->h_crt.fast ? 2 : c->h_crt.near ? 1 : 0;
+}
+
 static bool lazy_ok(const exacto_ctx* c, int base, int period) {
     bool lazy = true;
     for (int t = base; t < base + period; ++t) lazy &= c->primes[t] < (1ull << 60);
@@ -850,7 +857,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                 launch_hps_extend(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_primes, K, c->stream);
             else
                 launch_exact_lift(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_crt, c->d_primes, L, K,
-                                  c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
+                                  crt_mode(c), c->stream);
             CHECK_LAUNCH();
             // 3. forward NTT of the extended polynomials
             if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
@@ -870,7 +877,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D, d16 ? c->ws_D16 : nullptr, guse,
-                               cnt, n, c->d_crt, c->d_primes, L, K, c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0),
+                               cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
                                c->stream);
         CHECK_LAUNCH();
         // 7. forward NTT of the results (and digits)
@@ -1227,7 +1234,7 @@ static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
             launch_hps_extend(c->ws_coefQ, eo, 2 * cnt, n, c->d_primes, K, c->stream);
         else
             launch_exact_lift(c->ws_coefQ, eo, 2 * cnt, n, c->d_crt, c->d_primes, L, K,
-                              c->h_crt.fast ? 2 : (c->h_crt.near ? 1 : 0), c->stream);
+                              crt_mode(c), c->stream);
         CHECK_LAUNCH();
         if (int e = run_ntt(c, contiguous(eo, cnt, 2L * K, L, K, n), cnt * 2 * K, false)) return e;
     }

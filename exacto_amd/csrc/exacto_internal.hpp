@@ -55,6 +55,7 @@ struct CrtTables {
     u64 qpq_w[EXACTO_MAX_L + 1][EXACTO_MAX_K], qpq_ws[EXACTO_MAX_L + 1][EXACTO_MAX_K];
     int near;       // max prime < 2 * min prime: residues move between primes by one conditional subtraction
     int fast;       // near and every prime < 2^60: lazy CRT kernels (unreduced Shoup sums)
+    int special;    // fast and every prime is 2^60 - d, d < 2^24: reduce_near60 instead of reduce64
     int digit_small;  // gadget base <= every ciphertext prime: digit magnitudes are already reduced
     u64 pmod_w[EXACTO_MAX_PRIMES], pmod_ws[EXACTO_MAX_PRIMES];  // plain mod prime_t
     u64 Qwords[EXACTO_MAX_L];                   // Q as little-endian 64-bit words
@@ -109,7 +110,8 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 };
 
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
-// asm_inv: every prime in (2^60 - 2^32, 2^60) and n = 4096 / 8192 (generated inverse rounds)
+// asm_inv: every prime is 2^60 - d with d < 2^24 and n = 4096 / 8192 (generated inverse rounds,
+// special-prime products)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
                        const PrimeConst* primes, hipStream_t s, bool asm_inv = false);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.

@@ -117,7 +117,13 @@ __device__ __forceinline__ void garner_q_fast(u64 (&v)[EXACTO_MAX_L], const u64 
 
 // sum_k v_k * pref[k][t] - neg * pref[cnt][t]  (mod prime_t), canonical; 14q < 2^64 bounds
 // the unreduced run to 7 terms.
-template <int MAXN, int STRIDE>
+// SP: every prime is 2^60 - d, d < 2^24 (reduce_near60).
+template <bool SP>
+__device__ __forceinline__ u64 reduce_any(u64 x, const PrimeConst& P) {
+    return SP ? reduce_near60(x, P.q) : reduce64(x, P.q, P.mu64);
+}
+
+template <int MAXN, int STRIDE, bool SP = false>
 __device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool neg, const u64* pw,
                                             const u64* pws, int t, const PrimeConst& P) {
     const u64 q = P.q, nq = (u64)0 - q;
@@ -126,10 +132,10 @@ __device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool 
     for (int k = 0; k < MAXN; ++k) {
         if (k < cnt) {
             acc += shoup_mul_nq(v[k], pw[k * STRIDE + t], pws[k * STRIDE + t], nq);
-            if (k % 7 == 6) acc = reduce64(acc, q, P.mu64);
+            if (k % 7 == 6) acc = reduce_any<SP>(acc, P);
         }
     }
-    acc = reduce64(acc, q, P.mu64);
+    acc = reduce_any<SP>(acc, P);
     if (neg) acc = sub_mod(acc, pw[cnt * STRIDE + t], q);
     return acc;
 }
@@ -254,7 +260,7 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
 
 // ---------------------------------------------------------------- exact lift Q -> P
 
-template <bool NEAR, bool FAST, int LT, int KT>
+template <bool NEAR, bool FAST, int LT, int KT, bool SP = false>
 __global__ void __launch_bounds__(TPB)
 exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, int L_arg, int K_arg,
                   const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
@@ -271,8 +277,8 @@ exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
     for (int a = 0; a < K; ++a) {
         const int t = L + a;
         extP[(row * K + a) * n + j] =
-            FAST ? mr_eval_fast<EXACTO_MAX_L, EXACTO_MAX_PRIMES>(v, L, neg, &C->qpref_w[0][0],
-                                                               &C->qpref_ws[0][0], t, primes[t])
+            FAST ? mr_eval_fast<EXACTO_MAX_L, EXACTO_MAX_PRIMES, SP>(v, L, neg, &C->qpref_w[0][0],
+                                                                   &C->qpref_ws[0][0], t, primes[t])
                  : mr_eval<EXACTO_MAX_L, EXACTO_MAX_PRIMES, NEAR>(v, L, neg, &C->qpref_w[0][0],
                                                                  &C->qpref_ws[0][0], t, primes[t]);
     }
@@ -285,7 +291,19 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
 #define LIFT(NR, FS, LT, KT)                                                                                     \
     hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
                        primes)
-    if (mode == 2) {
+#define LIFT_SP(LT)                                                                                              \
+    hipLaunchKernelGGL((exact_lift_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, coefQ,  \
+                       extP, n, L, K, ct, primes)
+    if (mode == 3 && K == L + 1 && L >= 1 && L <= 6) {
+        switch (L) {
+            case 1: LIFT_SP(1); break;
+            case 2: LIFT_SP(2); break;
+            case 3: LIFT_SP(3); break;
+            case 4: LIFT_SP(4); break;
+            case 5: LIFT_SP(5); break;
+            default: LIFT_SP(6); break;
+        }
+    } else if (mode >= 2) {
         switch (L) {
             case 1: if (K == 2) LIFT(true, true, 1, 2); else LIFT(true, true, 1, 0); break;
             case 2: if (K == 3) LIFT(true, true, 2, 3); else LIFT(true, true, 2, 0); break;
@@ -301,6 +319,7 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
         LIFT(false, false, 0, 0);
     }
 #undef LIFT
+#undef LIFT_SP
 }
 
 // ---------------------------------------------------------------- HPS extension
@@ -333,7 +352,7 @@ void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const Prim
 
 // ---------------------------------------------------------------- exact scale-and-round
 
-template <bool NEAR, bool FAST, int LT, int KT>
+template <bool NEAR, bool FAST, int LT, int KT, bool SP = false>
 __global__ void __launch_bounds__(TPB)
 exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
                    u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n, int L_arg, int K_arg,
@@ -369,10 +388,10 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
             for (int k = 0; k < EXACTO_MAX_L; ++k) {
                 if (k < L) {
                     acc += 2 * pa - shoup_mul_nq(v[k], C->qpq_w[k][a], C->qpq_ws[k][a], np);
-                    if (k % 6 == 5) acc = reduce64(acc, pa, P.mu64);
+                    if (k % 6 == 5) acc = reduce_any<SP>(acc, P);
                 }
             }
-            acc = reduce64(acc, pa, P.mu64);
+            acc = reduce_any<SP>(acc, P);
             // Garner over P on the fly; w_k < p_k < 2 p_a
 #pragma unroll
             for (int k = 0; k < EXACTO_MAX_K; ++k)
@@ -403,8 +422,8 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
 #pragma unroll
     for (int i = 0; i < EXACTO_MAX_L; ++i)
         if (i < L)
-            res[i] = FAST ? mr_eval_fast<EXACTO_MAX_K, EXACTO_MAX_L>(w, K, negr, &C->ppref_w[0][0],
-                                                                      &C->ppref_ws[0][0], i, primes[i])
+            res[i] = FAST ? mr_eval_fast<EXACTO_MAX_K, EXACTO_MAX_L, SP>(w, K, negr, &C->ppref_w[0][0],
+                                                                          &C->ppref_ws[0][0], i, primes[i])
                           : mr_eval<EXACTO_MAX_K, EXACTO_MAX_L, NEAR>(w, K, negr, &C->ppref_w[0][0],
                                                                       &C->ppref_ws[0][0], i, primes[i]);
     if (comp < ncomp_r) {
@@ -427,7 +446,19 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
 #define SCALE(NR, FS, LT, KT)                                                                                    \
     hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
                        D, D16, guse, n, L, K, ct, primes)
-    if (mode == 2) {
+#define SCALE_SP(LT)                                                                                             \
+    hipLaunchKernelGGL((exact_scale_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, T, R,   \
+                       r_stride, ncomp_r, D, D16, guse, n, L, K, ct, primes)
+    if (mode == 3 && K == L + 1 && L >= 1 && L <= 6) {
+        switch (L) {
+            case 1: SCALE_SP(1); break;
+            case 2: SCALE_SP(2); break;
+            case 3: SCALE_SP(3); break;
+            case 4: SCALE_SP(4); break;
+            case 5: SCALE_SP(5); break;
+            default: SCALE_SP(6); break;
+        }
+    } else if (mode >= 2) {
         switch (L) {
             case 1: if (K == 2) SCALE(true, true, 1, 2); else SCALE(true, true, 1, 0); break;
             case 2: if (K == 3) SCALE(true, true, 2, 3); else SCALE(true, true, 2, 0); break;
@@ -443,6 +474,7 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
         SCALE(false, false, 0, 0);
     }
 #undef SCALE
+#undef SCALE_SP
 }
 
 // ---------------------------------------------------------------- decryption

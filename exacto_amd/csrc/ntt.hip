@@ -786,6 +786,20 @@ __device__ __forceinline__ u64 barrett_mul_lazy(u64 a, u64 b, const PrimeConst& 
 
 // ASM (n = 4096 / 8192, every prime in (2^60 - 2^32, 2^60)): the inverse rounds are the generated
 // InvRoundAsm statements (inputs < 4q: products < 3q, c1 < 4q).
+// a * b mod q for q = 2^60 - d, d < 2^24, a, b < q: P = H 2^60 + L == L + H d (mod q), folded
+// twice (H d < 2^84, then H2 d < 2^49): result < 2^60 + 2^49 < 2q.  No quotient estimate and no
+// runtime shift counts (barrett_mul_lazy needs both).
+__device__ __forceinline__ u64 mulmod_near60(u64 a, u64 b, uint32_t d) {
+    constexpr u64 M60 = (1ull << 60) - 1;
+    const u64 lo = a * b, hi = __umul64hi(a, b);
+    const u64 H = (hi << 4) | (lo >> 60);
+    const u64 xl = (lo & M60) + (u64)(uint32_t)H * d;               // < 2^60 + 2^56
+    const u64 xh = (u64)(uint32_t)(H >> 32) * d + (xl >> 32);       // X = xh 2^32 + (uint32)xl
+    const u64 H2 = xh >> 28;                                         // X >> 60
+    const u64 L2 = ((xh & 0x0FFFFFFFull) << 32) | (uint32_t)xl;
+    return L2 + H2 * d;
+}
+
 template <int LOGN, bool LAZY, bool ASM = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
@@ -817,7 +831,11 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
         A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
     }
-    auto mulr = [&](u64 a, u64 b) { return LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P); };
+    // ASM: every prime is 2^60 - d with d < 2^24 (launch_inv_tensor's caller checks)
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    auto mulr = [&](u64 a, u64 b) {
+        return ASM ? mulmod_near60(a, b, dq) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
+    };
     auto load = [&](const u64* src, u64 (&v)[16]) {
         const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
 #pragma unroll
@@ -845,7 +863,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const u64 v = z[k] + mulr(x[k], y[k]);
-            x[k] = LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
+            x[k] = ASM ? v : LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);  // ASM: < 4q
         }
     }
     if constexpr (ASM) {
