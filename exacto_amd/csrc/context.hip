@@ -190,6 +190,17 @@ struct exacto_ctx {
     bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
     bool ntt_pipe = true;   // EXACTO_NTT_PIPE=0: one workgroup per polynomial instead of the persistent LDS-DMA kernel
     bool ntt_asm_inv = true;  // EXACTO_NTT_ASM_INV=0: compiler-scheduled inverse NTT (A/B)
+    // relinearisation MAC in an auxiliary basis of S 31-bit primes (ks32.hip; EXACTO_KS32=0: the
+    // limb-wise 60-bit digit NTTs + relin_mac)
+    bool ks32 = true;
+    int S32 = 0;                 // 0: not eligible for these parameters
+    Prime32* d_p32 = nullptr;
+    uint2* d_tw32 = nullptr;
+    Ks32Tables* d_kst = nullptr;
+    uint32_t* d_rs = nullptr;    // key in the auxiliary basis [keys][2L][S][n], NTT domain mod p_s
+    size_t rs_cap = 0;
+    bool rs_valid = false;
+    uint32_t *ws_DS = nullptr, *ws_U = nullptr, *ws2_DS = nullptr, *ws2_U = nullptr;
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
@@ -336,6 +347,107 @@ static PrimeConst make_prime_const(u64 q, int n, int logn, TwPair* h_fwd, TwPair
 static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
     w = v;
     ws = shoup_h(v, q);
+}
+
+// ks32.hip's auxiliary basis: the fewest primes p == 1 mod 2n in (2^30, 2^32 / 3), largest first, with
+// prod p > 2 G n floor(B/2) floor(q_max/2) (the magnitude bound of sum_g d_g * r_g, digits balanced
+// in [-B/2, B/2), key coefficients balanced).  Eligible: exact path, gadget base <= 2^16 (int16
+// digits), every ciphertext prime 2^60 - d with d < 2^24 (ks32_crt reduces with reduce_near60),
+// 1024 <= n <= 16384; S <= 4.
+static int setup_ks32(exacto_ctx* c) {
+    c->S32 = 0;
+    if (c->path != EXACTO_PATH_EXACT_RNS || c->gbase > 65536 || c->logn < 10 || c->logn > 14 || c->L > 4)
+        return 0;
+    u64 qmax = 0;
+    for (u64 q : c->ctq) {
+        if (q >= (1ull << 60) || q <= (1ull << 60) - (1ull << 24)) return 0;
+        qmax = std::max(qmax, q);
+    }
+    Big bound((u64)c->G);
+    bound.mul((u64)c->n);
+    bound.mul(c->gbase / 2);
+    bound.mul(qmax / 2);
+    bound.mul(2);
+    bound.add(1);
+    std::vector<u64> ps;
+    Big P(1);
+    const u64 step = 2 * (u64)c->n;
+    // p < 2^32 / 3: sums of three residues fit 32 bits (ks32's reductions), and balanced products
+    // (< 2^59.1) leave room for twelve terms per signed 64-bit accumulation
+    const u64 pmax = (1ull << 32) / 3;
+    for (u64 p = (pmax - 1) / step * step + 1; p > (1ull << 30) && ps.size() < EXACTO_KS32_MAXS; p -= step) {
+        if (!is_prime_h(p)) continue;
+        ps.push_back(p);
+        P.mul(p);
+        if (P.cmp(bound) > 0) break;
+    }
+    if (P.cmp(bound) <= 0 || ps.size() < 2) return 0;
+    const int S = (int)ps.size(), n = c->n;
+    std::vector<uint2> tw((size_t)S * 2 * n);
+    std::vector<Prime32> pc(S);
+    auto sh32 = [](u64 w, u64 p) { return (uint32_t)((w << 32) / p); };
+    for (int s = 0; s < S; ++s) {
+        const u64 p = ps[s];
+        const u64 psi = find_psi(n, p), psi_inv = invmod_h(psi, p);
+        for (int i = 0; i < n; ++i) {
+            const int e = bitrev(i, c->logn);
+            const u64 w = powmod_h(psi, e, p), wi = powmod_h(psi_inv, e, p);
+            tw[(size_t)s * 2 * n + i] = make_uint2((uint32_t)w, sh32(w, p));
+            tw[(size_t)s * 2 * n + n + i] = make_uint2((uint32_t)wi, sh32(wi, p));
+        }
+        Prime32& Q = pc[s];
+        Q.p = (uint32_t)p;
+        const u64 ninv = invmod_h((u64)n % p, p);
+        Q.n_inv = (uint32_t)ninv;
+        Q.n_inv_s = sh32(ninv, p);
+        const u64 lw = mulmod_h(tw[(size_t)s * 2 * n + n + 1].x, ninv, p);
+        Q.last_w = (uint32_t)lw;
+        Q.last_ws = sh32(lw, p);
+        const u64 c32 = (1ull << 32) % p;
+        Q.c32 = (uint32_t)c32;
+        Q.c32s = sh32(c32, p);
+        const u64 m63 = (1ull << 63) % p;
+        Q.k63 = (uint32_t)(m63 == 0 ? 0 : p - m63);
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_tw32, tw.size() * sizeof(uint2)));
+    if (int e_ = upload(c, c->d_tw32, tw.data(), tw.size() * sizeof(uint2))) return e_;
+    for (int s = 0; s < S; ++s) {
+        pc[s].tw_fwd = c->d_tw32 + (size_t)s * 2 * n;
+        pc[s].tw_inv = c->d_tw32 + (size_t)s * 2 * n + n;
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_p32, S * sizeof(Prime32)));
+    if (int e_ = upload(c, c->d_p32, pc.data(), S * sizeof(Prime32))) return e_;
+    Ks32Tables T;
+    std::memset(&T, 0, sizeof(T));
+    for (int s = 0; s < S; ++s)
+        for (int k = 0; k < s; ++k) {
+            const u64 v = invmod_h(ps[k] % ps[s], ps[s]);
+            T.ginv[s][k] = (uint32_t)v;
+            T.ginv_s[s][k] = sh32(v, ps[s]);
+        }
+    Big H = P;
+    H.shr1();
+    {
+        std::vector<u64> hr(S);
+        for (int s = 0; s < S; ++s) hr[s] = H.mod(ps[s]);
+        auto mr = mixed_radix(hr, ps);
+        for (int s = 0; s < S; ++s) T.halfP[s] = (uint32_t)mr[s];
+    }
+    for (int l = 0; l < c->L; ++l) {
+        const u64 q = c->ctq[l];
+        u64 pref = 1;
+        for (int s = 0; s < S; ++s) {
+            T.pref_w[l][s] = pref;
+            T.pref_ws[l][s] = shoup_h(pref, q);
+            pref = mulmod_h(pref, ps[s] % q, q);
+        }
+        const u64 pm = P.mod(q);
+        T.negP[l] = pm == 0 ? 0 : q - pm;
+    }
+    HIP_TRY(hipMalloc((void**)&c->d_kst, sizeof(Ks32Tables)));
+    if (int e_ = upload(c, c->d_kst, &T, sizeof(Ks32Tables))) return e_;
+    c->S32 = S;
+    return 0;
 }
 
 static int build_tables(exacto_ctx* c) {
@@ -565,7 +677,9 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
+    if (int rc = setup_ks32(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
     return 0;
 }
@@ -582,6 +696,8 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
+    free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
+    free_dev(c->ws_DS); free_dev(c->ws_U); free_dev(c->ws2_DS); free_dev(c->ws2_U);
     if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -638,6 +754,7 @@ extern "C" uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* c, size_t num_keys)
     c->rlk_keys = num_keys;
     c->rlk_loaded = true;
     c->rlk_s_valid = false;  // contents change: companions recomputed before first use
+    c->rs_valid = false;     // and the auxiliary-basis key
     return c->d_rlk;
 }
 
@@ -746,6 +863,12 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     HIP_TRY(hipMalloc((void**)&c->ws_D, items * std::max(c->G, 1) * c->L * pb));
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     HIP_TRY(hipMalloc((void**)&c->ws_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
+    free_dev(c->ws_DS); free_dev(c->ws_U);
+    c->ws_DS = c->ws_U = nullptr;
+    if (c->S32) {  // ks32: digit residues [item][G][S][n] and accumulators [item][2L][S][n]
+        HIP_TRY(hipMalloc((void**)&c->ws_DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&c->ws_U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
+    }
     c->ws_items = items;
     return 0;
 }
@@ -767,6 +890,12 @@ static int ensure_lane2(exacto_ctx* c, size_t items) {
     HIP_TRY(hipMalloc((void**)&c->ws2_D, items * std::max(c->G, 1) * c->L * pb));
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     HIP_TRY(hipMalloc((void**)&c->ws2_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
+    free_dev(c->ws2_DS); free_dev(c->ws2_U);
+    c->ws2_DS = c->ws2_U = nullptr;
+    if (c->S32) {
+        HIP_TRY(hipMalloc((void**)&c->ws2_DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&c->ws2_U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
+    }
     c->ws2_items = items;
     return 0;
 }
@@ -781,6 +910,7 @@ struct LaneGuard {
         std::swap(c->stream, c->aux_stream);
         std::swap(c->ws_coefQ, c->ws2_coefQ); std::swap(c->ws_extP, c->ws2_extP);
         std::swap(c->ws_T, c->ws2_T); std::swap(c->ws_D, c->ws2_D); std::swap(c->ws_D16, c->ws2_D16);
+        std::swap(c->ws_DS, c->ws2_DS); std::swap(c->ws_U, c->ws2_U);
     }
 };
 
@@ -797,6 +927,28 @@ static int ensure_rlk_companions(exacto_ctx* c) {
 // CRT kernel variant: 3 special-prime reductions, 2 lazy (fast), 1 near primes, 0 generic
 static int crt_mode(const exacto_ctx* c) {
     return c->h_crt.special ? 3 : c->h_crt.fast ? 2 : c->h_crt.near ? 1 : 0;
+}
+
+// The resident relinearisation key in ks32's auxiliary basis: INTT mod q_l (coefficient domain),
+// balanced, reduced mod each p_s, forward NTT mod p_s -> d_rs [keys][2L][S][n].  Once per key.
+static int ensure_rs(exacto_ctx* c) {
+    if (c->rs_valid) return 0;
+    const long rows = (long)c->rlk_keys * 2 * c->L;
+    size_t cap = c->rs_cap;
+    if (grow((u64**)&c->d_rs, &cap, std::max<size_t>((size_t)rows * c->S32 * c->n * sizeof(uint32_t), 8)))
+        return EXACTO_ERR_HIP;
+    c->rs_cap = cap;
+    Scratch ks;
+    HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream));
+    NttBatch nb{};
+    nb.src = c->d_rlk; nb.src_item_stride = 2L * c->L * c->n;
+    nb.dst = ks.as<u64>(); nb.dst_item_stride = 2L * c->L * c->n;
+    nb.ppi = 2 * c->L; nb.prime_base = 0; nb.period = c->L;
+    if (int e = run_ntt(c, nb, rows, true)) return e;
+    ks32_key(ks.as<u64>(), c->d_rs, rows, c->L, c->S32, c->logn, c->d_p32, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    c->rs_valid = true;
+    return 0;
 }
 
 static bool lazy_ok(const exacto_ctx* c, int base, int period) {
@@ -818,8 +970,15 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
     const size_t C = std::min<size_t>(c->chunk, (size_t)P);
     if (int e = ensure_workspace(c, C)) return e;
-    if (relin && guse > 0)
-        if (int e = ensure_rlk_companions(c)) return e;
+    // int16 gadget digits (base <= 2^16, exact path): the scale kernel writes each digit once
+    const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
+                     c->gbase <= 65536;
+    // ... and then the key switch runs over the integers in the 31-bit basis (ks32.hip)
+    const bool k32 = d16 && c->ks32 && c->S32 > 0;
+    if (relin && guse > 0) {
+        // both before the second lane forks: its kernels read these too
+        if (int e = k32 ? ensure_rs(c) : ensure_rlk_companions(c)) return e;
+    }
     // two chunks or more: odd chunks on the second lane (profiling keeps one lane so its per-kernel
     // events time each kernel alone)
     const bool dual = c->dual && !c->prof && P > (long)C;
@@ -871,8 +1030,6 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         u64* R = out + s * out_stride;
         const int ncomp = relin ? 2 : 3;
         u64* D = relin ? c->ws_D : nullptr;
-        const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
-                         c->gbase <= 65536;
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
@@ -896,8 +1053,17 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             CHECK_LAUNCH();
             continue;
         }
+        if (k32) {
+            // 7'+8'. the key switch over the integers (ks32.hip): digits -> NTT mod p_s, MAC with the
+            // key in the same basis, inverse NTT + centred lift, added to R mod q_l in the
+            // coefficient domain; the forward NTT of R below then yields the relinearised result
+            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
+            ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
+            ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
+            CHECK_LAUNCH();
+        }
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
-        if (relin && guse > 0) {
+        if (relin && guse > 0 && !k32) {
             NttBatch db = contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n);
             if (d16) {  // int16 digits [item][g][n] -> NTT residues [item][g][L][n]
                 db.src16 = c->ws_D16;
@@ -1544,6 +1710,7 @@ extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, doubl
         c->rlk_keys = num_keys;
         c->rlk_loaded = true;
         c->rlk_s_valid = false;
+        c->rs_valid = false;
     }
     return 0;
 }

@@ -92,6 +92,38 @@ void launch_keyswitch(const KsArgs& a, int items, int logn, bool lazy, const Pri
 void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
                              hipStream_t s);
 
+// ---- ks32.hip: relinearisation MAC over the integers in an auxiliary basis of 31-bit primes ----
+#define EXACTO_KS32_MAXS 4
+struct Prime32 {
+    uint32_t p;                 // prime in (2^30, 2^32 / 3), p == 1 mod 2n
+    uint32_t n_inv, n_inv_s;    // n^-1 and its Shoup companion floor(w 2^32 / p)
+    uint32_t last_w, last_ws;   // psi_inv_rev[1] n^-1 (fused last inverse stage)
+    uint32_t c32, c32s;         // 2^32 mod p
+    uint32_t k63;               // (-2^63) mod p
+    const uint2* tw_fwd;        // [n] {psi^brv(i), Shoup}
+    const uint2* tw_inv;        // [n] {psi^-brv(i), Shoup}
+};
+struct Ks32Tables {
+    uint32_t ginv[EXACTO_KS32_MAXS][EXACTO_KS32_MAXS];    // p_k^-1 mod p_s (k < s)
+    uint32_t ginv_s[EXACTO_KS32_MAXS][EXACTO_KS32_MAXS];
+    uint32_t halfP[EXACTO_KS32_MAXS];                     // mixed-radix digits of floor(P / 2)
+    u64 pref_w[EXACTO_MAX_L][EXACTO_KS32_MAXS];           // (p_0 ... p_{s-1}) mod q_l
+    u64 pref_ws[EXACTO_MAX_L][EXACTO_KS32_MAXS];
+    u64 negP[EXACTO_MAX_L];                               // (q_l - P mod q_l) mod q_l
+};
+// int16 digits [items][G][n] -> DS [items][G][S][n], NTT mod p_s
+void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+                 hipStream_t st);
+// key rows [rows][n] (coefficient domain, canonical mod q_{row % L}) -> RS [rows][S][n]
+void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
+              const PrimeConst* qprimes, hipStream_t st);
+// U [items][2L][S][n] = sum_g DS (.) RS
+void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
+              const Prime32* primes, hipStream_t st);
+// R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
+void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
+              const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);
+
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item
     const u64* a;

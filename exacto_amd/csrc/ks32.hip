@@ -1,0 +1,435 @@
+// Relinearisation key switching over the integers in an auxiliary basis of 31-bit primes.
+//
+// relinearize (reference src/bfv/keyswitch.rs:86-95) adds sum_g NTT_l(d_g) (.) rlk_{g,c,l} to the
+// scaled components, limb by limb.  By the negacyclic convolution theorem that is
+// NTT_l(sum_g d_g * r_{g,c,l} mod q_l) with r = INTT_l(rlk) the key in the coefficient domain.  The
+// digits d_g are small integers (|d| <= B/2) and the same for every limb, so the integer
+// polynomial u_{c,l} = sum_g d_g * r_{g,c,l} (r balanced, |r| < q_l / 2) has coefficients below
+// G n (B/2) (q/2) in magnitude: for cfg3 below 2^90, for cfg5 below 2^84.  It is computed exactly
+// modulo S 31-bit primes p_s with prod p_s > 2 |u|max (S = 3 for every BASELINE config), then
+// lifted (Garner, centred) and reduced mod q_l.  Bit-identical with the limb-wise MAC by
+// construction; the work moves from G L 60-bit digit NTTs to G S 32-bit ones (no carry chains:
+// a 32-bit butterfly is three multiplies) plus 2 L S 32-bit inverse transforms.
+//
+// Kernels (all one residue polynomial per workgroup, n/16 threads x 16 coefficients, the same
+// round/LDS structure as ntt.hip):
+//   ks32_digit_ntt_kernel : int16 digits [item][g][n] -> DS [item][g][s][n], forward NTT mod p_s
+//   ks32_key_kernel        : coefficient-domain key rows (canonical mod q_l) -> balanced -> mod p_s,
+//                            forward NTT -> RS [g][c][l][s][n] (once per key)
+//   ks32_mac_kernel        : U [item][c][l][s] = sum_g DS [item][g][s] (.) RS [g][c][l][s] mod p_s,
+//                            key slice staged in LDS, 64-bit lazy accumulation
+//   ks32_crt_kernel        : per (item, c, l): S inverse NTTs, centred Garner lift, + R[item][c][l]
+//                            mod q_l, written back into R (coefficient domain)
+#include "exacto_internal.hpp"
+
+#include <algorithm>
+
+namespace exacto {
+
+// x * w mod p in [0, 2p) for any x < 2^32 (ws = floor(w 2^32 / p), p < 2^31)
+__device__ __forceinline__ uint32_t shoup32(uint32_t x, uint32_t w, uint32_t ws, uint32_t p) {
+    return x * w - __umulhi(x, ws) * p;
+}
+
+// [0, 2p) -> [0, p): x - p wraps above x when x < p
+__device__ __forceinline__ uint32_t red32(uint32_t x, uint32_t p) { return min(x, x - p); }
+
+__device__ __forceinline__ int swz32(int j) { return j ^ ((j >> 4) & 15) ^ (((j >> 8) & 1) << 4); }
+
+template <int LO>
+__device__ __forceinline__ int eidx(int tid, int k) {
+    return ((tid >> LO) << (LO + 4)) | (k << LO) | (tid & ((1 << LO) - 1));
+}
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ---------------------------------------------------------------- forward (Cooley-Tukey)
+
+// One round: stage bits BHI..LO of the 4-bit window at LO.  Values < 2p between stages.
+template <int LOGN, int LO, int BHI>
+__device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const uint2* __restrict__ tw, uint32_t p) {
+    constexpr int N = 1 << LOGN;
+    const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+#pragma unroll
+    for (int b = BHI; b >= LO; --b) {
+        const int lb = b - LO, half = 1 << lb;
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> lb); ++g) {
+            const uint2 t = tw[base + g];
+#pragma unroll
+            for (int m = 0; m < half; ++m) {
+                const int k0 = g * 2 * half + m, k1 = k0 + half;
+                const uint32_t X = red32(x[k0], p);
+                const uint32_t T = red32(shoup32(x[k1], t.x, t.y, p), p);
+                x[k0] = X + T;
+                x[k1] = X + p - T;
+            }
+        }
+    }
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const uint2* tw, uint32_t p) {
+    constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
+    constexpr int BHI = LOGN - 1 - 4 * R;
+    if constexpr (R > 0) {
+        constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
+        lds_sync();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lds[swz32(eidx<PLO>(tid, k))] = x[k];
+        lds_sync();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = lds[swz32(eidx<LO>(tid, k))];
+    }
+    fwd32_round<LOGN, LO, BHI>(x, tid, tw, p);
+    if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1>(x, lds, tid, tw, p);
+}
+
+// x (element tid + k T) -> NTT, canonical, stored coalesced at dst (element tid + k T of the
+// bit-reversed-order evaluation array)
+template <int LOGN>
+__device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P,
+                                            uint32_t* __restrict__ dst) {
+    constexpr int T = (1 << LOGN) / 16;
+    fwd32_rounds<LOGN, 0>(x, lds, tid, P.tw_fwd, P.p);
+    lds_sync();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[swz32(eidx<0>(tid, k))] = red32(x[k], P.p);
+    lds_sync();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = lds[swz32(eidx<LOGN - 4>(tid, k))];
+}
+
+// ---------------------------------------------------------------- inverse (Gentleman-Sande)
+
+template <int LOGN, int LO, int BLO, int BHI>
+__device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Prime32& P) {
+    constexpr int N = 1 << LOGN;
+    const uint32_t p = P.p;
+    const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
+#pragma unroll
+    for (int b = BLO; b <= BHI; ++b) {
+        const int lb = b - LO, half = 1 << lb;
+        const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
+#pragma unroll
+        for (int g = 0; g < (8 >> lb); ++g) {
+            uint2 t = make_uint2(0, 0);
+            if (b != LOGN - 1) t = P.tw_inv[base + g];
+#pragma unroll
+            for (int m = 0; m < half; ++m) {
+                const int k0 = g * 2 * half + m, k1 = k0 + half;
+                const uint32_t U = red32(x[k0], p), V = red32(x[k1], p);
+                if (b == LOGN - 1) {  // n^-1 folded in, canonical
+                    x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
+                    x[k1] = red32(shoup32(U + p - V, P.last_w, P.last_ws, p), p);
+                } else {
+                    x[k0] = U + V;
+                    x[k1] = shoup32(U + p - V, t.x, t.y, p);
+                }
+            }
+        }
+    }
+}
+
+template <int LOGN, int R>
+__device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
+    constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
+    constexpr int BLO = 4 * R;
+    constexpr int BHI = (4 * R + 3) < (LOGN - 1) ? 4 * R + 3 : LOGN - 1;
+    if constexpr (R > 0) {
+        constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
+        lds_sync();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) lds[swz32(eidx<PLO>(tid, k))] = x[k];
+        lds_sync();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = lds[swz32(eidx<LO>(tid, k))];
+    }
+    inv32_round<LOGN, LO, BLO, BHI>(x, tid, P);
+    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1>(x, lds, tid, P);
+}
+
+// ---------------------------------------------------------------- kernels
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16)
+ks32_digit_ntt_kernel(const int16_t* __restrict__ D16, uint32_t* __restrict__ DS, int G, int S,
+                      const Prime32* __restrict__ primes) {
+    constexpr int N = 1 << LOGN, T = N / 16;
+    __shared__ uint32_t lds[N];
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;                 // (item, g, s)
+    const int s = (int)(b % S);
+    const long ig = b / S;                     // item * G + g
+    const Prime32& P = primes[s];
+    const int16_t* src = D16 + ig * N;
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int d = src[tid + k * T];
+        x[k] = d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
+    }
+    fwd32_store<LOGN>(x, lds, tid, P, DS + b * N);
+}
+
+// key rows [rows][n] canonical mod q_{row's limb} (u64) -> RS [rows][S][n]: balanced, mod p_s, NTT
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16)
+ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int S,
+                const Prime32* __restrict__ primes, const PrimeConst* __restrict__ qprimes) {
+    constexpr int N = 1 << LOGN, T = N / 16;
+    __shared__ uint32_t lds[N];
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;                 // (row, s), row = (g * 2 + c) * L + l
+    const int s = (int)(b % S);
+    const long row = b / S;
+    const int l = (int)(row % L);
+    const Prime32& P = primes[s];
+    const u64 q = qprimes[l].q, half = q >> 1;
+    const u64* src = K + row * N;
+    uint32_t x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const u64 r = src[tid + k * T];
+        // balanced representative r - q (r > q/2) as a residue mod p
+        if (r > half) {
+            const uint32_t m = (uint32_t)((q - r) % P.p);
+            x[k] = m == 0 ? 0 : P.p - m;
+        } else {
+            x[k] = (uint32_t)(r % P.p);
+        }
+    }
+    fwd32_store<LOGN>(x, lds, tid, P, RS + b * N);
+}
+
+// Signed 64-bit x -> x mod p, canonical (p in (2^30, 2^32 / 3)): x = hi 2^32 + lo with hi signed;
+// (hi + 2^31) 2^32 by Shoup with 2^32 mod p, lo by two halvings, -2^63 by the constant k63.
+__device__ __forceinline__ uint32_t red_s64(long long x, const Prime32& P) {
+    const uint32_t p = P.p;
+    const uint32_t hu = (uint32_t)((unsigned long long)x >> 32) ^ 0x80000000u;
+    const uint32_t a = red32(shoup32(hu, P.c32, P.c32s, p), p);
+    const uint32_t b = red32(red32((uint32_t)x, 2 * p), p);
+    return red32(red32(a + b + P.k63, 2 * p), p);    // a + b + k63 < 3p < 2^32
+}
+
+__device__ __forceinline__ int balanced32(uint32_t v, uint32_t p) { return v > (p >> 1) ? (int)(v - p) : (int)v; }
+
+// U[item][cl][s][j] = sum_g DS[item][g][s][j] * RS[g][cl][s][j] mod p_s   (cl = c * L + l)
+// Block: 64 coefficients j of one prime s, CLB consecutive (c, l) pairs starting at cl0, and up to
+// KS_IG items; its key words (G * CLB * 64, balanced) are staged in LDS once.  Lane = coefficient,
+// wave w handles items it0 + w, it0 + w + 4, ...  Digit residue and key are both balanced,
+// |product| < (p/2)^2 < 2^59.1, so twelve signed products and the carried residue stay below 2^63
+// (one v_mad_i64_i32 each) before a reduction.
+constexpr int KS_LS = 64;
+constexpr int KS_IG = 16;   // items per block: more, shorter blocks keep more loads in flight
+constexpr int KS_RUN = 12;  // signed products summed between reductions
+
+template <int CLB>
+__global__ void __launch_bounds__(256)
+ks32_mac_kernel(const uint32_t* __restrict__ DS, const uint32_t* __restrict__ RS, uint32_t* __restrict__ U,
+                int G, int CL, int S, int items, int n, const Prime32* __restrict__ primes) {
+    extern __shared__ int kl[];                // [g][cl - cl0][lane]
+    const int lane = threadIdx.x & (KS_LS - 1), wave = threadIdx.x / KS_LS;
+    const int nb = n / KS_LS;
+    const int jb = blockIdx.x % nb;
+    const int s = (blockIdx.x / nb) % S;
+    const int cl0 = (blockIdx.x / (nb * S)) * CLB;
+    const int j = jb * KS_LS + lane;
+    const Prime32& P = primes[s];
+    const uint32_t p = P.p;
+    for (int r = threadIdx.x; r < G * CLB * KS_LS; r += 256) {
+        const int g = r / (CLB * KS_LS), c = (r / KS_LS) % CLB, t = r & (KS_LS - 1);
+        kl[r] = balanced32(RS[(((long)g * CL + cl0 + c) * S + s) * n + jb * KS_LS + t], p);
+    }
+    __syncthreads();
+    const int it_end = min(items, (int)(blockIdx.y + 1) * KS_IG);
+    for (int it = blockIdx.y * KS_IG + wave; it < it_end; it += 256 / KS_LS) {
+        const uint32_t* dp = DS + ((long)it * G * S + s) * n + j;
+        long long acc[CLB];
+#pragma unroll
+        for (int c = 0; c < CLB; ++c) acc[c] = 0;
+        for (int g0 = 0; g0 < G; g0 += KS_RUN) {
+            // unconditional (clamped) loads, all in flight together; digits past G are zeroed after
+            uint32_t raw[KS_RUN];
+#pragma unroll
+            for (int e = 0; e < KS_RUN; ++e) raw[e] = dp[(long)min(g0 + e, G - 1) * S * n];
+            int d[KS_RUN];
+#pragma unroll
+            for (int e = 0; e < KS_RUN; ++e) d[e] = g0 + e < G ? balanced32(raw[e], p) : 0;
+#pragma unroll
+            for (int e = 0; e < KS_RUN; ++e) {
+                const int* kg = kl + (min(g0 + e, G - 1) * CLB) * KS_LS + lane;
+#pragma unroll
+                for (int c = 0; c < CLB; ++c) acc[c] += (long long)d[e] * kg[c * KS_LS];
+            }
+            if (g0 + KS_RUN < G) {
+#pragma unroll
+                for (int c = 0; c < CLB; ++c) acc[c] = red_s64(acc[c], P);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CLB; ++c) U[(((long)it * CL + cl0 + c) * S + s) * n + j] = red_s64(acc[c], P);
+    }
+}
+
+// Per (item, c, l): the S accumulated rows -> inverse NTT mod p_s -> centred Garner lift ->
+// R[item][c][l] += lift mod q_l (R canonical, coefficient domain).  The lift mod q = 2^60 - d is a
+// Horner evaluation x = a_0 + p_0 (a_1 + p_1 (a_2 + ...)) whose every step folds the 92-bit
+// product through 2^60 == d (5 instructions); the centring (x > floor(P/2)) is decided on the
+// mixed-radix digits and adds q - (P mod q).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16)
+ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L, int S,
+                const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
+                const PrimeConst* __restrict__ qprimes) {
+    constexpr int N = 1 << LOGN, T = N / 16;
+    __shared__ uint32_t lds[N];
+    const int tid = threadIdx.x;
+    const long b = blockIdx.x;                 // (item, cl)
+    const int CL = 2 * L;
+    const long item = b / CL;
+    const int cl = (int)(b - item * CL);
+    const int l = cl % L;
+    uint32_t v[EXACTO_KS32_MAXS][16];
+#pragma unroll
+    for (int s = 0; s < EXACTO_KS32_MAXS; ++s) {
+        if (s < S) {
+            const uint4* src = reinterpret_cast<const uint4*>(U + (b * S + s) * N + 16 * tid);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint4 w = src[h];
+                v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
+            }
+            inv32_rounds<LOGN, 0>(v[s], lds, tid, primes[s]);
+        }
+    }
+    // element k*T + tid of every row is in v[s][k]
+    const u64 q = qprimes[l].q;
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+    const u64 negP = KT->negP[l];
+    u64* dst = R + item * r_stride + (long)cl * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        // Garner over the p_s: a_s = (v_s - a_0 - a_1 p_0 - ...) / (p_0 ... p_{s-1}) mod p_s
+        uint32_t a[EXACTO_KS32_MAXS];
+#pragma unroll
+        for (int s = 0; s < EXACTO_KS32_MAXS; ++s) {
+            if (s < S) {
+                const uint32_t ps = primes[s].p;
+                uint32_t t = v[s][k];
+#pragma unroll
+                for (int kk = 0; kk < EXACTO_KS32_MAXS; ++kk) {
+                    if (kk < s) {   // a_kk < p_kk < 2 p_s
+                        t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
+                        t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
+                    }
+                }
+                a[s] = t;
+            }
+        }
+        bool neg = false, undecided = true;
+#pragma unroll
+        for (int s = EXACTO_KS32_MAXS - 1; s >= 0; --s) {
+            if (s < S && undecided && a[s] != KT->halfP[s]) {
+                neg = a[s] > KT->halfP[s];
+                undecided = false;
+            }
+        }
+        // Horner mod q from the most significant digit; t < 2q between steps
+        u64 t = a[S - 1];
+#pragma unroll
+        for (int s = EXACTO_KS32_MAXS - 2; s >= 0; --s) {
+            if (s < S - 1) {
+                const u64 lo = (u64)(uint32_t)t * primes[s].p + a[s];               // < 2^63
+                const u64 hi = (u64)(uint32_t)(t >> 32) * primes[s].p + (lo >> 32);  // x = hi 2^32 + lo.lo
+                const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
+                t = l60 + (hi >> 28) * dq;                                         // < 2^60 + 2^56
+            }
+        }
+        if (neg) t += negP;
+        t += dst[k * T + tid];
+        dst[k * T + tid] = reduce_near60(t, q);                                    // t < 2^62
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+
+template <int LOGN>
+static void ks32_launch_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, const Prime32* primes,
+                               hipStream_t st) {
+    hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN>), dim3((unsigned)((long)items * G * S)), dim3((1 << LOGN) / 16), 0,
+                       st, D16, DS, G, S, primes);
+}
+
+template <int LOGN>
+static void ks32_launch_key(const u64* K, uint32_t* RS, long rows, int L, int S, const Prime32* primes,
+                            const PrimeConst* qprimes, hipStream_t st) {
+    hipLaunchKernelGGL((ks32_key_kernel<LOGN>), dim3((unsigned)(rows * S)), dim3((1 << LOGN) / 16), 0, st, K, RS, L,
+                       S, primes, qprimes);
+}
+
+template <int LOGN>
+static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
+                            const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
+    hipLaunchKernelGGL((ks32_crt_kernel<LOGN>), dim3((unsigned)((long)items * 2 * L)), dim3((1 << LOGN) / 16), 0, st, U,
+                       R, r_stride, L, S, KT, primes, qprimes);
+}
+
+#define KS32_SWITCH(logn, CALL)                  \
+    switch (logn) {                              \
+        case 10: CALL(10); break;                \
+        case 11: CALL(11); break;                \
+        case 12: CALL(12); break;                \
+        case 13: CALL(13); break;                \
+        case 14: CALL(14); break;                \
+        default: break;                          \
+    }
+
+void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+                 hipStream_t st) {
+    if (items <= 0) return;
+#define CALL(L_) ks32_launch_digits<L_>(D16, DS, items, G, S, primes, st)
+    KS32_SWITCH(logn, CALL)
+#undef CALL
+}
+
+void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
+              const PrimeConst* qprimes, hipStream_t st) {
+    if (rows <= 0) return;
+#define CALL(L_) ks32_launch_key<L_>(K, RS, rows, L, S, primes, qprimes, st)
+    KS32_SWITCH(logn, CALL)
+#undef CALL
+}
+
+void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
+              const Prime32* primes, hipStream_t st) {
+    if (items <= 0) return;
+    const int CL = 2 * L;
+    // (c, l) pairs per block: the largest divisor of 2L whose key slice (G * CLB * 64 words) fits
+    // 32 KiB of LDS
+    int CLB = CL;
+    while (CLB > 1 && (CL % CLB != 0 || (size_t)G * CLB * KS_LS * sizeof(int) > 32768)) --CLB;
+    const dim3 grid((unsigned)((n / KS_LS) * S * (CL / CLB)), (unsigned)((items + KS_IG - 1) / KS_IG));
+    const size_t lds = (size_t)G * CLB * KS_LS * sizeof(int);
+#define MAC(C_) hipLaunchKernelGGL((ks32_mac_kernel<C_>), grid, dim3(256), lds, st, DS, RS, U, G, CL, S, items, n, primes)
+    switch (CLB) {
+        case 8: MAC(8); break;
+        case 6: MAC(6); break;
+        case 4: MAC(4); break;
+        case 3: MAC(3); break;
+        case 2: MAC(2); break;
+        default: MAC(1); break;
+    }
+#undef MAC
+}
+
+void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
+              const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
+    if (items <= 0) return;
+#define CALL(L_) ks32_launch_crt<L_>(U, R, r_stride, items, L, S, KT, primes, qprimes, st)
+    KS32_SWITCH(logn, CALL)
+#undef CALL
+}
+
+}  // namespace exacto
