@@ -259,6 +259,23 @@ def main():
         roofline["traffic_over_algorithmic"] = round(tr["traffic_bytes_avg"] / roofline["bytes_per_launch"], 4)
         roofline["traffic_source"] = os.path.relpath(tfile, ROOT)
 
+    # the compute-side ceiling of the same kernel (integer modular arithmetic: the VALU issue rate,
+    # not MFMA): VALU wave-instructions and GPU cycles per dispatch from the committed PMC pass
+    # over this bench (tools/r2_evidence.sh), at the measured ~4.4 cycles per integer
+    # multiply-class wave-instruction per SIMD (tools/op_rate.hip, 1024 SIMDs)
+    vfile = os.path.join(ROOT, "profiles", f"r2_{args.config}_valu_counters.json")
+    if os.path.exists(vfile):
+        with open(vfile) as f:
+            vc = json.load(f)["kernels"]
+        hit = [v for k, v in vc.items() if dom_name.split("<")[0] in k]
+        if hit:
+            v = hit[0]
+            need = v["valu_insts"] * 4.4 / 1024.0
+            roofline["compute"] = {"bound": "valu", "valu_insts_per_launch": round(v["valu_insts"]),
+                                   "cycles_per_valu": 4.4, "gpu_cycles_per_launch": round(v["gpu_cycles"]),
+                                   "frac": round(need / v["gpu_cycles"], 3),
+                                   "source": os.path.relpath(vfile, ROOT)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cfg3":
         # all the host cores this job may use (16 on the GPU box, whose os.cpu_count() reports the

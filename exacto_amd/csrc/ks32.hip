@@ -43,6 +43,25 @@ __device__ __forceinline__ int eidx(int tid, int k) {
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// The swizzle is linear over GF(2) and eidx<LO>(tid, k) = A(tid) ^ (k << LO) with disjoint bits, so
+// every exchange address is one per-thread base XOR a compile-time constant (as ntt.hip's
+// lds_store_x): one VALU per access instead of recomputing the swizzle of each index.
+template <int LO>
+__device__ __forceinline__ void lds32_store(uint32_t* lds, const uint32_t (&x)[16], int tid) {
+    char* lb = reinterpret_cast<char*>(lds);
+    const int b = swz32(eidx<LO>(tid, 0)) << 2;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) *reinterpret_cast<uint32_t*>(lb + (b ^ (swz32(k << LO) << 2))) = x[k];
+}
+
+template <int LO>
+__device__ __forceinline__ void lds32_load(const uint32_t* lds, uint32_t (&x)[16], int tid) {
+    const char* lb = reinterpret_cast<const char*>(lds);
+    const int b = swz32(eidx<LO>(tid, 0)) << 2;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = *reinterpret_cast<const uint32_t*>(lb + (b ^ (swz32(k << LO) << 2)));
+}
+
 // ---------------------------------------------------------------- forward (Cooley-Tukey)
 
 // One round: stage bits BHI..LO of the 4-bit window at LO.  Values < 2p between stages.
@@ -76,11 +95,9 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
     if constexpr (R > 0) {
         constexpr int PLO = (LOGN - 4 * R) > 0 ? (LOGN - 4 * R) : 0;
         lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) lds[swz32(eidx<PLO>(tid, k))] = x[k];
+        lds32_store<PLO>(lds, x, tid);
         lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = lds[swz32(eidx<LO>(tid, k))];
+        lds32_load<LO>(lds, x, tid);
     }
     fwd32_round<LOGN, LO, BHI>(x, tid, tw, p);
     if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1>(x, lds, tid, tw, p);
@@ -93,12 +110,14 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     fwd32_rounds<LOGN, 0>(x, lds, tid, P.tw_fwd, P.p);
-    lds_sync();
 #pragma unroll
-    for (int k = 0; k < 16; ++k) lds[swz32(eidx<0>(tid, k))] = red32(x[k], P.p);
+    for (int k = 0; k < 16; ++k) x[k] = red32(x[k], P.p);
     lds_sync();
+    lds32_store<0>(lds, x, tid);
+    lds_sync();
+    lds32_load<LOGN - 4>(lds, x, tid);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = lds[swz32(eidx<LOGN - 4>(tid, k))];
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
 }
 
 // ---------------------------------------------------------------- inverse (Gentleman-Sande)
@@ -140,11 +159,9 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
     if constexpr (R > 0) {
         constexpr int PLO = (4 * (R - 1)) < (LOGN - 4) ? 4 * (R - 1) : LOGN - 4;
         lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) lds[swz32(eidx<PLO>(tid, k))] = x[k];
+        lds32_store<PLO>(lds, x, tid);
         lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = lds[swz32(eidx<LO>(tid, k))];
+        lds32_load<LO>(lds, x, tid);
     }
     inv32_round<LOGN, LO, BLO, BHI>(x, tid, P);
     if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1>(x, lds, tid, P);
@@ -278,9 +295,9 @@ ks32_mac_kernel(const uint32_t* __restrict__ DS, const uint32_t* __restrict__ RS
 // Horner evaluation x = a_0 + p_0 (a_1 + p_1 (a_2 + ...)) whose every step folds the 92-bit
 // product through 2^60 == d (5 instructions); the centring (x > floor(P/2)) is decided on the
 // mixed-radix digits and adds q - (P mod q).
-template <int LOGN>
+template <int LOGN, int S>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
-ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L, int S,
+ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
                 const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
                 const PrimeConst* __restrict__ qprimes) {
     constexpr int N = 1 << LOGN, T = N / 16;
@@ -291,18 +308,22 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     const long item = b / CL;
     const int cl = (int)(b - item * CL);
     const int l = cl % L;
-    uint32_t v[EXACTO_KS32_MAXS][16];
+    uint32_t v[S][16];
 #pragma unroll
-    for (int s = 0; s < EXACTO_KS32_MAXS; ++s) {
-        if (s < S) {
-            const uint4* src = reinterpret_cast<const uint4*>(U + (b * S + s) * N + 16 * tid);
+    for (int s = 0; s < S; ++s) {
+        const uint4* src = reinterpret_cast<const uint4*>(U + (b * S + s) * N + 16 * tid);
 #pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                const uint4 w = src[h];
-                v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
-            }
-            inv32_rounds<LOGN, 0>(v[s], lds, tid, primes[s]);
+        for (int h = 0; h < 4; ++h) {
+            const uint4 w = src[h];
+            v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
         }
+        inv32_rounds<LOGN, 0>(v[s], lds, tid, primes[s]);
+    }
+    uint32_t pr[S], hp[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        pr[s] = primes[s].p;
+        hp[s] = KT->halfP[s];
     }
     // element k*T + tid of every row is in v[s][k]
     const u64 q = qprimes[l].q;
@@ -312,40 +333,34 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         // Garner over the p_s: a_s = (v_s - a_0 - a_1 p_0 - ...) / (p_0 ... p_{s-1}) mod p_s
-        uint32_t a[EXACTO_KS32_MAXS];
+        uint32_t a[S];
 #pragma unroll
-        for (int s = 0; s < EXACTO_KS32_MAXS; ++s) {
-            if (s < S) {
-                const uint32_t ps = primes[s].p;
-                uint32_t t = v[s][k];
+        for (int s = 0; s < S; ++s) {
+            const uint32_t ps = pr[s];
+            uint32_t t = v[s][k];
 #pragma unroll
-                for (int kk = 0; kk < EXACTO_KS32_MAXS; ++kk) {
-                    if (kk < s) {   // a_kk < p_kk < 2 p_s
-                        t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
-                        t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
-                    }
-                }
-                a[s] = t;
+            for (int kk = 0; kk < s; ++kk) {   // a_kk < p_kk < 2 p_s
+                t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
+                t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
             }
+            a[s] = t;
         }
-        bool neg = false, undecided = true;
+        // centred: x > floor(P/2), on the mixed-radix digits, most significant first
+        bool gt = false, eq = true;
 #pragma unroll
-        for (int s = EXACTO_KS32_MAXS - 1; s >= 0; --s) {
-            if (s < S && undecided && a[s] != KT->halfP[s]) {
-                neg = a[s] > KT->halfP[s];
-                undecided = false;
-            }
+        for (int s = S - 1; s >= 0; --s) {
+            gt = gt || (eq && a[s] > hp[s]);
+            eq = eq && a[s] == hp[s];
         }
+        const bool neg = gt;
         // Horner mod q from the most significant digit; t < 2q between steps
         u64 t = a[S - 1];
 #pragma unroll
-        for (int s = EXACTO_KS32_MAXS - 2; s >= 0; --s) {
-            if (s < S - 1) {
-                const u64 lo = (u64)(uint32_t)t * primes[s].p + a[s];               // < 2^63
-                const u64 hi = (u64)(uint32_t)(t >> 32) * primes[s].p + (lo >> 32);  // x = hi 2^32 + lo.lo
-                const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
-                t = l60 + (hi >> 28) * dq;                                         // < 2^60 + 2^56
-            }
+        for (int s = S - 2; s >= 0; --s) {
+            const u64 lo = (u64)(uint32_t)t * pr[s] + a[s];                      // < 2^63
+            const u64 hi = (u64)(uint32_t)(t >> 32) * pr[s] + (lo >> 32);         // x = hi 2^32 + lo.lo
+            const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
+            t = l60 + (hi >> 28) * dq;                                         // < 2^60 + 2^56
         }
         if (neg) t += negP;
         t += dst[k * T + tid];
@@ -372,8 +387,13 @@ static void ks32_launch_key(const u64* K, uint32_t* RS, long rows, int L, int S,
 template <int LOGN>
 static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
                             const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
-    hipLaunchKernelGGL((ks32_crt_kernel<LOGN>), dim3((unsigned)((long)items * 2 * L)), dim3((1 << LOGN) / 16), 0, st, U,
-                       R, r_stride, L, S, KT, primes, qprimes);
+    const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
+    if (S == 2)
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+    else if (S == 3)
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 3>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+    else
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 4>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
 }
 
 #define KS32_SWITCH(logn, CALL)                  \
