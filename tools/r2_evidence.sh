@@ -11,4 +11,10 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_BU
 bash $R/tools/prof_bench.sh ev2/prof_cfg3 --steps 10
 EXACTO_DUAL_STREAM=0 bash $R/tools/prof_bench.sh ev2/prof_cfg3_single --steps 6
 python3 $R/tools/trace_steady.py $E/prof_cfg3_single/run_kernel_trace.csv > $E/steady_single.json
+python3 $R/tools/valu_report.py $E/valu "rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- bench.py --steps 2 --warmup 1 (cfg3)" > $E/valu_counters.json
+cd $R
+for c in ${BENCH_CONFIGS:-cfg2 cfg3 cfg4 cfg5 galois}; do
+  timeout -k 10 400 python3 bench.py --config $c > $E/bench_$c.json 2>> $E/bench_err.log
+  cat $E/bench_$c.json
+done
 echo done
