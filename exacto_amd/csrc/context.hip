@@ -1035,7 +1035,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         else
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D, d16 ? c->ws_D16 : nullptr, guse,
                                cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
-                               c->stream);
+                               c->stream, c->h_crt.gshift);
         CHECK_LAUNCH();
         // 7. forward NTT of the results (and digits)
         NttBatch rb{};

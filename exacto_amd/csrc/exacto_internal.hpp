@@ -158,10 +158,11 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s);
 void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const PrimeConst* primes,
                        int K, hipStream_t s);
-// D16 (or nullptr): gadget digits of the third component as int16 [item][g][n] instead of D
+// D16 (or nullptr): gadget digits of the third component as int16 [item][g][n] instead of D;
+// gshift: log2 of the gadget base (-1 if not a power of two), selects the digit code at launch
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s);
+                        int K, int mode, hipStream_t s, int gshift = -1);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);

@@ -140,6 +140,43 @@ __device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool 
     return acc;
 }
 
+// ---- 30-bit-limb dot products (SP: every prime 2^60 - d, d < 2^24) ----
+// sum_k x_k c_k with x_k, c_k < 2^60, kept exactly as a0 + a1 2^30 + a2 2^60: each operand is
+// split into 30-bit limbs, so every limb product is below 2^60 and one v_mad_u64_u32 adds it to
+// its column without a carry (up to 7 terms plus an additive constant below 2^60 in a0).  One
+// fold through 2^60 == d at the end replaces a Shoup product (about 16 VALU) per term with 4
+// multiply-adds per term.  The constants are wave-uniform: their limbs are split on the SALU.
+struct Dot30 {
+    u64 a0, a1, a2;
+};
+
+constexpr uint32_t M30 = (1u << 30) - 1;
+
+__device__ __forceinline__ void dot30_mac(Dot30& A, uint32_t x0, uint32_t x1, u64 c) {
+    const uint32_t c0 = (uint32_t)c & M30, c1 = (uint32_t)(c >> 30);
+    A.a0 += (u64)x0 * c0;
+    A.a1 += (u64)x0 * c1;
+    A.a1 += (u64)x1 * c0;
+    A.a2 += (u64)x1 * c1;
+}
+
+// (a0 + a1 2^30 + a2 2^60) mod q, canonical.  With m <= 7 terms: a0 < (m + 1) 2^60,
+// a1 < 2 m 2^60, a2 < m 2^60.  2^60 == d gives
+//   X == a0 + (a1 mod 2^30) 2^30 + H d,   H = a2 + floor(a1 / 2^30) < 2^63,
+//   H d = Hl d + F 2^32 (Hl = H mod 2^32, F = floor(H / 2^32) d < 2^55),
+//   F 2^32 == (F mod 2^28) 2^32 + floor(F / 2^28) d,
+// and the five terms sum below (m + 3.1) 2^60 < 2^64; reduce_near60 makes it canonical.
+__device__ __forceinline__ u64 dot30_fold(const Dot30& A, u64 q) {
+    const uint32_t d = (uint32_t)((1ull << 60) - q);
+    const u64 H = A.a2 + (A.a1 >> 30);
+    const u64 F = (u64)(uint32_t)(H >> 32) * d;
+    u64 x = A.a0 + (u64)(uint32_t)H * d;
+    x += (A.a1 & M30) << 30;
+    x += (F & ((1ull << 28) - 1)) << 32;
+    x += (u64)(uint32_t)(F >> 28) * d;
+    return reduce_near60(x, q);
+}
+
 // Balanced gadget digits of the centred CRT value of residues res[0..L) (mod Q).
 // keyswitch.rs:24-44 literally (truncating %, [-B/2, B/2) adjustment, final carry dropped),
 // on the exact value (extension semantics for Q >= 2^64; identical to rns.rs:114-151 below).
@@ -258,6 +295,75 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
     }
 }
 
+// int16 gadget digits (base 2^sh, sh | 32) of the centred CRT value of canonical residues res,
+// the same digits as gadget_digits (keyswitch.rs:24-44: truncating %, [-B/2, B/2) adjustment,
+// final carry dropped).  gadget_digits adds each balancing carry back into the multiword
+// magnitude; here it is a 1-bit carry c added to the next raw field instead: r = field + c lies in
+// [0, B], and r == B (the carry rippling through a field of ones) gives digit 0 with carry 1 under
+// the same rule, exactly as the multiword increment does.  The fields are read from the 32-bit
+// words of the magnitude in place: no multiword shift or add per digit.  Digit g goes to
+// D16[g * n].
+template <int LT>
+__device__ __forceinline__ void gadget_digits16_sp(const u64 (&res)[EXACTO_MAX_L], const CrtTables* __restrict__ C,
+                                                   const PrimeConst* __restrict__ primes, int n, int guse,
+                                                   int16_t* D16) {
+    constexpr int L = LT;
+    u64 z[EXACTO_MAX_L];
+    garner_q_fast<LT>(z, res, L, C, primes);
+    const bool neg = mr_greater<EXACTO_MAX_L>(z, C->halfQ_mr, L);
+    u64 M[L];
+    M[0] = z[L - 1];
+#pragma unroll
+    for (int w = 1; w < L; ++w) M[w] = 0;
+#pragma unroll
+    for (int k = L - 2; k >= 0; --k) {
+        const u64 qk = primes[k].q;
+        u64 carry = z[k];
+#pragma unroll
+        for (int w = 0; w < L; ++w) {
+            const u128 t = (u128)M[w] * qk + carry;
+            M[w] = (u64)t;
+            carry = (u64)(t >> 64);
+        }
+    }
+    if (neg) {  // magnitude Q - x
+        u64 borrow = 0;
+#pragma unroll
+        for (int w = 0; w < L; ++w) {
+            const u64 a = C->Qwords[w], b = M[w];
+            const u64 d1 = a - b;
+            const u64 b1 = a < b;
+            const u64 d2 = d1 - borrow;
+            const u64 b2 = d1 < borrow;
+            M[w] = d2;
+            borrow = b1 | b2;
+        }
+    }
+    const int sh = C->gshift;
+    const uint32_t B = 1u << sh, mask = B - 1;
+    // !neg: r >= B/2 balances down; neg: r > B/2 does (the digit then takes the other sign)
+    const uint32_t thr = (B >> 1) - (neg ? 0u : 1u);
+    const int sgn = neg ? -1 : 0;
+    uint32_t c = 0;
+    int g = 0;
+#pragma unroll
+    for (int w = 0; w < 2 * L; ++w) {
+        const uint32_t word = (w & 1) ? (uint32_t)(M[w >> 1] >> 32) : (uint32_t)M[w >> 1];
+        for (int o = 0; o < 32 && g < guse; o += sh, ++g) {
+            const uint32_t r = ((word >> o) & mask) + c;
+            c = r > thr ? 1u : 0u;
+            const int dv = (int)r - (int)(c << sh);
+            D16[(long)g * n] = (int16_t)((dv ^ sgn) - sgn);
+        }
+    }
+    for (; g < guse; ++g) {   // past the magnitude's words: only the carry remains
+        const uint32_t r = c;
+        c = r > thr ? 1u : 0u;
+        const int dv = (int)r - (int)(c << sh);
+        D16[(long)g * n] = (int16_t)((dv ^ sgn) - sgn);
+    }
+}
+
 // ---------------------------------------------------------------- exact lift Q -> P
 
 template <bool NEAR, bool FAST, int LT, int KT, bool SP = false>
@@ -284,10 +390,62 @@ exact_lift_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
     }
 }
 
+// SP, K = L + 1: extP_a = sum_k v_k (q_0 .. q_{k-1}) - neg Q  mod p_a as one 30-bit-limb dot
+// product per auxiliary prime (the constant -Q folded into the accumulator).
+template <int LT>
+__global__ void __launch_bounds__(TPB)
+exact_lift_sp_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n,
+                     const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    constexpr int L = LT, K = LT + 1;
+    u64 x[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) x[i] = coefQ[(row * L + i) * n + j];
+    garner_q_fast<LT>(v, x, L, C, primes);
+    const bool neg = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+    uint32_t v0[L], v1[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        v0[k] = (uint32_t)v[k] & M30;
+        v1[k] = (uint32_t)(v[k] >> 30);
+    }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const int t = L + a;
+        const u64 pa = primes[t].q;
+        Dot30 A{neg ? pa - C->qpref_w[L][t] : 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < L; ++k) dot30_mac(A, v0[k], v1[k], C->qpref_w[k][t]);
+        extP[(row * K + a) * n + j] = dot30_fold(A, pa);
+    }
+}
+
+// EXACTO_DOT30=0 keeps the Shoup-per-term SP kernels (A/B switch)
+static bool use_dot30() {
+    static const bool on = [] {
+        const char* e = std::getenv("EXACTO_DOT30");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtTables* ct,
                        const PrimeConst* primes, int L, int K, int mode, hipStream_t s) {
     const long blocks = rows * blocks_per_row(n);
     if (blocks == 0) return;
+    if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
+#define LIFT30(LT) hipLaunchKernelGGL((exact_lift_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, ct, primes)
+        switch (L) {
+            case 1: LIFT30(1); break;
+            case 2: LIFT30(2); break;
+            case 3: LIFT30(3); break;
+            case 4: LIFT30(4); break;
+            case 5: LIFT30(5); break;
+            default: LIFT30(6); break;
+        }
+#undef LIFT30
+        return;
+    }
 #define LIFT(NR, FS, LT, KT)                                                                                     \
     hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
                        primes)
@@ -438,11 +596,108 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
         gadget_digits<NEAR, LT>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
 }
 
+// SP, K = L + 1: exact_scale_kernel with every modular dot product as a 30-bit-limb dot:
+//   r_a = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs        mod p_a   (then Garner over P)
+//   res_i = sum_a w_a (p_0 .. p_{a-1}) + negr (q_i - P mod q_i)    mod q_i
+// and int16 gadget digits by gadget_digits16_sp.
+template <int LT, int DIG>
+__global__ void __launch_bounds__(TPB)
+exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
+                      u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n,
+                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    constexpr int L = LT, K = LT + 1, NP = L + K;
+    const long item = row / 3;
+    const int comp = (int)(row - item * 3);
+    const u64* Tin = T + row * NP * n + j;
+    u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
+    garner_q_fast<LT>(v, u, L, C, primes);
+    const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+    uint32_t v0[L], v1[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        v0[k] = (uint32_t)v[k] & M30;
+        v1[k] = (uint32_t)(v[k] >> 30);
+    }
+    u64 w[EXACTO_MAX_K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const u64 pa = primes[L + a].q, np = (u64)0 - pa;
+        const u64 ta = Tin[(long)(L + a) * n];   // canonical (the inverse tensor's last stage)
+        Dot30 A{negs ? 1ull : 0ull, 0, 0};
+        dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->pq_w[a]);
+#pragma unroll
+        for (int k = 0; k < L; ++k) dot30_mac(A, v0[k], v1[k], pa - C->qpq_w[k][a]);
+        u64 acc = dot30_fold(A, pa);
+        // Garner over P on the fly; w_k < p_k < 2 p_a
+#pragma unroll
+        for (int k = 0; k < a; ++k) acc = shoup_mul_nq(acc + 2 * pa - w[k], C->gp_w[a][k], C->gp_ws[a][k], np);
+        w[a] = (a > 0 && acc >= pa) ? acc - pa : acc;
+    }
+    const bool negr = mr_greater<EXACTO_MAX_K>(w, C->halfP_mr, K);
+    uint32_t w0[K], w1[K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        w0[a] = (uint32_t)w[a] & M30;
+        w1[a] = (uint32_t)(w[a] >> 30);
+    }
+    u64 res[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const u64 q = primes[i].q;
+        Dot30 A{negr ? q - C->ppref_w[K][i] : 0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < K; ++a) dot30_mac(A, w0[a], w1[a], C->ppref_w[a][i]);
+        res[i] = dot30_fold(A, q);
+    }
+    if (comp < ncomp_r) {
+        u64* out = R + item * r_stride + (long)comp * L * n + j;
+#pragma unroll
+        for (int i = 0; i < L; ++i) out[(long)i * n] = res[i];
+    }
+    if (comp != 2) return;
+    if constexpr (DIG == 1) {
+        gadget_digits16_sp<LT>(res, C, primes, n, guse, D16 + item * (long)guse * n + j);
+    } else if constexpr (DIG == 2) {
+        if (D16 != nullptr)
+            gadget_digits<true, LT>(res, L, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
+        else
+            gadget_digits<true, LT>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
+    }
+}
+
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s) {
+                        int K, int mode, hipStream_t s, int gshift) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
+    if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
+        // digit code: 0 none, 1 int16 fields of the magnitude (base 2^sh, sh | 32), 2 gadget_digits
+        const int dig = (D16 == nullptr && D == nullptr) || guse <= 0 ? 0
+                        : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? 1 : 2;
+#define SCALE30_(LT, DG)                                                                                        \
+    hipLaunchKernelGGL((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
+                       D16, guse, n, ct, primes)
+#define SCALE30(LT)                         \
+    do {                                    \
+        if (dig == 1) SCALE30_(LT, 1);      \
+        else if (dig == 2) SCALE30_(LT, 2); \
+        else SCALE30_(LT, 0);               \
+    } while (0)
+        switch (L) {
+            case 1: SCALE30(1); break;
+            case 2: SCALE30(2); break;
+            case 3: SCALE30(3); break;
+            case 4: SCALE30(4); break;
+            case 5: SCALE30(5); break;
+            default: SCALE30(6); break;
+        }
+#undef SCALE30
+#undef SCALE30_
+        return;
+    }
 #define SCALE(NR, FS, LT, KT)                                                                                    \
     hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
                        D, D16, guse, n, L, K, ct, primes)
