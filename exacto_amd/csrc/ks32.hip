@@ -103,15 +103,20 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
     if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1>(x, lds, tid, tw, p);
 }
 
-// x (element tid + k T) -> NTT, canonical, stored coalesced at dst (element tid + k T of the
-// bit-reversed-order evaluation array)
+// x (element tid + k T) -> NTT, stored coalesced at dst (element tid + k T of the
+// bit-reversed-order evaluation array), as balanced residues in (-p/2, p/2] (int32 bits): the
+// only consumer, ks32_mac_kernel, multiplies balanced values
 template <int LOGN>
 __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P,
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     fwd32_rounds<LOGN, 0>(x, lds, tid, P.tw_fwd, P.p);
+    const uint32_t half = P.p >> 1;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = red32(x[k], P.p);
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t v = red32(x[k], P.p);
+        x[k] = v > half ? v - P.p : v;
+    }
     lds_sync();
     lds32_store<0>(lds, x, tid);
     lds_sync();
@@ -230,23 +235,30 @@ __device__ __forceinline__ uint32_t red_s64(long long x, const Prime32& P) {
     return red32(red32(a + b + P.k63, 2 * p), p);    // a + b + k63 < 3p < 2^32
 }
 
-__device__ __forceinline__ int balanced32(uint32_t v, uint32_t p) { return v > (p >> 1) ? (int)(v - p) : (int)v; }
+// Signed 64-bit x (|x| < 2^63) -> a small non-negative value == x mod p, below 3p + 2^32 < 2^33.2:
+// (hi + 2^31) 2^32 by Shoup with 2^32 mod p, plus lo, plus (-2^63) mod p.  Carried between runs
+// of signed products (7 VALU instead of red_s64's full reduction).
+__device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P) {
+    const uint32_t hu = (uint32_t)((unsigned long long)x >> 32) ^ 0x80000000u;
+    const uint32_t a = shoup32(hu, P.c32, P.c32s, P.p);
+    return (long long)((unsigned long long)a + (uint32_t)x + P.k63);
+}
 
 // U[item][cl][s][j] = sum_g DS[item][g][s][j] * RS[g][cl][s][j] mod p_s   (cl = c * L + l)
 // Block: 64 coefficients j of one prime s, CLB consecutive (c, l) pairs starting at cl0, and up to
-// KS_IG items; its key words (G * CLB * 64, balanced) are staged in LDS once.  Lane = coefficient,
-// wave w handles items it0 + w, it0 + w + 4, ...  Digit residue and key are both balanced,
-// |product| < (p/2)^2 < 2^59.1, so twelve signed products and the carried residue stay below 2^63
-// (one v_mad_i64_i32 each) before a reduction.
+// 4 NW items; its key words (G * CLB * 64, balanced) are staged in LDS once.  Lane = coefficient,
+// wave w handles items it0 + w, it0 + w + NW, ...  Digit residues and key are stored balanced by
+// their transforms, |product| < (p/2)^2 < 2^58.9, so twelve signed products plus the carried
+// value (< 2^33.2) stay below 2^63 (one v_mad_i64_i32 each) before a lazy reduction.
 constexpr int KS_LS = 64;
-constexpr int KS_IG = 16;   // items per block: more, shorter blocks keep more loads in flight
 constexpr int KS_RUN = 12;  // signed products summed between reductions
 
-template <int CLB>
-__global__ void __launch_bounds__(256)
-ks32_mac_kernel(const uint32_t* __restrict__ DS, const uint32_t* __restrict__ RS, uint32_t* __restrict__ U,
+template <int CLB, int NW>
+__global__ void __launch_bounds__(NW * 64)
+ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t* __restrict__ U,
                 int G, int CL, int S, int items, int n, const Prime32* __restrict__ primes) {
     extern __shared__ int kl[];                // [g][cl - cl0][lane]
+    constexpr int IG = 4 * NW;                 // items per block
     const int lane = threadIdx.x & (KS_LS - 1), wave = threadIdx.x / KS_LS;
     const int nb = n / KS_LS;
     const int jb = blockIdx.x % nb;
@@ -254,26 +266,24 @@ ks32_mac_kernel(const uint32_t* __restrict__ DS, const uint32_t* __restrict__ RS
     const int cl0 = (blockIdx.x / (nb * S)) * CLB;
     const int j = jb * KS_LS + lane;
     const Prime32& P = primes[s];
-    const uint32_t p = P.p;
-    for (int r = threadIdx.x; r < G * CLB * KS_LS; r += 256) {
+    for (int r = threadIdx.x; r < G * CLB * KS_LS; r += NW * 64) {
         const int g = r / (CLB * KS_LS), c = (r / KS_LS) % CLB, t = r & (KS_LS - 1);
-        kl[r] = balanced32(RS[(((long)g * CL + cl0 + c) * S + s) * n + jb * KS_LS + t], p);
+        kl[r] = RS[(((long)g * CL + cl0 + c) * S + s) * n + jb * KS_LS + t];
     }
     __syncthreads();
-    const int it_end = min(items, (int)(blockIdx.y + 1) * KS_IG);
-    for (int it = blockIdx.y * KS_IG + wave; it < it_end; it += 256 / KS_LS) {
-        const uint32_t* dp = DS + ((long)it * G * S + s) * n + j;
+    const int it_end = min(items, (int)(blockIdx.y + 1) * IG);
+    for (int it = blockIdx.y * IG + wave; it < it_end; it += NW) {
+        const int* dp = DS + ((long)it * G * S + s) * n + j;
         long long acc[CLB];
 #pragma unroll
         for (int c = 0; c < CLB; ++c) acc[c] = 0;
         for (int g0 = 0; g0 < G; g0 += KS_RUN) {
             // unconditional (clamped) loads, all in flight together; digits past G are zeroed after
-            uint32_t raw[KS_RUN];
-#pragma unroll
-            for (int e = 0; e < KS_RUN; ++e) raw[e] = dp[(long)min(g0 + e, G - 1) * S * n];
             int d[KS_RUN];
 #pragma unroll
-            for (int e = 0; e < KS_RUN; ++e) d[e] = g0 + e < G ? balanced32(raw[e], p) : 0;
+            for (int e = 0; e < KS_RUN; ++e) d[e] = dp[(long)min(g0 + e, G - 1) * S * n];
+#pragma unroll
+            for (int e = 0; e < KS_RUN; ++e) d[e] = g0 + e < G ? d[e] : 0;
 #pragma unroll
             for (int e = 0; e < KS_RUN; ++e) {
                 const int* kg = kl + (min(g0 + e, G - 1) * CLB) * KS_LS + lane;
@@ -282,7 +292,7 @@ ks32_mac_kernel(const uint32_t* __restrict__ DS, const uint32_t* __restrict__ RS
             }
             if (g0 + KS_RUN < G) {
 #pragma unroll
-                for (int c = 0; c < CLB; ++c) acc[c] = red_s64(acc[c], P);
+                for (int c = 0; c < CLB; ++c) acc[c] = red_s64_lazy(acc[c], P);
             }
         }
 #pragma unroll
@@ -427,12 +437,17 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
     if (items <= 0) return;
     const int CL = 2 * L;
     // (c, l) pairs per block: the largest divisor of 2L whose key slice (G * CLB * 64 words) fits
-    // 32 KiB of LDS
+    // 64 KiB of LDS, so the digits are read once per pair group (once at every BASELINE config);
+    // a slice above 32 KiB leaves room for 2 blocks per CU, which then get 8 waves each
     int CLB = CL;
-    while (CLB > 1 && (CL % CLB != 0 || (size_t)G * CLB * KS_LS * sizeof(int) > 32768)) --CLB;
-    const dim3 grid((unsigned)((n / KS_LS) * S * (CL / CLB)), (unsigned)((items + KS_IG - 1) / KS_IG));
+    while (CLB > 1 && (CL % CLB != 0 || (size_t)G * CLB * KS_LS * sizeof(int) > 65536)) --CLB;
     const size_t lds = (size_t)G * CLB * KS_LS * sizeof(int);
-#define MAC(C_) hipLaunchKernelGGL((ks32_mac_kernel<C_>), grid, dim3(256), lds, st, DS, RS, U, G, CL, S, items, n, primes)
+    const int NW = lds > 32768 ? 8 : 4;
+    const dim3 grid((unsigned)((n / KS_LS) * S * (CL / CLB)), (unsigned)((items + 4 * NW - 1) / (4 * NW)));
+    const int* ds = reinterpret_cast<const int*>(DS);
+    const int* rs = reinterpret_cast<const int*>(RS);
+#define MAC_(C_, W_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
+#define MAC(C_) do { if (NW == 8) MAC_(C_, 8); else MAC_(C_, 4); } while (0)
     switch (CLB) {
         case 8: MAC(8); break;
         case 6: MAC(6); break;
@@ -442,6 +457,7 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
         default: MAC(1); break;
     }
 #undef MAC
+#undef MAC_
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,

@@ -800,11 +800,23 @@ __device__ __forceinline__ u64 mulmod_near60(u64 a, u64 b, uint32_t d) {
     return L2 + H2 * d;
 }
 
+// Block b -> logical index, so that each group of G consecutive logical indices runs on one XCD
+// in consecutive dispatch slots (workgroups go to XCDs round robin, b % 8: a placement used for
+// speed only, never for correctness).  Bijective on [0, total); a tail that does not fill 8
+// groups keeps the identity.
+__device__ __forceinline__ long xcd_group_remap(long b, long total, int G) {
+    const long span = 8L * G;
+    const long full = total / span * span;
+    if (b >= full) return b;
+    const long x = b & 7, slot = b >> 3;
+    return ((slot / G) * 8 + x) * G + slot % G;
+}
+
 template <int LOGN, bool LAZY, bool ASM = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                      const PrimeConst* __restrict__ primes) {
+                      const PrimeConst* __restrict__ primes, int remap) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
@@ -812,10 +824,12 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
     const int NP = L + K;
-    const long p = blockIdx.x;
+    // the three components of one (item, prime) read overlapping inputs (c1 reads c0's and c2's):
+    // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
+    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
     const long item = p / (3 * NP);
     const int rem = (int)(p - item * 3 * NP);
-    const int c = rem / NP, t = rem - c * NP;
+    const int t = rem / 3, c = rem - t * 3;
     const PrimeConst& P = primes[t];
     const u64 *A0, *A1, *B0, *B1;
     if (t < L) {
@@ -872,7 +886,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
-    u64* dst = Tout + p * N;
+    u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
@@ -1003,19 +1017,21 @@ template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false) {
     constexpr int threads = (1 << LOGN) / 16;
+    // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
+    static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv) {
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(blocks), dim3(threads), 0, s, op, extP,
-                               T, L, K, primes);
+                               T, L, K, primes, remap);
             return;
         }
     }
     if (lazy)
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L, K,
-                           primes);
+                           primes, remap);
     else
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L,
-                           K, primes);
+                           K, primes, remap);
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
