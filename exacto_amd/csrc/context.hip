@@ -232,6 +232,8 @@ struct exacto_ctx {
     size_t enc_cap = 0;
     u64* gk_s = nullptr;  // Shoup companions of the Galois key of the last automorphism call
     size_t gk_s_cap = 0;
+    uint32_t* d_gk_rs = nullptr;  // ks32: Galois key of the last automorphism call in the 31-bit basis
+    size_t gk_rs_cap = 0;
     u64* pl_buf = nullptr;  // lifted plaintexts / monomial scratch
     size_t pl_cap = 0;
     u64 *ext_a = nullptr, *ext_b = nullptr;
@@ -693,7 +695,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->pl_buf);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
@@ -929,24 +931,32 @@ static int crt_mode(const exacto_ctx* c) {
     return c->h_crt.special ? 3 : c->h_crt.fast ? 2 : c->h_crt.near ? 1 : 0;
 }
 
-// The resident relinearisation key in ks32's auxiliary basis: INTT mod q_l (coefficient domain),
-// balanced, reduced mod each p_s, forward NTT mod p_s -> d_rs [keys][2L][S][n].  Once per key.
-static int ensure_rs(exacto_ctx* c) {
-    if (c->rs_valid) return 0;
-    const long rows = (long)c->rlk_keys * 2 * c->L;
-    size_t cap = c->rs_cap;
-    if (grow((u64**)&c->d_rs, &cap, std::max<size_t>((size_t)rows * c->S32 * c->n * sizeof(uint32_t), 8)))
+// A key [keys][2][L][n] (NTT domain mod q_l) in ks32's auxiliary basis: INTT mod q_l
+// (coefficient domain), balanced, reduced mod each p_s, forward NTT mod p_s -> dst [keys][2L][S][n]
+// (grown as needed).
+static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t** dst, size_t* cap) {
+    const long rows = (long)keys * 2 * c->L;
+    if (grow((u64**)dst, cap, std::max<size_t>((size_t)rows * c->S32 * c->n * sizeof(uint32_t), 8)))
         return EXACTO_ERR_HIP;
-    c->rs_cap = cap;
     Scratch ks;
     HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream));
     NttBatch nb{};
-    nb.src = c->d_rlk; nb.src_item_stride = 2L * c->L * c->n;
+    nb.src = key; nb.src_item_stride = 2L * c->L * c->n;
     nb.dst = ks.as<u64>(); nb.dst_item_stride = 2L * c->L * c->n;
     nb.ppi = 2 * c->L; nb.prime_base = 0; nb.period = c->L;
     if (int e = run_ntt(c, nb, rows, true)) return e;
-    ks32_key(ks.as<u64>(), c->d_rs, rows, c->L, c->S32, c->logn, c->d_p32, c->d_primes, c->stream);
+    ks32_key(ks.as<u64>(), *dst, rows, c->L, c->S32, c->logn, c->d_p32, c->d_primes, c->stream);
     CHECK_LAUNCH();
+    return 0;
+}
+
+// The resident relinearisation key in ks32's basis (d_rs).  Once per key.
+static int ensure_rs(exacto_ctx* c) {
+    if (c->rs_valid) return 0;
+    size_t cap = c->rs_cap;
+    const int e = ks32_convert_key(c, c->d_rlk, c->rlk_keys, &c->d_rs, &cap);
+    c->rs_cap = cap;
+    if (e) return e;
     c->rs_valid = true;
     return 0;
 }
@@ -1865,11 +1875,22 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
     const long Ln = (long)L * n;
     const int guse = (int)std::min<size_t>(c->G, num_keys);
     const size_t count = (size_t)guse * 2 * Ln;
-    size_t cap = c->gk_s_cap;
-    if (grow(&c->gk_s, &cap, count * sizeof(u64))) return EXACTO_ERR_HIP;
-    c->gk_s_cap = cap;
-    launch_shoup_companions(gk, c->gk_s, (long)count, n, L, c->d_primes, c->stream);
-    CHECK_LAUNCH();
+    const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
+    // ks32 key switch (as run_mul): the key converted to the 31-bit basis on every call (the
+    // caller may pass a different key in the same buffer), G L (2L) 60-bit (32-bit) transforms
+    const bool k32 = d16 && c->ks32 && c->S32 > 0 && c->path == EXACTO_PATH_EXACT_RNS;
+    if (k32) {
+        size_t cap = c->gk_rs_cap;
+        const int e = ks32_convert_key(c, gk, (size_t)guse, &c->d_gk_rs, &cap);
+        c->gk_rs_cap = cap;
+        if (e) return e;
+    } else {
+        size_t cap = c->gk_s_cap;
+        if (grow(&c->gk_s, &cap, count * sizeof(u64))) return EXACTO_ERR_HIP;
+        c->gk_s_cap = cap;
+        launch_shoup_companions(gk, c->gk_s, (long)count, n, L, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+    }
     const size_t C = std::min<size_t>(c->chunk, B);
     if (int e = ensure_workspace(c, C)) return e;
     for (size_t s0 = 0; s0 < B; s0 += C) {
@@ -1883,13 +1904,31 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
         if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
         launch_automorph(c->ws_coefQ, 2 * Ln, c->ws_T, 2 * Ln, cnt, 2, n, L, element, c->d_primes, -1, c->stream);
         CHECK_LAUNCH();
+        if (k32) {
+            // digits of sigma(c1); sum_g d_g * r_g over the integers added to (sigma(c0), 0) in the
+            // coefficient domain; then both components forward
+            launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream,
+                             c->ws_D16);
+            CHECK_LAUNCH();
+            launch_rows(c->ws_T + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
+            CHECK_LAUNCH();
+            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
+            ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
+            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
+            CHECK_LAUNCH();
+            NttBatch rb{};
+            rb.src = c->ws_T; rb.src_item_stride = 2 * Ln;
+            rb.dst = dst; rb.dst_item_stride = 2 * Ln;
+            rb.ppi = 2 * L; rb.prime_base = 0; rb.period = L;
+            if (int e = run_ntt(c, rb, (long)cnt * 2 * L, false)) return e;
+            continue;
+        }
         NttBatch c0{};
         c0.src = c->ws_T; c0.src_item_stride = 2 * Ln;
         c0.dst = dst; c0.dst_item_stride = 2 * Ln;
         c0.ppi = L; c0.prime_base = 0; c0.period = L;
         if (int e = run_ntt(c, c0, (long)cnt * L, false)) return e;
         launch_rows(dst + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
-        const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
         launch_decompose(c->ws_T + Ln, 2 * Ln, c->ws_D, guse, cnt, n, c->d_crt, c->d_primes, L, c->stream,
                          d16 ? c->ws_D16 : nullptr);
         CHECK_LAUNCH();

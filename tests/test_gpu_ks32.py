@@ -75,3 +75,27 @@ def test_ks32_key_reload(gpu_available):
         ctx.load_relin_key(k)
         ref.load_relin_key(k)
         assert np.array_equal(ctx.bfv_mul_and_relin(ct1, ct2), ref.bfv_mul_and_relin(ct1, ct2))
+
+
+@pytest.mark.parametrize("n,which,B,keys,chunk", [
+    (1024, "cfg3", 3, None, 0),
+    (4096, "cfg3", 5, None, 2),        # 3 chunks
+    (4096, "cfg3", 2, 5, 0),           # fewer Galois key digits than G (eval.rs:540-548)
+    (8192, "cfg5", 2, None, 0),
+])
+def test_ks32_automorphism_matches_limbwise(gpu_available, n, which, B, keys, chunk):
+    """bfv_apply_automorphism (eval.rs:512-561) with the ks32 key switch against the limb-wise
+    60-bit MAC, for an odd and the conjugation element, and a new key in every call."""
+    prm = P.cfg3_params(n) if which == "cfg3" else P.cfg5_params(n).bfv_params
+    q = prm.ct_basis.moduli
+    rng = np.random.default_rng(3 * n + B)
+    ct = uniform_residues(rng, (B, 2), q, n)
+    ct[0, 1] = np.array(q, dtype=np.uint64)[:, None] - 1
+    ctxs = [_ctx(prm, True, chunk), _ctx(prm, False, chunk)]
+    for element in (5, 2 * n - 1):
+        gk = uniform_residues(rng, (keys or prm.gadget_digits, 2), q, n)
+        got, want = (c.bfv_apply_automorphism(ct, element, gk) for c in ctxs)
+        assert np.array_equal(got, want), (n, element)
+        if n <= 1024:
+            keyset = obfv.GaloisKey(np_to_rlk(gk, prm).keys, element, prm)
+            assert np.array_equal(got[0], ct_to_np(obfv.bfv_apply_automorphism(np_to_ct(ct[0], prm), keyset)))
