@@ -971,7 +971,12 @@ static bool lazy_ok(const exacto_ctx* c, int base, int period) {
 
 // products [0, P): ct1 = op.a + off_a(p), ct2 = op.b + off_b(p) (each [2][L][n], NTT domain).
 // relin: out[p] = [2][L][n] = relinearize(mul_no_relin); else out[p] = [3][L][n].
-static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out_stride, bool relin) {
+// coef (optional): when the key switch runs over the integers (ks32), the last forward NTT is left
+// to the caller and *coef is set: out then holds the coefficient domain (a caller that first sums
+// products, as dbfv_mul does, transforms the sums instead of every product).
+static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out_stride, bool relin,
+                   bool* coef = nullptr) {
+    if (coef) *coef = false;
     if (c->deferred_code) return fail(c->deferred_code, c->deferred_msg);
     if (relin && !c->rlk_loaded) return fail(EXACTO_ERR_MISSING_KEY, "key not available: relinearization key not loaded");
     if (P <= 0) return 0;
@@ -985,6 +990,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                      c->gbase <= 65536;
     // ... and then the key switch runs over the integers in the 31-bit basis (ks32.hip)
     const bool k32 = d16 && c->ks32 && c->S32 > 0;
+    const bool skip_fwd = coef && k32;
+    if (skip_fwd) *coef = true;
     if (relin && guse > 0) {
         // both before the second lane forks: its kernels read these too
         if (int e = k32 ? ensure_rs(c) : ensure_rlk_companions(c)) return e;
@@ -1072,6 +1079,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
             CHECK_LAUNCH();
         }
+        if (skip_fwd) continue;
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
         if (relin && guse > 0 && !k32) {
             NttBatch db = contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n);
@@ -1442,10 +1450,17 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
         op.ea = c->ext_a; op.ea_off = c->d_off + 2 * BP;
         op.eb = c->ext_b; op.eb_off = c->d_off + 3 * BP;
     }
-    if (int e = run_mul(c, op, P, c->prod, Ln2, true)) return e;
+    // the per-limb sums (dbfv/eval.rs:124-132) and the degree reduction are linear, so with ks32 they
+    // run on the products' coefficient-domain results and only the d output limbs are transformed
+    // (B d 2L forward NTTs instead of B npairs 2L)
+    bool coef = false;
+    if (int e = run_mul(c, op, P, c->prod, Ln2, true, &coef)) return e;
     launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
                         c->stream);
     CHECK_LAUNCH();
+    if (coef)
+        if (int e = run_ntt(c, contiguous(out, (long)B * d, 2L * c->L, 0, c->L, c->n), (long)B * d * 2 * c->L, false))
+            return e;
     return 0;
 }
 

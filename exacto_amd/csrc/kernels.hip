@@ -22,10 +22,13 @@ static constexpr int TPB = 256;
 
 static inline int blocks_per_row(int n) { return (n + TPB - 1) / TPB; }
 
-#define ROW_SETUP(n)                                        \
-    const int nblk = (n + TPB - 1) / TPB;                   \
-    const long row = blockIdx.x / nblk;                     \
-    const int j = (blockIdx.x - row * nblk) * TPB + threadIdx.x; \
+// n is a power of two: blocks per row too (1 below TPB), so row and column are a shift and a
+// mask of the block index (SALU), not a division
+#define ROW_SETUP(n)                                                   \
+    const int nblk = (n + TPB - 1) / TPB;                              \
+    const int nsh = __builtin_ctz((unsigned)nblk);                     \
+    const long row = (long)(blockIdx.x >> nsh);                        \
+    const int j = (int)(blockIdx.x & (unsigned)(nblk - 1)) * TPB + threadIdx.x; \
     if (j >= (n)) return;
 
 // ---------------------------------------------------------------- mixed radix helpers

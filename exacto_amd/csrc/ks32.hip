@@ -181,9 +181,9 @@ ks32_digit_ntt_kernel(const int16_t* __restrict__ D16, uint32_t* __restrict__ DS
     constexpr int N = 1 << LOGN, T = N / 16;
     __shared__ uint32_t lds[N];
     const int tid = threadIdx.x;
-    const long b = blockIdx.x;                 // (item, g, s)
-    const int s = (int)(b % S);
-    const long ig = b / S;                     // item * G + g
+    const uint32_t b = blockIdx.x;             // (item, g, s)
+    const int s = (int)(b % (uint32_t)S);
+    const long ig = b / (uint32_t)S;           // item * G + g
     const Prime32& P = primes[s];
     const int16_t* src = D16 + ig * N;
     uint32_t x[16];
@@ -192,7 +192,7 @@ ks32_digit_ntt_kernel(const int16_t* __restrict__ D16, uint32_t* __restrict__ DS
         const int d = src[tid + k * T];
         x[k] = d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
     }
-    fwd32_store<LOGN>(x, lds, tid, P, DS + b * N);
+    fwd32_store<LOGN>(x, lds, tid, P, DS + (long)b * N);
 }
 
 // key rows [rows][n] canonical mod q_{row's limb} (u64) -> RS [rows][S][n]: balanced, mod p_s, NTT
@@ -203,13 +203,13 @@ ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int
     constexpr int N = 1 << LOGN, T = N / 16;
     __shared__ uint32_t lds[N];
     const int tid = threadIdx.x;
-    const long b = blockIdx.x;                 // (row, s), row = (g * 2 + c) * L + l
-    const int s = (int)(b % S);
-    const long row = b / S;
-    const int l = (int)(row % L);
+    const uint32_t b = blockIdx.x;             // (row, s), row = (g * 2 + c) * L + l
+    const int s = (int)(b % (uint32_t)S);
+    const uint32_t row = b / (uint32_t)S;
+    const int l = (int)(row % (uint32_t)L);
     const Prime32& P = primes[s];
     const u64 q = qprimes[l].q, half = q >> 1;
-    const u64* src = K + row * N;
+    const u64* src = K + (long)row * N;
     uint32_t x[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -222,7 +222,7 @@ ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int
             x[k] = (uint32_t)(r % P.p);
         }
     }
-    fwd32_store<LOGN>(x, lds, tid, P, RS + b * N);
+    fwd32_store<LOGN>(x, lds, tid, P, RS + (long)b * N);
 }
 
 // Signed 64-bit x -> x mod p, canonical (p in (2^30, 2^32 / 3)): x = hi 2^32 + lo with hi signed;
@@ -313,15 +313,15 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     constexpr int N = 1 << LOGN, T = N / 16;
     __shared__ uint32_t lds[N];
     const int tid = threadIdx.x;
-    const long b = blockIdx.x;                 // (item, cl)
-    const int CL = 2 * L;
+    const uint32_t b = blockIdx.x;             // (item, cl)
+    const uint32_t CL = 2 * L;
     const long item = b / CL;
-    const int cl = (int)(b - item * CL);
+    const int cl = (int)(b - (uint32_t)item * CL);
     const int l = cl % L;
     uint32_t v[S][16];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const uint4* src = reinterpret_cast<const uint4*>(U + (b * S + s) * N + 16 * tid);
+        const uint4* src = reinterpret_cast<const uint4*>(U + ((long)b * S + s) * N + 16 * tid);
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
             const uint4 w = src[h];
