@@ -194,6 +194,10 @@ struct exacto_ctx {
     // limb-wise 60-bit digit NTTs + relin_mac)
     bool ks32 = true;
     int S32 = 0;                 // 0: not eligible for these parameters
+    int ks32_sum_max = 0;        // key-switch sums that may be added before one lift (prod p bound)
+    uint32_t* ks_defer = nullptr;  // run_mul: MAC results of product p to ks_defer + p 2L S n, no lift
+    uint32_t *d_uall = nullptr, *d_uk = nullptr;  // dBFV: per-product and per-limb ks32 sums
+    size_t uall_cap = 0, uk_cap = 0;
     Prime32* d_p32 = nullptr;
     uint2* d_tw32 = nullptr;
     Ks32Tables* d_kst = nullptr;
@@ -255,6 +259,7 @@ struct exacto_ctx {
     size_t cached_B = 0, cached_d = 0;
     u64 cached_base = 0, cached_p = 0;
     int cached_npairs = 0;
+    int cached_sum_m = 0;        // max products per dBFV output limb when all combine terms are sums, else -1
     int* d_term_start = nullptr;
     CombineTerm* d_terms = nullptr;
     size_t terms_cap = 0;
@@ -384,6 +389,18 @@ static int setup_ks32(exacto_ctx* c) {
         if (P.cmp(bound) > 0) break;
     }
     if (P.cmp(bound) <= 0 || ps.size() < 2) return 0;
+    // how many such sums the basis lifts exactly when added first (dBFV output limbs)
+    c->ks32_sum_max = 1;
+    for (u64 m = 2; m <= 64; ++m) {
+        Big bm((u64)c->G);
+        bm.mul((u64)c->n);
+        bm.mul(c->gbase / 2);
+        bm.mul(qmax / 2);
+        bm.mul(2 * m);
+        bm.add(1);
+        if (P.cmp(bm) <= 0) break;
+        c->ks32_sum_max = (int)m;
+    }
     const int S = (int)ps.size(), n = c->n;
     std::vector<uint2> tw((size_t)S * 2 * n);
     std::vector<Prime32> pc(S);
@@ -695,7 +712,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
     free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->pl_buf);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_uall); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
@@ -1075,8 +1092,14 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // key in the same basis, inverse NTT + centred lift, added to R mod q_l in the
             // coefficient domain; the forward NTT of R below then yields the relinearised result
             ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-            ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
-            ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
+            if (c->ks_defer) {   // the caller sums products first and lifts once (dbfv_mul_core)
+                ks32_mac(c->ws_DS, c->d_rs, c->ks_defer + s * 2L * L * c->S32 * n, cnt, guse, L, c->S32, n,
+                         c->d_p32, c->stream);
+            } else {
+                ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
+                ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
+                         c->stream);
+            }
             CHECK_LAUNCH();
         }
         if (skip_fwd) continue;
@@ -1354,6 +1377,10 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
         }
     }
     start[d] = (int)terms.size();
+    // ks32 sums before the lift: every combine term a plain sum (zero reps), at most this many per limb
+    int sum_m = 0;
+    for (const CombineTerm& t : terms) if (t.coef != 1) sum_m = -1;
+    for (size_t ko = 0; ko < d && sum_m >= 0; ++ko) sum_m = std::max(sum_m, start[ko + 1] - start[ko]);
     const long Ln2 = 2L * c->L * c->n, Kn2 = 2L * c->K * c->n;
     // [0, BP): a offsets, [BP, 2BP): b offsets (ciphertexts), [2BP, 4BP): the same into the
     // per-ciphertext extension buffers
@@ -1379,6 +1406,7 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
         if (int e_ = upload(c, c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm))) return e_;
     c->cached_B = B; c->cached_d = d; c->cached_base = base; c->cached_p = plain;
     c->cached_npairs = npairs;
+    c->cached_sum_m = sum_m;
     return 0;
 }
 
@@ -1453,11 +1481,33 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     // the per-limb sums (dbfv/eval.rs:124-132) and the degree reduction are linear, so with ks32 they
     // run on the products' coefficient-domain results and only the d output limbs are transformed
     // (B d 2L forward NTTs instead of B npairs 2L)
+    // ... and when the 31-bit basis holds the sum of a limb's key switches, those are added there
+    // and lifted once per output limb instead of once per product
+    const bool sum_ks = c->S32 > 0 && c->ks32 && c->cached_sum_m > 0 && c->cached_sum_m <= c->ks32_sum_max &&
+                        c->digit16 && c->gbase <= 65536 && !c->fused_ks && c->rlk_loaded &&
+                        std::min<size_t>(c->G, c->rlk_keys) > 0;
+    const size_t ul = 2 * c->L * (size_t)c->S32 * c->n;   // words per product
+    if (sum_ks) {
+        if (grow((u64**)&c->d_uall, &c->uall_cap, std::max<size_t>((size_t)P * ul * sizeof(uint32_t), 8)) ||
+            grow((u64**)&c->d_uk, &c->uk_cap, std::max<size_t>(B * d * ul * sizeof(uint32_t), 8)))
+            return EXACTO_ERR_HIP;
+        c->ks_defer = c->d_uall;
+    }
     bool coef = false;
-    if (int e = run_mul(c, op, P, c->prod, Ln2, true, &coef)) return e;
+    const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
+    c->ks_defer = nullptr;
+    if (rc) return rc;
+    if (sum_ks && !coef) return fail(EXACTO_ERR_HIP, "internal: ks32 sums without the ks32 key switch");
     launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
                         c->stream);
     CHECK_LAUNCH();
+    if (sum_ks) {
+        ks32_sum(c->d_uall, npairs, c->d_term_start, c->d_terms, c->d_uk, (int)B, (int)d, c->L, c->S32, c->n,
+                 c->d_p32, c->stream);
+        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)(B * d), c->L, c->S32, c->logn, c->d_kst, c->d_p32,
+                 c->d_primes, c->stream);
+        CHECK_LAUNCH();
+    }
     if (coef)
         if (int e = run_ntt(c, contiguous(out, (long)B * d, 2L * c->L, 0, c->L, c->n), (long)B * d * 2 * c->L, false))
             return e;
