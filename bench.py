@@ -140,11 +140,16 @@ def main():
         a = uniform_dev((B,), moduli, n, gen, device)
         b = uniform_dev((B,), moduli, n, gen, device)
 
+        fused = os.environ.get("EXACTO_BENCH_UNFUSED", "0") == "0"
+
         def step():  # fwd NTT of both operands, pointwise product, inverse NTT
             ctx.rns_fwd_dev(a, B)
             ctx.rns_fwd_dev(b, B)
-            ctx.rns_mul_dev(a, b, a, B)
-            ctx.rns_inv_dev(a, B)
+            if fused:   # the product formed on the inverse's load (exacto_rns_mul_inv_dev)
+                ctx.rns_mul_inv_dev(a, b, a, B)
+            else:
+                ctx.rns_mul_dev(a, b, a, B)
+                ctx.rns_inv_dev(a, B)
         units_per_step = B
         unit = "poly_mul/s"
         metric = "NTT-based negacyclic poly muls/sec (fwd NTT x2 + pointwise + inv NTT)"

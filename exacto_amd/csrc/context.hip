@@ -1185,6 +1185,21 @@ extern "C" int exacto_rns_neg_dev(exacto_ctx* c, const uint64_t* a, uint64_t* o,
 extern "C" int exacto_rns_mul_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t n) {
     return pw(c, PwOp::Mul, a, b, o, (long)n * (c ? c->L : 0), nullptr);
 }
+// INTT(a (.) b): RnsPoly::mul then to_coeff_poly per limb, fused (one pass instead of a
+// pointwise pass and an inverse transform); [count][L][n], out may alias a or b.
+extern "C" int exacto_rns_mul_inv_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t count) {
+    if (int e = check_ctx(c)) return e;
+    if (count == 0) return 0;
+    if (!a || !b || !o) return invalid_param("null buffer");
+    bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
+    for (int t = 0; t < c->L; ++t) {
+        lazy &= c->ctq[t] < (1ull << 60);
+        near60 &= c->ctq[t] < (1ull << 60) && c->ctq[t] > (1ull << 60) - (1ull << 24);
+    }
+    launch_mul_inv(a, b, o, (long)count * c->L, c->L, c->logn, lazy, near60, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
 extern "C" int exacto_rns_scalar_mul_dev(exacto_ctx* c, const uint64_t* a, uint64_t scalar, uint64_t* o, size_t n) {
     if (int e = check_ctx(c)) return e;
     // s = scalar % q_i per limb (ntt.rs:136); tiny synchronous upload into the context's table

@@ -144,6 +144,9 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
 // asm_inv: every prime is 2^60 - d with d < 2^24 and n = 4096 / 8192 (generated inverse rounds,
 // special-prime products)
+// out = INTT(A (.) B) row by row ([rows][n], row r mod prime r % period); out may alias A or B
+void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period, int logn, bool lazy, bool asm_inv,
+                    const PrimeConst* primes, hipStream_t s);
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
                        const PrimeConst* primes, hipStream_t s, bool asm_inv = false);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.

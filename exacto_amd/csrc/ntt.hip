@@ -891,6 +891,85 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
+// ---------------------------------------------------------------- fused product + inverse
+
+// out = INTT(a (.) b) per residue polynomial: NttPoly::mul then to_coeff_poly (ntt.rs:58-67,
+// 119-129) in one pass, the product formed on load as the tensor kernel does (the pointwise pass
+// and its HBM round trip disappear).  Rows [rows][n], row r mod prime r % period.
+template <int LOGN, bool LAZY, bool ASM = false>
+__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
+__attribute__((amdgpu_waves_per_eu(3)))
+ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
+                  const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
+    if (tid >= T) return;
+    const long p = blockIdx.x;
+    const PrimeConst& P = primes[(int)(blockIdx.x % (unsigned)period)];
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    u64 x[16], y[16];
+    const ulonglong2* a2 = reinterpret_cast<const ulonglong2*>(A + p * N + 16 * tid);
+    const ulonglong2* b2 = reinterpret_cast<const ulonglong2*>(B + p * N + 16 * tid);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const ulonglong2 u = a2[k], v = b2[k];
+        x[2 * k] = u.x; x[2 * k + 1] = u.y;
+        y[2 * k] = v.x; y[2 * k + 1] = v.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        x[k] = ASM ? mulmod_near60(x[k], y[k], dq) : LAZY ? barrett_mul_lazy(x[k], y[k], P) : mul_mod(x[k], y[k], P);
+    if constexpr (ASM) {
+        const AsmK AK = make_asmk_inv(P);
+        inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
+    } else {
+        inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
+    }
+    u64* dst = out + p * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
+template <int LOGN>
+static void launch_mi(const u64* A, const u64* B, u64* out, long rows, int period, bool lazy, bool asm_inv,
+                      const PrimeConst* primes, hipStream_t s) {
+    constexpr int threads = (1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16;
+    if constexpr (LOGN == 12 || LOGN == 13) {
+        if (asm_inv) {
+            hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, true, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
+                               primes);
+            return;
+        }
+    }
+    if (lazy)
+        hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period, primes);
+    else
+        hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, false>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
+                           primes);
+}
+
+void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period, int logn, bool lazy, bool asm_inv,
+                    const PrimeConst* primes, hipStream_t s) {
+    if (rows <= 0) return;
+    switch (logn) {
+        case 4: launch_mi<4>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 5: launch_mi<5>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 6: launch_mi<6>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 7: launch_mi<7>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 8: launch_mi<8>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 9: launch_mi<9>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 10: launch_mi<10>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 11: launch_mi<11>(A, B, out, rows, period, lazy, false, primes, s); break;
+        case 12: launch_mi<12>(A, B, out, rows, period, lazy, asm_inv, primes, s); break;
+        case 13: launch_mi<13>(A, B, out, rows, period, lazy, asm_inv, primes, s); break;
+        case 14: launch_mi<14>(A, B, out, rows, period, lazy, false, primes, s); break;
+        default: break;
+    }
+}
+
 // ---------------------------------------------------------------- fused key switching
 
 // One workgroup per (product, limb i) of relinearize (keyswitch.rs:86-95):

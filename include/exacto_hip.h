@@ -122,6 +122,10 @@ int exacto_rns_sub_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, ui
 int exacto_rns_neg_dev(exacto_ctx* ctx, const uint64_t* a, uint64_t* out, size_t count);
 int exacto_rns_mul_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
 int exacto_rns_scalar_mul_dev(exacto_ctx* ctx, const uint64_t* a, uint64_t scalar, uint64_t* out, size_t count);
+/* INTT(a (.) b): RnsPoly::mul followed by the per-limb inverse (to_coeff_poly, ntt.rs:58-67,
+ * 119-129) fused into one pass, as the reference's own negacyclic-product test composes them
+ * (ntt.rs:181-195).  a, b NTT domain, out coefficient domain; out may alias a or b. */
+int exacto_rns_mul_inv_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
 
 /* ---- BFV ciphertext ops (bfv/eval.rs).  Degree-1 ct batches [B][2][L][n]. ---- */
 /* bfv_add / bfv_sub / bfv_neg (eval.rs:14-60) on equal-degree ciphertexts of `polys` polys. */

@@ -142,3 +142,40 @@ def test_ntt_extreme_inputs(gpu_available, n, q):
     assert np.array_equal(ctx.ntt_inv(got), a)
     inv_top = ctx.ntt_inv(top[None, :])
     assert np.array_equal(ctx.ntt_fwd(inv_top), top[None, :])
+
+
+@pytest.mark.parametrize("n,qs", [(16, [65537]), (256, [65537, 1099509805057]), (1024, [1099509805057]),
+                                  (4096, [CFG2_Q]), (8192, [CFG2_Q, 1152921504606748673]),
+                                  (4096, [1152921504606830593, 1152921504606748673, 1152921504606683137]),
+                                  (4096, [4611686018427322369]), (16384, [1152921504606748673])])
+def test_rns_mul_inv_fused_matches_composition(gpu_available, n, qs):
+    """exacto_rns_mul_inv_dev (pointwise product fused into the inverse) against rns_mul + rns_inv
+    (ntt.rs:119-129 then 58-67) on the same inputs, in place (out = a) and out of place, with
+    extreme residues; n = 16 also against mul_naive (ntt.rs:181-195)."""
+    import torch
+    L = len(qs)
+    B = 5
+    rng = np.random.default_rng(n + L)
+    ctx = HipContext(n, qs, plain_modulus=257)
+    q = np.array(qs, dtype=np.uint64)[None, :, None]
+    a = (rng.integers(0, 1 << 63, size=(B, L, n), dtype=np.uint64) % q).astype(np.uint64)
+    b = (rng.integers(0, 1 << 63, size=(B, L, n), dtype=np.uint64) % q).astype(np.uint64)
+    a[0] = q[0] - 1
+    b[0, :, ::2] = q[0, :, 0:1] - 1
+    da = torch.from_numpy(a.view(np.int64)).cuda()
+    db = torch.from_numpy(b.view(np.int64)).cuda()
+    ref = da.clone()
+    ctx.rns_mul_dev(ref, db, ref, B)
+    ctx.rns_inv_dev(ref, B)
+    out = torch.empty_like(da)
+    ctx.rns_mul_inv_dev(da, db, out, B)
+    ctx.rns_mul_inv_dev(da, db, da, B)       # in place
+    ctx.synchronize()
+    want = ref.cpu().numpy()
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(da.cpu().numpy(), want)
+    if n == 16:
+        fa = ctx.ntt_inv(a.reshape(-1, n)[:1])   # coefficient-domain operands: INTT of the inputs
+        fb = ctx.ntt_inv(b.reshape(-1, n)[:1])
+        naive = CoeffPoly([int(v) for v in fa[0]], qs[0]).mul_naive(CoeffPoly([int(v) for v in fb[0]], qs[0]))
+        assert [int(v) for v in want.view(np.uint64)[0, 0]] == naive.coeffs
