@@ -63,6 +63,7 @@ _SIGS = [
     ("exacto_rns_neg_dev", [_P, _P, _P, _SZ], C.c_int),
     ("exacto_rns_mul_dev", [_P, _P, _P, _P, _SZ], C.c_int),
     ("exacto_rns_mul_inv_dev", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_rns_polymul_dev", [_P, _P, _P, _P, _SZ], C.c_int),
     ("exacto_rns_scalar_mul_dev", [_P, _P, _U64, _P, _SZ], C.c_int),
     ("exacto_bfv_add_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
     ("exacto_bfv_sub_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
@@ -598,6 +599,10 @@ class HipContext:
     def rns_mul_inv_dev(self, a, b, out, count):
         """INTT(a (.) b) per limb, fused (exacto_rns_mul_inv_dev)."""
         check(self._lib.exacto_rns_mul_inv_dev(self._h, self._p(a), self._p(b), self._p(out), count))
+
+    def rns_polymul_dev(self, a, b, out, count):
+        """Negacyclic products of coefficient-domain polys (exacto_rns_polymul_dev)."""
+        check(self._lib.exacto_rns_polymul_dev(self._h, self._p(a), self._p(b), self._p(out), count))
 
     def rns_scalar_mul_dev(self, a, scalar, out, count):
         check(self._lib.exacto_rns_scalar_mul_dev(self._h, self._p(a), scalar, self._p(out), count))

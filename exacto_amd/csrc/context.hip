@@ -1200,6 +1200,52 @@ extern "C" int exacto_rns_mul_inv_dev(exacto_ctx* c, const uint64_t* a, const ui
     CHECK_LAUNCH();
     return 0;
 }
+// Negacyclic products of coefficient-domain RnsPolys: to_coeff_poly(from_coeff_poly(a) (.)
+// from_coeff_poly(b)) per limb (ntt.rs:181-195 composed).  n = 4096 / 8192 with special primes:
+// one fused kernel; otherwise the forward transforms into scratch and the fused product + inverse.
+// [count][L][n]; out may alias a or b.
+extern "C" int exacto_rns_polymul_dev(exacto_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* o, size_t count) {
+    if (int e = check_ctx(c)) return e;
+    if (count == 0) return 0;
+    if (!a || !b || !o) return invalid_param("null buffer");
+    bool near60 = c->ntt_asm && c->ntt_asm_inv, lazy = true;
+    for (int t = 0; t < c->L; ++t) {
+        lazy &= c->ctq[t] < (1ull << 60);
+        near60 &= c->ctq[t] < (1ull << 60) && c->ctq[t] > (1ull << 60) - (1ull << 24);
+    }
+    const long rows = (long)count * c->L;
+    ProfRec rec{};
+    if (near60 && (c->logn == 12 || c->logn == 13)) {
+        if (c->prof) {
+            HIP_TRY(hipEventCreate(&rec.a));
+            HIP_TRY(hipEventCreate(&rec.b));
+            HIP_TRY(hipEventRecord(rec.a, c->stream));
+        }
+        launch_polymul(a, b, o, rows, c->L, c->logn, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+        if (c->prof) {
+            HIP_TRY(hipEventRecord(rec.b, c->stream));
+            rec.kind = 3;   // fused product: 3 transforms, algorithmic bytes a + b in, product out
+            rec.polys = (u64)rows;
+            rec.bytes = 24.0 * c->n * (double)rows;
+            c->recs.push_back(rec);
+        }
+        return 0;
+    }
+    Scratch sa, sb;
+    HIP_TRY(sa.alloc((size_t)rows * poly_bytes(c), c->stream));
+    HIP_TRY(sb.alloc((size_t)rows * poly_bytes(c), c->stream));
+    NttBatch nb = contiguous(sa.as<u64>(), count, c->L, 0, c->L, c->n);
+    nb.src = a;
+    if (int e = run_ntt(c, nb, rows, false)) return e;
+    nb = contiguous(sb.as<u64>(), count, c->L, 0, c->L, c->n);
+    nb.src = b;
+    if (int e = run_ntt(c, nb, rows, false)) return e;
+    launch_mul_inv(sa.as<u64>(), sb.as<u64>(), o, rows, c->L, c->logn, lazy, false, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
+}
+
 extern "C" int exacto_rns_scalar_mul_dev(exacto_ctx* c, const uint64_t* a, uint64_t scalar, uint64_t* o, size_t n) {
     if (int e = check_ctx(c)) return e;
     // s = scalar % q_i per limb (ntt.rs:136); tiny synchronous upload into the context's table

@@ -144,6 +144,10 @@ struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per i
 // Tensor product + inverse NTT of its three components, T[item][3][L+K][n] (ntt.hip).
 // asm_inv: every prime is 2^60 - d with d < 2^24 and n = 4096 / 8192 (generated inverse rounds,
 // special-prime products)
+// out = INTT(NTT(A) (.) NTT(B)) row by row, one workgroup per row (n = 4096 / 8192 and primes
+// 2^60 - d, d < 2^24 only; false = not launched)
+bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,
+                    hipStream_t s);
 // out = INTT(A (.) B) row by row ([rows][n], row r mod prime r % period); out may alias A or B
 void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period, int logn, bool lazy, bool asm_inv,
                     const PrimeConst* primes, hipStream_t s);

@@ -970,6 +970,59 @@ void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period,
     }
 }
 
+// ---------------------------------------------------------------- fused negacyclic product
+
+// out = INTT(NTT(a) (.) NTT(b)) per residue polynomial (coefficient domain in and out): the
+// reference's NTT multiplication (ntt.rs:181-195: from_coeff_poly twice, mul, to_coeff_poly) in
+// one workgroup.  The forward transform leaves element 16 tid + k in x[k], which is the layout
+// the inverse's first round takes, so neither operand's evaluations nor the product ever leave
+// the chip: 3 HBM passes per product instead of 7, and no output transposes of the forward
+// transforms.  n = 4096 / 8192, every prime 2^60 - d with d < 2^24 (asm rounds, mulmod_near60).
+// b's coefficients are loaded at the start and stay in flight across a's transform; x_a is held
+// across b's, which needs 2 waves per SIMD (the asm rounds' clobbered VGPRs plus both operands).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(2)))
+ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const long p = blockIdx.x;
+    const PrimeConst& P = primes[(int)(blockIdx.x % (unsigned)period)];
+    const u64 q = P.q;
+    const u64* a = A + p * N;
+    const u64* b = B + p * N;
+    u64 xa[16], xb[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xa[k] = a[tid + k * T];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xb[k] = b[tid + k * T];
+    const AsmK K = make_asmk(q);
+    const TwTab tf = tw_table(P.tw_fwd);
+    fwd_rounds_asm<LOGN, 0>(xa, lds, tid, tf, K);
+    fwd_rounds_asm<LOGN, 0>(xb, lds, tid, tf, K);
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xa[k] = mulmod_near60(xa[k], xb[k], dq);   // < 2q: the inverse's input bound
+    const AsmK AK = make_asmk_inv(P);
+    inv_rounds_asm<LOGN, 0>(xa, lds, tid, tw_table(P.tw_inv), AK);
+    u64* dst = out + p * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = xa[k];
+}
+
+bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,
+                    hipStream_t s) {
+    if (logn == 12)
+        hipLaunchKernelGGL(ntt_polymul_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
+    else if (logn == 13)
+        hipLaunchKernelGGL(ntt_polymul_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
+    else
+        return false;
+    return true;
+}
+
 // ---------------------------------------------------------------- fused key switching
 
 // One workgroup per (product, limb i) of relinearize (keyswitch.rs:86-95):

@@ -126,6 +126,10 @@ int exacto_rns_scalar_mul_dev(exacto_ctx* ctx, const uint64_t* a, uint64_t scala
  * 119-129) fused into one pass, as the reference's own negacyclic-product test composes them
  * (ntt.rs:181-195).  a, b NTT domain, out coefficient domain; out may alias a or b. */
 int exacto_rns_mul_inv_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
+/* Negacyclic products of coefficient-domain RnsPolys: to_coeff_poly(from_coeff_poly(a) (.)
+ * from_coeff_poly(b)) per limb, the reference's NTT multiplication (ntt.rs:181-195), fused into
+ * one kernel at n = 4096 / 8192 (neither operand's evaluations are stored).  out may alias a or b. */
+int exacto_rns_polymul_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
 
 /* ---- BFV ciphertext ops (bfv/eval.rs).  Degree-1 ct batches [B][2][L][n]. ---- */
 /* bfv_add / bfv_sub / bfv_neg (eval.rs:14-60) on equal-degree ciphertexts of `polys` polys. */

@@ -179,3 +179,39 @@ def test_rns_mul_inv_fused_matches_composition(gpu_available, n, qs):
         fb = ctx.ntt_inv(b.reshape(-1, n)[:1])
         naive = CoeffPoly([int(v) for v in fa[0]], qs[0]).mul_naive(CoeffPoly([int(v) for v in fb[0]], qs[0]))
         assert [int(v) for v in want.view(np.uint64)[0, 0]] == naive.coeffs
+
+
+@pytest.mark.parametrize("n,qs", [(16, [65537]), (1024, [1099509805057, 562949953443841]), (4096, [CFG2_Q]),
+                                  (4096, [1152921504606830593, 1152921504606748673, 1152921504606683137]),
+                                  (8192, [CFG2_Q, 1152921504606748673]), (4096, [4611686018427322369])])
+def test_rns_polymul_matches_composition(gpu_available, n, qs):
+    """exacto_rns_polymul_dev (one kernel per product at n = 4096 / 8192 with special primes, the
+    composition otherwise) against rns_fwd x2 + rns_mul + rns_inv, in place and out of place; the
+    reference's own negacyclic identity (ntt.rs:181-195) against mul_naive on the first product."""
+    import torch
+    L = len(qs)
+    B = 4
+    rng = np.random.default_rng(3 * n + L)
+    ctx = HipContext(n, qs, plain_modulus=257)
+    q = np.array(qs, dtype=np.uint64)[None, :, None]
+    a = (rng.integers(0, 1 << 63, size=(B, L, n), dtype=np.uint64) % q).astype(np.uint64)
+    b = (rng.integers(0, 1 << 63, size=(B, L, n), dtype=np.uint64) % q).astype(np.uint64)
+    a[1] = q[0] - 1
+    b[1, :, 1::2] = q[0, :, 0:1] - 1
+    da = torch.from_numpy(a.view(np.int64)).cuda()
+    db = torch.from_numpy(b.view(np.int64)).cuda()
+    ra, rb = da.clone(), db.clone()
+    ctx.rns_fwd_dev(ra, B)
+    ctx.rns_fwd_dev(rb, B)
+    ctx.rns_mul_dev(ra, rb, ra, B)
+    ctx.rns_inv_dev(ra, B)
+    out = torch.empty_like(da)
+    ctx.rns_polymul_dev(da, db, out, B)
+    ctx.rns_polymul_dev(da, db, db, B)   # in place on b
+    ctx.synchronize()
+    want = ra.cpu().numpy()
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(db.cpu().numpy(), want)
+    if n <= 1024:
+        naive = CoeffPoly([int(v) for v in a[0, 0]], qs[0]).mul_naive(CoeffPoly([int(v) for v in b[0, 0]], qs[0]))
+        assert [int(v) for v in want.view(np.uint64)[0, 0]] == naive.coeffs
