@@ -1145,13 +1145,96 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
 }
 
+// One workgroup per (item, prime) for all three tensor components: the four operands are read once
+// (the per-component form reads eight), c0 = a0 b0, c1 = a0 b1 + a1 b0, c2 = a1 b1 are formed in
+// registers, and the three inverse transforms run back to back with the other components held
+// in registers (2 waves per SIMD).  n = 4096 / 8192, special primes (mulmod_near60, asm rounds).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(2)))
+ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
+                       const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    __shared__ u64 stash[N];   // c2 while c0 and c1 are transformed (lane-interleaved: no bank conflicts)
+    const int tid = threadIdx.x;
+    const int NP = L + K;
+    const long p = blockIdx.x;
+    const long item = p / NP;
+    const int t = (int)(p - item * NP);
+    const PrimeConst& P = primes[t];
+    const u64 *A0, *A1, *B0, *B1;
+    if (t < L) {
+        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
+        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
+        A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
+        B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
+    } else if (op.ea) {
+        const u64* EA = op.ea + (long)op.ea_off[item] + (long)(t - L) * N;
+        const u64* EB = op.eb + (long)op.eb_off[item] + (long)(t - L) * N;
+        A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
+    } else {
+        const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
+        A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
+    }
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    auto load = [&](const u64* src, u64 (&v)[16]) {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 w = s2[k];
+            v[2 * k] = w.x;
+            v[2 * k + 1] = w.y;
+        }
+    };
+    u64 c0[16], c1[16];
+    {
+        u64 a0[16], a1[16], b0[16], b1[16];
+        load(A0, a0);
+        load(B0, b0);
+        load(A1, a1);
+        load(B1, b1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            stash[k * T + tid] = mulmod_near60(a1[k], b1[k], dq);
+            c1[k] = mulmod_near60(a0[k], b1[k], dq) + mulmod_near60(a1[k], b0[k], dq);   // < 4q
+            c0[k] = mulmod_near60(a0[k], b0[k], dq);
+        }
+    }
+    const AsmK AK = make_asmk_inv(P);
+    const TwTab ti = tw_table(P.tw_inv);
+    u64* dst = Tout + (item * 3 * NP + t) * N;   // [item][c][prime][n]
+    inv_rounds_asm<LOGN, 0>(c0, lds, tid, ti, AK);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = c0[k];
+    inv_rounds_asm<LOGN, 0>(c1, lds, tid, ti, AK);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[(long)NP * N + elem_index<LAST_LO>(tid, k)] = c1[k];
+    u64 c2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c2[k] = stash[k * T + tid];   // this thread's own words: no barrier
+    inv_rounds_asm<LOGN, 0>(c2, lds, tid, ti, AK);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[2L * NP * N + elem_index<LAST_LO>(tid, k)] = c2[k];
+}
+
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
+    // one workgroup per (item, prime) at n = 8192 (cfg5 +1.6 % A/B); at n = 4096 the per-component
+    // form at 3 waves per SIMD is faster (327 vs 335 us per cfg3 chunk).  EXACTO_TENSOR3=0/1 forces.
+    static const int t3env = [] { const char* e = std::getenv("EXACTO_TENSOR3"); return e ? (e[0] == '1') : -1; }();
+    const bool t3 = t3env >= 0 ? t3env == 1 : LOGN == 13;
     if constexpr (LOGN == 12 || LOGN == 13) {
+        if (asm_inv && t3) {
+            hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(blocks / 3), dim3(threads), 0, s, op, extP, T, L, K,
+                               primes);
+            return;
+        }
         if (asm_inv) {
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(blocks), dim3(threads), 0, s, op, extP,
                                T, L, K, primes, remap);
