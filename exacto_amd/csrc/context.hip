@@ -736,6 +736,7 @@ extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
     info->plain_modulus = c->plain;
     info->mul_path = c->path;
     info->device = c->device;
+    info->ks32_primes = c->ks32 ? c->S32 : 0;
     return 0;
 }
 

@@ -75,6 +75,7 @@ typedef struct exacto_ctx_info {
     uint64_t plain_modulus;
     int mul_path;             /* enum exacto_mul_path */
     int device;
+    int ks32_primes;          /* primes of the 31-bit key-switch basis in use (0: limb-wise MAC) */
 } exacto_ctx_info;
 
 /* ---- context: replaces BfvParamsBuilder::build + RnsBasis::new + make_plan ----

@@ -36,14 +36,24 @@ def _ctx(prm, ks32: bool, chunk=0):
     return ctx
 
 
+def _params(which, n):
+    if which == "cfg3":
+        return P.cfg3_params(n)
+    if which == "q2":
+        return P.BfvParamsBuilder().ring_degree(n).plain_modulus(65537).ct_moduli(P.Q3[1:]).build()
+    return P.cfg5_params(n).bfv_params
+
+
 @pytest.mark.parametrize("n,which,B,keys,chunk", [
     (1024, "cfg3", 5, None, 0),
     (4096, "cfg3", 7, None, 3),        # 3 chunks: both pipeline lanes
     (4096, "cfg3", 2, 7, 0),           # a key with fewer digits than G (keyswitch.rs:87-89)
     (8192, "cfg5", 2, None, 0),
+    (2048, "cfg3", 3, None, 0),        # the remaining transform lengths of the 31-bit basis
+    (16384, "q2", 1, None, 0),         # n = 16384: cfg3's last two primes (== 1 mod 2^15)
 ])
 def test_ks32_matches_limbwise_mac(gpu_available, n, which, B, keys, chunk):
-    prm = P.cfg3_params(n) if which == "cfg3" else P.cfg5_params(n).bfv_params
+    prm = _params(which, n)
     q = prm.ct_basis.moduli
     rng = np.random.default_rng(n + B)
     ct1 = uniform_residues(rng, (B, 2), q, n)
@@ -53,6 +63,7 @@ def test_ks32_matches_limbwise_mac(gpu_available, n, which, B, keys, chunk):
     outs = []
     for ks in (True, False):
         ctx = _ctx(prm, ks, chunk)
+        assert (ctx.ks32_primes > 0) == ks       # the 31-bit basis is in use exactly when asked
         ctx.load_relin_key(rlk)
         outs.append(ctx.bfv_mul_and_relin(ct1, ct2))
     assert np.array_equal(outs[0], outs[1])
@@ -86,12 +97,13 @@ def test_ks32_key_reload(gpu_available):
 def test_ks32_automorphism_matches_limbwise(gpu_available, n, which, B, keys, chunk):
     """bfv_apply_automorphism (eval.rs:512-561) with the ks32 key switch against the limb-wise
     60-bit MAC, for an odd and the conjugation element, and a new key in every call."""
-    prm = P.cfg3_params(n) if which == "cfg3" else P.cfg5_params(n).bfv_params
+    prm = _params(which, n)
     q = prm.ct_basis.moduli
     rng = np.random.default_rng(3 * n + B)
     ct = uniform_residues(rng, (B, 2), q, n)
     ct[0, 1] = np.array(q, dtype=np.uint64)[:, None] - 1
     ctxs = [_ctx(prm, True, chunk), _ctx(prm, False, chunk)]
+    assert ctxs[0].ks32_primes > 0 and ctxs[1].ks32_primes == 0
     for element in (5, 2 * n - 1):
         gk = uniform_residues(rng, (keys or prm.gadget_digits, 2), q, n)
         got, want = (c.bfv_apply_automorphism(ct, element, gk) for c in ctxs)
