@@ -166,6 +166,17 @@ struct ProfRec {
     double bytes;
 };
 
+// Stream and per-chunk workspace of one extra pipeline lane (lane 0 is the context's own).
+constexpr int EXACTO_MAX_LANES = 4;
+struct LaneSet {
+    hipStream_t stream = nullptr;
+    hipEvent_t join = nullptr;
+    size_t items = 0;
+    u64 *coefQ = nullptr, *extP = nullptr, *T = nullptr, *D = nullptr;
+    int16_t* D16 = nullptr;
+    uint32_t *DS = nullptr, *U = nullptr;
+};
+
 struct exacto_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -204,7 +215,7 @@ struct exacto_ctx {
     uint32_t* d_rs = nullptr;    // key in the auxiliary basis [keys][2L][S][n], NTT domain mod p_s
     size_t rs_cap = 0;
     bool rs_valid = false;
-    uint32_t *ws_DS = nullptr, *ws_U = nullptr, *ws2_DS = nullptr, *ws2_U = nullptr;
+    uint32_t *ws_DS = nullptr, *ws_U = nullptr;
     bool rlk_loaded = false;
     // workspace (per chunk)
     size_t chunk = 512;  // products per pipeline pass; throughput plateaus from ~512 (r1 sweep)
@@ -213,14 +224,14 @@ struct exacto_ctx {
     // exact path with gadget base <= 2^16: the scale kernel writes each digit once as int16 and
     // the digit NTT converts it per limb on load (EXACTO_DIGIT16=0: u64 digits per limb)
     bool digit16 = true;
-    int16_t *ws_D16 = nullptr, *ws2_D16 = nullptr;
-    // second pipeline lane: odd chunks run on aux_stream with their own workspace, so the
-    // kernels of two chunks overlap (the NTTs are latency-bound; EXACTO_DUAL_STREAM=0 disables)
+    int16_t* ws_D16 = nullptr;
+    // further pipeline lanes: chunk i runs on lane i % lanes, each lane a stream with its own
+    // workspace, so the kernels of consecutive chunks overlap (EXACTO_DUAL_STREAM=0: one lane;
+    // EXACTO_LANES: lane count, 2 by default)
     bool dual = true;
-    hipStream_t aux_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    size_t ws2_items = 0;
-    u64 *ws2_coefQ = nullptr, *ws2_extP = nullptr, *ws2_T = nullptr, *ws2_D = nullptr;
+    int lanes = 2;
+    hipEvent_t ev_fork = nullptr;
+    LaneSet xl[EXACTO_MAX_LANES - 1];   // lanes 1 .. lanes-1
     // dBFV: per-ciphertext extensions shared by the products that use the ciphertext
     // (EXACTO_SHARE_EXT=0 recomputes them per product)
     bool share_ext = true;
@@ -694,6 +705,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM_INV")) c->ntt_asm_inv = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_LANES")) c->lanes = std::max(1, std::min(EXACTO_MAX_LANES, atoi(e)));
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
@@ -710,16 +722,18 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
-    free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
+    for (LaneSet& l : c->xl) {
+        if (l.stream) { (void)hipStreamSynchronize(l.stream); (void)hipStreamDestroy(l.stream); }
+        if (l.join) (void)hipEventDestroy(l.join);
+        free_dev(l.coefQ); free_dev(l.extP); free_dev(l.T); free_dev(l.D); free_dev(l.DS); free_dev(l.U);
+        if (l.D16) (void)hipFree(l.D16);
+    }
     free_dev(c->ext_a); free_dev(c->ext_b);
     free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_uall); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
-    if (c->ws2_D16) (void)hipFree(c->ws2_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
-    free_dev(c->ws_DS); free_dev(c->ws_U); free_dev(c->ws2_DS); free_dev(c->ws2_U);
-    if (c->aux_stream) { (void)hipStreamSynchronize(c->aux_stream); (void)hipStreamDestroy(c->aux_stream); }
+    free_dev(c->ws_DS); free_dev(c->ws_U);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -893,44 +907,46 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     return 0;
 }
 
-// Lane 1 of the pipeline: aux stream + second workspace (allocated on first use).
-static int ensure_lane2(exacto_ctx* c, size_t items) {
-    if (!c->aux_stream) HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+// Extra pipeline lane `idx` (1 ..): its stream, join event and workspace (allocated on first use).
+static int ensure_lane(exacto_ctx* c, int idx, size_t items) {
     if (!c->ev_fork) HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    if (!c->ev_join) HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-    if (c->ws2_items >= items) return 0;
-    free_dev(c->ws2_coefQ); free_dev(c->ws2_extP); free_dev(c->ws2_T); free_dev(c->ws2_D);
-    c->ws2_coefQ = c->ws2_extP = c->ws2_T = c->ws2_D = nullptr;
-    c->ws2_items = 0;
+    LaneSet& l = c->xl[idx - 1];
+    if (!l.stream) HIP_TRY(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+    if (!l.join) HIP_TRY(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
+    if (l.items >= items) return 0;
+    free_dev(l.coefQ); free_dev(l.extP); free_dev(l.T); free_dev(l.D); free_dev(l.DS); free_dev(l.U);
+    if (l.D16) (void)hipFree(l.D16);
+    l.coefQ = l.extP = l.T = l.D = nullptr;
+    l.D16 = nullptr;
+    l.DS = l.U = nullptr;
+    l.items = 0;
     const size_t pb = poly_bytes(c);
     const int NP = c->L + c->K;
-    HIP_TRY(hipMalloc((void**)&c->ws2_coefQ, items * 4 * c->L * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws2_extP, items * 4 * std::max(c->K, 1) * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws2_T, items * 3 * NP * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws2_D, items * std::max(c->G, 1) * c->L * pb));
-    if (c->ws2_D16) (void)hipFree(c->ws2_D16);
-    HIP_TRY(hipMalloc((void**)&c->ws2_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
-    free_dev(c->ws2_DS); free_dev(c->ws2_U);
-    c->ws2_DS = c->ws2_U = nullptr;
+    HIP_TRY(hipMalloc((void**)&l.coefQ, items * 4 * c->L * pb));
+    HIP_TRY(hipMalloc((void**)&l.extP, items * 4 * std::max(c->K, 1) * pb));
+    HIP_TRY(hipMalloc((void**)&l.T, items * 3 * NP * pb));
+    HIP_TRY(hipMalloc((void**)&l.D, items * std::max(c->G, 1) * c->L * pb));
+    HIP_TRY(hipMalloc((void**)&l.D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
     if (c->S32) {
-        HIP_TRY(hipMalloc((void**)&c->ws2_DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc((void**)&c->ws2_U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&l.DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc((void**)&l.U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
     }
-    c->ws2_items = items;
+    l.items = items;
     return 0;
 }
 
-// Points the context's stream and workspace at lane 1 for the lifetime of the guard.
+// Points the context's stream and workspace at lane idx (> 0) for the lifetime of the guard.
 struct LaneGuard {
     exacto_ctx* c;
-    bool on;
-    LaneGuard(exacto_ctx* c_, bool on_) : c(c_), on(on_) { if (on) flip(); }
-    ~LaneGuard() { if (on) flip(); }
+    int idx;
+    LaneGuard(exacto_ctx* c_, int idx_) : c(c_), idx(idx_) { if (idx > 0) flip(); }
+    ~LaneGuard() { if (idx > 0) flip(); }
     void flip() {
-        std::swap(c->stream, c->aux_stream);
-        std::swap(c->ws_coefQ, c->ws2_coefQ); std::swap(c->ws_extP, c->ws2_extP);
-        std::swap(c->ws_T, c->ws2_T); std::swap(c->ws_D, c->ws2_D); std::swap(c->ws_D16, c->ws2_D16);
-        std::swap(c->ws_DS, c->ws2_DS); std::swap(c->ws_U, c->ws2_U);
+        LaneSet& l = c->xl[idx - 1];
+        std::swap(c->stream, l.stream);
+        std::swap(c->ws_coefQ, l.coefQ); std::swap(c->ws_extP, l.extP);
+        std::swap(c->ws_T, l.T); std::swap(c->ws_D, l.D); std::swap(c->ws_D16, l.D16);
+        std::swap(c->ws_DS, l.DS); std::swap(c->ws_U, l.U);
     }
 };
 
@@ -1016,23 +1032,26 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     }
     // two chunks or more: odd chunks on the second lane (profiling keeps one lane so its per-kernel
     // events time each kernel alone)
-    const bool dual = c->dual && !c->prof && P > (long)C;
-    if (dual) {
-        if (int e = ensure_lane2(c, C)) return e;
+    const long nchunks = (P + (long)C - 1) / (long)C;
+    const int nl = (c->dual && !c->prof) ? (int)std::min<long>(c->lanes, nchunks) : 1;
+    if (nl > 1) {
+        for (int i = 1; i < nl; ++i)
+            if (int e = ensure_lane(c, i, C)) return e;
         HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+        for (int i = 1; i < nl; ++i) HIP_TRY(hipStreamWaitEvent(c->xl[i - 1].stream, c->ev_fork, 0));
     }
     struct Join {
         exacto_ctx* c;
-        bool on;
+        int nl;
         ~Join() {
-            if (on && hipEventRecord(c->ev_join, c->aux_stream) == hipSuccess)
-                (void)hipStreamWaitEvent(c->stream, c->ev_join, 0);
+            for (int i = 1; i < nl; ++i)
+                if (hipEventRecord(c->xl[i - 1].join, c->xl[i - 1].stream) == hipSuccess)
+                    (void)hipStreamWaitEvent(c->stream, c->xl[i - 1].join, 0);
         }
-    } join{c, dual};
+    } join{c, nl};
     for (long s = 0; s < P; s += (long)C) {
         const int cnt = (int)std::min<long>((long)C, P - s);
-        LaneGuard lane(c, dual && ((s / (long)C) & 1));
+        LaneGuard lane(c, (int)((s / (long)C) % nl));
         Operands o = op;
         if (o.a_off) o.a_off += s; else o.a += s * o.a_stride;
         if (o.b_off) o.b_off += s; else o.b += s * o.b_stride;
