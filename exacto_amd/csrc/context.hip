@@ -950,6 +950,28 @@ struct LaneGuard {
     }
 };
 
+// Lanes for a pass of nchunks chunks of C items: extra lanes forked off c->stream (their
+// streams wait for everything enqueued so far); LaneJoin makes c->stream wait for them again.
+static int fork_lanes(exacto_ctx* c, long nchunks, size_t C, int* nl) {
+    *nl = (c->dual && !c->prof) ? (int)std::min<long>(c->lanes, nchunks) : 1;
+    if (*nl <= 1) return 0;
+    for (int i = 1; i < *nl; ++i)
+        if (int e = ensure_lane(c, i, C)) return e;
+    HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+    for (int i = 1; i < *nl; ++i) HIP_TRY(hipStreamWaitEvent(c->xl[i - 1].stream, c->ev_fork, 0));
+    return 0;
+}
+
+struct LaneJoin {
+    exacto_ctx* c;
+    int nl;
+    ~LaneJoin() {
+        for (int i = 1; i < nl; ++i)
+            if (hipEventRecord(c->xl[i - 1].join, c->xl[i - 1].stream) == hipSuccess)
+                (void)hipStreamWaitEvent(c->stream, c->xl[i - 1].join, 0);
+    }
+};
+
 static int ensure_rlk_companions(exacto_ctx* c) {
     if (c->rlk_s_valid) return 0;
     const size_t count = c->rlk_keys * 2 * c->L * (size_t)c->n;
@@ -1032,23 +1054,9 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     }
     // two chunks or more: odd chunks on the second lane (profiling keeps one lane so its per-kernel
     // events time each kernel alone)
-    const long nchunks = (P + (long)C - 1) / (long)C;
-    const int nl = (c->dual && !c->prof) ? (int)std::min<long>(c->lanes, nchunks) : 1;
-    if (nl > 1) {
-        for (int i = 1; i < nl; ++i)
-            if (int e = ensure_lane(c, i, C)) return e;
-        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-        for (int i = 1; i < nl; ++i) HIP_TRY(hipStreamWaitEvent(c->xl[i - 1].stream, c->ev_fork, 0));
-    }
-    struct Join {
-        exacto_ctx* c;
-        int nl;
-        ~Join() {
-            for (int i = 1; i < nl; ++i)
-                if (hipEventRecord(c->xl[i - 1].join, c->xl[i - 1].stream) == hipSuccess)
-                    (void)hipStreamWaitEvent(c->stream, c->xl[i - 1].join, 0);
-        }
-    } join{c, nl};
+    int nl = 1;
+    if (int e = fork_lanes(c, (P + (long)C - 1) / (long)C, C, &nl)) return e;
+    LaneJoin join{c, nl};
     for (long s = 0; s < P; s += (long)C) {
         const int cnt = (int)std::min<long>((long)C, P - s);
         LaneGuard lane(c, (int)((s / (long)C) % nl));
@@ -2039,8 +2047,14 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
     }
     const size_t C = std::min<size_t>(c->chunk, B);
     if (int e = ensure_workspace(c, C)) return e;
+    // chunks alternate over the pipeline lanes as in run_mul (the key tables above are made on
+    // the main stream before the fork)
+    int nl = 1;
+    if (int e = fork_lanes(c, (long)((B + C - 1) / C), C, &nl)) return e;
+    LaneJoin join{c, nl};
     for (size_t s0 = 0; s0 < B; s0 += C) {
         const int cnt = (int)std::min(C, B - s0);
+        LaneGuard lane(c, (int)((s0 / C) % (size_t)nl));
         const u64* src = ct + s0 * 2 * Ln;
         u64* dst = out + s0 * 2 * Ln;
         NttBatch nb{};
