@@ -215,3 +215,22 @@ def test_rns_polymul_matches_composition(gpu_available, n, qs):
     if n <= 1024:
         naive = CoeffPoly([int(v) for v in a[0, 0]], qs[0]).mul_naive(CoeffPoly([int(v) for v in b[0, 0]], qs[0]))
         assert [int(v) for v in want.view(np.uint64)[0, 0]] == naive.coeffs
+
+
+def test_fused_product_entry_points_edge_cases(gpu_available):
+    """count = 0 is a no-op; a null buffer is InvalidParam (the library's pointer checks), for the
+    fused product + inverse and the one-kernel product."""
+    import ctypes
+    import torch
+    n = 4096
+    ctx = HipContext(n, [CFG2_Q], plain_modulus=257)
+    a = torch.zeros((1, 1, n), dtype=torch.int64, device="cuda")
+    ctx.rns_mul_inv_dev(a, a, a, 0)
+    ctx.rns_polymul_dev(a, a, a, 0)
+    for fn in ("exacto_rns_mul_inv_dev", "exacto_rns_polymul_dev"):
+        rc = getattr(ctx._lib, fn)(ctx._h, None, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(a.data_ptr()), 1)
+        assert rc != 0, fn
+    # all-zero operands: the product is zero
+    ctx.rns_polymul_dev(a, a, a, 1)
+    ctx.synchronize()
+    assert not a.any()
