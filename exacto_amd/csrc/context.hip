@@ -206,9 +206,10 @@ struct exacto_ctx {
     bool ks32 = true;
     int S32 = 0;                 // 0: not eligible for these parameters
     int ks32_sum_max = 0;        // key-switch sums that may be added before one lift (prod p bound)
-    uint32_t* ks_defer = nullptr;  // run_mul: MAC results of product p to ks_defer + p 2L S n, no lift
-    uint32_t *d_uall = nullptr, *d_uk = nullptr;  // dBFV: per-product and per-limb ks32 sums
-    size_t uall_cap = 0, uk_cap = 0;
+    int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
+    int16_t *d_dall = nullptr, *d_dk = nullptr;   // dBFV: per-product and per-limb digit sums
+    uint32_t *d_dsk = nullptr, *d_uk = nullptr;   // their residues and key-switch sums in the 31-bit basis
+    size_t dall_cap = 0, dk_cap = 0, dsk_cap = 0, uk_cap = 0;
     Prime32* d_p32 = nullptr;
     uint2* d_tw32 = nullptr;
     Ks32Tables* d_kst = nullptr;
@@ -729,7 +730,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
         if (l.D16) (void)hipFree(l.D16);
     }
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_uall); free_dev(c->d_uk); free_dev(c->pl_buf);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_dall); free_dev(c->d_dk); free_dev(c->d_dsk); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
     free_dev(c->ws_DS); free_dev(c->ws_U);
@@ -1095,7 +1096,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
-            launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D, d16 ? c->ws_D16 : nullptr, guse,
+            launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D,
+                               d16 ? (c->ks_defer ? c->ks_defer + s * (long)guse * n : c->ws_D16) : nullptr, guse,
                                cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
                                c->stream, c->h_crt.gshift);
         CHECK_LAUNCH();
@@ -1119,16 +1121,13 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // 7'+8'. the key switch over the integers (ks32.hip): digits -> NTT mod p_s, MAC with the
             // key in the same basis, inverse NTT + centred lift, added to R mod q_l in the
             // coefficient domain; the forward NTT of R below then yields the relinearised result
-            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-            if (c->ks_defer) {   // the caller sums products first and lifts once (dbfv_mul_core)
-                ks32_mac(c->ws_DS, c->d_rs, c->ks_defer + s * 2L * L * c->S32 * n, cnt, guse, L, c->S32, n,
-                         c->d_p32, c->stream);
-            } else {
+            if (!c->ks_defer) {   // (deferred: the caller sums the digits of products first, dbfv_mul_core)
+                ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
                 ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
                 ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
                          c->stream);
+                CHECK_LAUNCH();
             }
-            CHECK_LAUNCH();
         }
         if (skip_fwd) continue;
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
@@ -1570,17 +1569,23 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     // the per-limb sums (dbfv/eval.rs:124-132) and the degree reduction are linear, so with ks32 they
     // run on the products' coefficient-domain results and only the d output limbs are transformed
     // (B d 2L forward NTTs instead of B npairs 2L)
-    // ... and when the 31-bit basis holds the sum of a limb's key switches, those are added there
-    // and lifted once per output limb instead of once per product
+    // ... and when the 31-bit basis holds the sum of a limb's key switches, the key switch is
+    // linear in the digits, so the products' int16 digits are summed per output limb (still int16)
+    // and transformed, multiplied with the key and lifted once per limb instead of once per product
+    // (cfg5: 8 instead of 36 products' worth of digit NTTs, MACs and lifts per dbfv_mul)
+    const size_t gu = std::min<size_t>(c->G, c->rlk_keys);
     const bool sum_ks = c->S32 > 0 && c->ks32 && c->cached_sum_m > 0 && c->cached_sum_m <= c->ks32_sum_max &&
-                        c->digit16 && c->gbase <= 65536 && !c->fused_ks && c->rlk_loaded &&
-                        std::min<size_t>(c->G, c->rlk_keys) > 0;
-    const size_t ul = 2 * c->L * (size_t)c->S32 * c->n;   // words per product
+                        (u64)c->cached_sum_m * (c->gbase / 2) <= 32767 && c->digit16 && c->gbase <= 65536 &&
+                        !c->fused_ks && c->rlk_loaded && gu > 0;
+    const size_t Bd = B * d, Sn = (size_t)c->S32 * c->n;
     if (sum_ks) {
-        if (grow((u64**)&c->d_uall, &c->uall_cap, std::max<size_t>((size_t)P * ul * sizeof(uint32_t), 8)) ||
-            grow((u64**)&c->d_uk, &c->uk_cap, std::max<size_t>(B * d * ul * sizeof(uint32_t), 8)))
+        if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
+            grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * sizeof(int16_t), 8)) ||
+            grow((u64**)&c->d_dsk, &c->dsk_cap, std::max<size_t>(Bd * gu * Sn * sizeof(uint32_t), 8)) ||
+            grow((u64**)&c->d_uk, &c->uk_cap, std::max<size_t>(Bd * 2 * c->L * Sn * sizeof(uint32_t), 8)))
             return EXACTO_ERR_HIP;
-        c->ks_defer = c->d_uall;
+        if (int e = ensure_rs(c)) return e;
+        c->ks_defer = c->d_dall;
     }
     bool coef = false;
     const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
@@ -1591,9 +1596,11 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
                         c->stream);
     CHECK_LAUNCH();
     if (sum_ks) {
-        ks32_sum(c->d_uall, npairs, c->d_term_start, c->d_terms, c->d_uk, (int)B, (int)d, c->L, c->S32, c->n,
-                 c->d_p32, c->stream);
-        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)(B * d), c->L, c->S32, c->logn, c->d_kst, c->d_p32,
+        ks32_digit_sum(c->d_dall, npairs, c->d_term_start, c->d_terms, c->d_dk, (int)B, (int)d, (int)gu, c->n,
+                       c->stream);
+        ks32_digits(c->d_dk, c->d_dsk, (int)Bd, (int)gu, c->S32, c->logn, c->d_p32, c->stream);
+        ks32_mac(c->d_dsk, c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, c->S32, c->n, c->d_p32, c->stream);
+        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, c->S32, c->logn, c->d_kst, c->d_p32,
                  c->d_primes, c->stream);
         CHECK_LAUNCH();
     }

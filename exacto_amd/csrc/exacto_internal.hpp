@@ -195,10 +195,10 @@ struct CombineTerm {
 void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const CombineTerm* terms, u64* out, int items, int d, int n, int L,
                          const PrimeConst* primes, hipStream_t s);
-// ks32 sums for dBFV: out[item][k][cl][s][n] = sum over the item's products with i + j = k (combine
-// terms with coefficient 1) of U[item][pair][cl][s][n], mod p_s
-void ks32_sum(const uint32_t* U, int npairs, const int* term_start, const CombineTerm* terms, uint32_t* out,
-              int items, int d, int L, int S, int n, const Prime32* primes, hipStream_t st);
+// dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
+// coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n]
+void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, int16_t* out,
+                    int items, int d, int gu, int n, hipStream_t st);
 
 }  // namespace exacto
 

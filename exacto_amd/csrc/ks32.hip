@@ -378,23 +378,24 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     }
 }
 
-// dBFV: the products of one output limb k summed in the 31-bit basis before the (single) lift.
-// Residues are canonical (the MAC's red_s64), so each sum needs one conditional subtraction.
+// dBFV: the gadget digits of the products of one output limb k summed before their transforms.
+// Every step after the digits (NTT mod p_s, MAC with the key, lift) is linear in them, so the sum
+// of the products' key switches is the key switch of the summed digits (an integer identity; the
+// basis bound covers the sum, see setup_ks32).  D [item][pair][g][n] -> out [item][k][g][n].
 __global__ void __launch_bounds__(256)
-ks32_sum_kernel(const uint32_t* __restrict__ U, int npairs, const int* __restrict__ term_start,
-                const CombineTerm* __restrict__ terms, uint32_t* __restrict__ out, int d, int CLS, int S,
-                int n, int nsh, const Prime32* __restrict__ primes) {
-    const long row = blockIdx.x >> nsh;                  // (item * d + k) * CLS + cl * S + s
+ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __restrict__ term_start,
+                      const CombineTerm* __restrict__ terms, int16_t* __restrict__ out, int d, int gu, int n,
+                      int nsh) {
+    const long row = blockIdx.x >> nsh;                  // (item * d + k) * gu + g
     const int j = (int)(blockIdx.x & ((1u << nsh) - 1)) * 256 + threadIdx.x;
-    const int r = (int)(row % CLS);
-    const long ik = row / CLS;
+    const int g = (int)(row % gu);
+    const long ik = row / gu;
     const int k = (int)(ik % d);
     const long item = ik / d;
-    const uint32_t p = primes[r % S].p;
-    uint32_t acc = 0;
+    int acc = 0;
     for (int t = term_start[k]; t < term_start[k + 1]; ++t)
-        acc = red32(acc + U[((item * npairs + terms[t].pair) * CLS + r) * (long)n + j], p);
-    out[row * n + j] = acc;
+        acc += D[((item * npairs + terms[t].pair) * gu + g) * (long)n + j];
+    out[row * n + j] = (int16_t)acc;
 }
 
 // ---------------------------------------------------------------- launchers
@@ -479,13 +480,13 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
 #undef MAC_
 }
 
-void ks32_sum(const uint32_t* U, int npairs, const int* term_start, const CombineTerm* terms, uint32_t* out,
-              int items, int d, int L, int S, int n, const Prime32* primes, hipStream_t st) {
-    const long rows = (long)items * d * 2 * L * S;
+void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, int16_t* out,
+                    int items, int d, int gu, int n, hipStream_t st) {
+    const long rows = (long)items * d * gu;
     if (rows <= 0) return;
     const int nb = n / 256;   // n >= 1024, a power of two
-    hipLaunchKernelGGL(ks32_sum_kernel, dim3((unsigned)(rows * nb)), dim3(256), 0, st, U, npairs, term_start, terms,
-                       out, d, 2 * L * S, S, n, __builtin_ctz((unsigned)nb), primes);
+    hipLaunchKernelGGL(ks32_digit_sum_kernel, dim3((unsigned)(rows * nb)), dim3(256), 0, st, D, npairs, term_start,
+                       terms, out, d, gu, n, __builtin_ctz((unsigned)nb));
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
