@@ -386,16 +386,28 @@ __global__ void __launch_bounds__(256)
 ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __restrict__ term_start,
                       const CombineTerm* __restrict__ terms, int16_t* __restrict__ out, int d, int gu, int n,
                       int nsh) {
-    const long row = blockIdx.x >> nsh;                  // (item * d + k) * gu + g
-    const int j = (int)(blockIdx.x & ((1u << nsh) - 1)) * 256 + threadIdx.x;
-    const int g = (int)(row % gu);
-    const long ik = row / gu;
-    const int k = (int)(ik % d);
-    const long item = ik / d;
-    int acc = 0;
-    for (int t = term_start[k]; t < term_start[k + 1]; ++t)
-        acc += D[((item * npairs + terms[t].pair) * gu + g) * (long)n + j];
-    out[row * n + j] = (int16_t)acc;
+    // eight consecutive digits per thread (one 16-byte load per term), 2048 per block
+    const uint32_t row = blockIdx.x >> nsh;              // (item * d + k) * gu + g
+    const int j = (int)(blockIdx.x & ((1u << nsh) - 1)) * 2048 + 8 * threadIdx.x;
+    const uint32_t g = row % (uint32_t)gu;
+    const uint32_t ik = row / (uint32_t)gu;
+    const int k = (int)(ik % (uint32_t)d);
+    const long item = ik / (uint32_t)d;
+    int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+        const uint4 w = *reinterpret_cast<const uint4*>(D + ((item * npairs + terms[t].pair) * gu + g) * (long)n + j);
+        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            acc[2 * h] += (int)(int16_t)(v[h] & 0xFFFF);
+            acc[2 * h + 1] += (int)(int16_t)(v[h] >> 16);
+        }
+    }
+    uint4 o;
+    uint32_t* op = &o.x;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) op[h] = ((uint32_t)acc[2 * h] & 0xFFFF) | ((uint32_t)acc[2 * h + 1] << 16);
+    *reinterpret_cast<uint4*>(out + (long)row * n + j) = o;
 }
 
 // ---------------------------------------------------------------- launchers
@@ -484,9 +496,9 @@ void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const C
                     int items, int d, int gu, int n, hipStream_t st) {
     const long rows = (long)items * d * gu;
     if (rows <= 0) return;
-    const int nb = n / 256;   // n >= 1024, a power of two
-    hipLaunchKernelGGL(ks32_digit_sum_kernel, dim3((unsigned)(rows * nb)), dim3(256), 0, st, D, npairs, term_start,
-                       terms, out, d, gu, n, __builtin_ctz((unsigned)nb));
+    const int nb = n >= 2048 ? n / 2048 : 1;   // n >= 1024, a power of two; 2048 digits per block
+    hipLaunchKernelGGL(ks32_digit_sum_kernel, dim3((unsigned)(rows * nb)), dim3(n >= 2048 ? 256 : n / 8), 0, st, D,
+                       npairs, term_start, terms, out, d, gu, n, __builtin_ctz((unsigned)nb));
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
