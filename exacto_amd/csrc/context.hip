@@ -166,6 +166,20 @@ struct ProfRec {
     double bytes;
 };
 
+// A 31-bit auxiliary basis of the ks32 key switch (ks32.hip) with its device tables and the
+// relinearisation key converted to it.
+struct Ks32Basis {
+    int S = 0;
+    int sum_max = 0;              // dBFV key-switch sums the basis lifts exactly
+    bool long_runs = false;       // every prime below 2^32 / 3: 12 MAC products per reduction
+    Prime32* d_p32 = nullptr;
+    uint2* d_tw32 = nullptr;
+    Ks32Tables* d_kst = nullptr;
+    uint32_t* d_rs = nullptr;     // the relinearisation key in this basis
+    size_t rs_cap = 0;
+    bool rs_valid = false;
+};
+
 // Stream and per-chunk workspace of one extra pipeline lane (lane 0 is the context's own).
 constexpr int EXACTO_MAX_LANES = 4;
 struct LaneSet {
@@ -206,8 +220,11 @@ struct exacto_ctx {
     bool ks32 = true;
     int S32 = 0;                 // 0: not eligible for these parameters
     int ks32_sum_max = 0;        // key-switch sums that may be added before one lift (prod p bound)
+    bool ks32_long_runs = false; // every 31-bit prime below 2^32 / 3: 12 MAC products per reduction
+    Ks32Basis kw;                // wide basis (primes up to 2^31) for dBFV digit sums the primary cannot hold
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
-    int16_t *d_dall = nullptr, *d_dk = nullptr;   // dBFV: per-product and per-limb digit sums
+    int16_t* d_dall = nullptr;   // dBFV: per-product digits
+    void* d_dk = nullptr;        // ... and their per-limb sums (int16, or int32 when m B/2 > 2^15 - 1)
     uint32_t *d_dsk = nullptr, *d_uk = nullptr;   // their residues and key-switch sums in the 31-bit basis
     size_t dall_cap = 0, dk_cap = 0, dsk_cap = 0, uk_cap = 0;
     Prime32* d_p32 = nullptr;
@@ -368,32 +385,20 @@ static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
     ws = shoup_h(v, q);
 }
 
-// ks32.hip's auxiliary basis: the fewest primes p == 1 mod 2n in (2^30, 2^32 / 3), largest first, with
+// ks32.hip's auxiliary basis: the fewest primes p == 1 mod 2n in (2^30, 2^31), largest first, with
 // prod p > 2 G n floor(B/2) floor(q_max/2) (the magnitude bound of sum_g d_g * r_g, digits balanced
 // in [-B/2, B/2), key coefficients balanced).  Eligible: exact path, gadget base <= 2^16 (int16
 // digits), every ciphertext prime 2^60 - d with d < 2^24 (ks32_crt reduces with reduce_near60),
 // 1024 <= n <= 16384; S <= 4.
-static int setup_ks32(exacto_ctx* c) {
-    c->S32 = 0;
-    if (c->path != EXACTO_PATH_EXACT_RNS || c->gbase > 65536 || c->logn < 10 || c->logn > 14 || c->L > 4)
-        return 0;
-    u64 qmax = 0;
-    for (u64 q : c->ctq) {
-        if (q >= (1ull << 60) || q <= (1ull << 60) - (1ull << 24)) return 0;
-        qmax = std::max(qmax, q);
-    }
-    Big bound((u64)c->G);
-    bound.mul((u64)c->n);
-    bound.mul(c->gbase / 2);
-    bound.mul(qmax / 2);
-    bound.mul(2);
-    bound.add(1);
+// One 31-bit basis for ks32: the fewest primes p == 1 mod 2n below pmax (largest first, all above
+// 2^30) with prod p > `bound`, its twiddles, constants and Garner tables on the device.  sum_max:
+// how many key-switch sums (dBFV products of one output limb) the basis lifts exactly when they
+// are added first.  S = 0 when no basis of at most EXACTO_KS32_MAXS primes exists.
+static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
+    b->S = 0;
     std::vector<u64> ps;
     Big P(1);
     const u64 step = 2 * (u64)c->n;
-    // p < 2^32 / 3: sums of three residues fit 32 bits (ks32's reductions), and balanced products
-    // (< 2^59.1) leave room for twelve terms per signed 64-bit accumulation
-    const u64 pmax = (1ull << 32) / 3;
     for (u64 p = (pmax - 1) / step * step + 1; p > (1ull << 30) && ps.size() < EXACTO_KS32_MAXS; p -= step) {
         if (!is_prime_h(p)) continue;
         ps.push_back(p);
@@ -401,8 +406,9 @@ static int setup_ks32(exacto_ctx* c) {
         if (P.cmp(bound) > 0) break;
     }
     if (P.cmp(bound) <= 0 || ps.size() < 2) return 0;
-    // how many such sums the basis lifts exactly when added first (dBFV output limbs)
-    c->ks32_sum_max = 1;
+    b->long_runs = true;
+    for (u64 p : ps) b->long_runs &= p < (1ull << 32) / 3;
+    b->sum_max = 1;
     for (u64 m = 2; m <= 64; ++m) {
         Big bm((u64)c->G);
         bm.mul((u64)c->n);
@@ -411,7 +417,7 @@ static int setup_ks32(exacto_ctx* c) {
         bm.mul(2 * m);
         bm.add(1);
         if (P.cmp(bm) <= 0) break;
-        c->ks32_sum_max = (int)m;
+        b->sum_max = (int)m;
     }
     const int S = (int)ps.size(), n = c->n;
     std::vector<uint2> tw((size_t)S * 2 * n);
@@ -440,14 +446,14 @@ static int setup_ks32(exacto_ctx* c) {
         const u64 m63 = (1ull << 63) % p;
         Q.k63 = (uint32_t)(m63 == 0 ? 0 : p - m63);
     }
-    HIP_TRY(hipMalloc((void**)&c->d_tw32, tw.size() * sizeof(uint2)));
-    if (int e_ = upload(c, c->d_tw32, tw.data(), tw.size() * sizeof(uint2))) return e_;
+    HIP_TRY(hipMalloc((void**)&b->d_tw32, tw.size() * sizeof(uint2)));
+    if (int e_ = upload(c, b->d_tw32, tw.data(), tw.size() * sizeof(uint2))) return e_;
     for (int s = 0; s < S; ++s) {
-        pc[s].tw_fwd = c->d_tw32 + (size_t)s * 2 * n;
-        pc[s].tw_inv = c->d_tw32 + (size_t)s * 2 * n + n;
+        pc[s].tw_fwd = b->d_tw32 + (size_t)s * 2 * n;
+        pc[s].tw_inv = b->d_tw32 + (size_t)s * 2 * n + n;
     }
-    HIP_TRY(hipMalloc((void**)&c->d_p32, S * sizeof(Prime32)));
-    if (int e_ = upload(c, c->d_p32, pc.data(), S * sizeof(Prime32))) return e_;
+    HIP_TRY(hipMalloc((void**)&b->d_p32, S * sizeof(Prime32)));
+    if (int e_ = upload(c, b->d_p32, pc.data(), S * sizeof(Prime32))) return e_;
     Ks32Tables T;
     std::memset(&T, 0, sizeof(T));
     for (int s = 0; s < S; ++s)
@@ -475,9 +481,57 @@ static int setup_ks32(exacto_ctx* c) {
         const u64 pm = P.mod(q);
         T.negP[l] = pm == 0 ? 0 : q - pm;
     }
-    HIP_TRY(hipMalloc((void**)&c->d_kst, sizeof(Ks32Tables)));
-    if (int e_ = upload(c, c->d_kst, &T, sizeof(Ks32Tables))) return e_;
-    c->S32 = S;
+    HIP_TRY(hipMalloc((void**)&b->d_kst, sizeof(Ks32Tables)));
+    if (int e_ = upload(c, b->d_kst, &T, sizeof(Ks32Tables))) return e_;
+    b->S = S;
+    return 0;
+}
+
+// ks32.hip's auxiliary bases, bounding |sum_g d_g * r_g| <= G n floor(B/2) floor(q_max/2) (digits
+// balanced in [-B/2, B/2), key coefficients balanced).  Eligible: exact path, gadget base <= 2^16
+// (int16 digits), every ciphertext prime 2^60 - d with d < 2^24 (ks32_crt reduces with
+// reduce_near60), 1024 <= n <= 16384; S <= 4.
+//   primary: primes below 2^32 / 3, so that sums of three residues fit 32 bits and the MAC adds
+//            twelve balanced products (< 2^58.9) per reduction;
+//   wide:    primes up to 2^31 (seven products per reduction), kept only when it holds more
+//            dBFV digit sums than the primary (cfg4: two products per limb).
+// EXACTO_KS32_WIDE=0: no wide basis; =2: the wide basis as the primary too (A/B switch).
+static int setup_ks32(exacto_ctx* c) {
+    c->S32 = 0;
+    if (c->path != EXACTO_PATH_EXACT_RNS || c->gbase > 65536 || c->logn < 10 || c->logn > 14 || c->L > 4)
+        return 0;
+    u64 qmax = 0;
+    for (u64 q : c->ctq) {
+        if (q >= (1ull << 60) || q <= (1ull << 60) - (1ull << 24)) return 0;
+        qmax = std::max(qmax, q);
+    }
+    Big bound((u64)c->G);
+    bound.mul((u64)c->n);
+    bound.mul(c->gbase / 2);
+    bound.mul(qmax / 2);
+    bound.mul(2);
+    bound.add(1);
+    const char* wide_env = getenv("EXACTO_KS32_WIDE");
+    const int wide_mode = wide_env ? atoi(wide_env) : 1;
+    Ks32Basis prim;
+    if (int e = build_ks32_basis(c, wide_mode == 2 ? (1ull << 31) : (1ull << 32) / 3, qmax, bound, &prim)) return e;
+    if (wide_mode == 1) {
+        if (int e = build_ks32_basis(c, 1ull << 31, qmax, bound, &c->kw)) return e;
+        if (prim.S == 0 && c->kw.S > 0) {   // only the wide range holds the bound: it is the primary
+            prim = c->kw;
+            c->kw = Ks32Basis{};
+        } else if (c->kw.S > 0 && c->kw.sum_max <= prim.sum_max) {
+            free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst);
+            c->kw = Ks32Basis{};
+        }
+    }
+    if (prim.S == 0) return 0;
+    c->S32 = prim.S;
+    c->d_p32 = prim.d_p32;
+    c->d_tw32 = prim.d_tw32;
+    c->d_kst = prim.d_kst;
+    c->ks32_sum_max = prim.sum_max;
+    c->ks32_long_runs = prim.long_runs;
     return 0;
 }
 
@@ -733,6 +787,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_dall); free_dev(c->d_dk); free_dev(c->d_dsk); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
+    free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst); free_dev(c->kw.d_rs);
     free_dev(c->ws_DS); free_dev(c->ws_U);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
@@ -789,7 +844,7 @@ extern "C" uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* c, size_t num_keys)
     c->rlk_keys = num_keys;
     c->rlk_loaded = true;
     c->rlk_s_valid = false;  // contents change: companions recomputed before first use
-    c->rs_valid = false;     // and the auxiliary-basis key
+    c->rs_valid = false; c->kw.rs_valid = false;     // and the auxiliary-basis key
     return c->d_rlk;
 }
 
@@ -991,9 +1046,11 @@ static int crt_mode(const exacto_ctx* c) {
 // A key [keys][2][L][n] (NTT domain mod q_l) in ks32's auxiliary basis: INTT mod q_l
 // (coefficient domain), balanced, reduced mod each p_s, forward NTT mod p_s -> dst [keys][2L][S][n]
 // (grown as needed).
-static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t** dst, size_t* cap) {
+static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t** dst, size_t* cap, int S = 0,
+                            const Prime32* p32 = nullptr) {
+    if (!S) { S = c->S32; p32 = c->d_p32; }
     const long rows = (long)keys * 2 * c->L;
-    if (grow((u64**)dst, cap, std::max<size_t>((size_t)rows * c->S32 * c->n * sizeof(uint32_t), 8)))
+    if (grow((u64**)dst, cap, std::max<size_t>((size_t)rows * S * c->n * sizeof(uint32_t), 8)))
         return EXACTO_ERR_HIP;
     Scratch ks;
     HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream));
@@ -1002,7 +1059,7 @@ static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t
     nb.dst = ks.as<u64>(); nb.dst_item_stride = 2L * c->L * c->n;
     nb.ppi = 2 * c->L; nb.prime_base = 0; nb.period = c->L;
     if (int e = run_ntt(c, nb, rows, true)) return e;
-    ks32_key(ks.as<u64>(), *dst, rows, c->L, c->S32, c->logn, c->d_p32, c->d_primes, c->stream);
+    ks32_key(ks.as<u64>(), *dst, rows, c->L, S, c->logn, p32, c->d_primes, c->stream);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1015,6 +1072,17 @@ static int ensure_rs(exacto_ctx* c) {
     c->rs_cap = cap;
     if (e) return e;
     c->rs_valid = true;
+    return 0;
+}
+
+// ... and in the wide basis (dBFV digit sums), on first use after each key load
+static int ensure_rs_wide(exacto_ctx* c) {
+    if (c->kw.rs_valid) return 0;
+    size_t cap = c->kw.rs_cap;
+    const int e = ks32_convert_key(c, c->d_rlk, c->rlk_keys, &c->kw.d_rs, &cap, c->kw.S, c->kw.d_p32);
+    c->kw.rs_cap = cap;
+    if (e) return e;
+    c->kw.rs_valid = true;
     return 0;
 }
 
@@ -1123,7 +1191,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // coefficient domain; the forward NTT of R below then yields the relinearised result
             if (!c->ks_defer) {   // (deferred: the caller sums the digits of products first, dbfv_mul_core)
                 ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-                ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
+                ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
                 ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
                          c->stream);
                 CHECK_LAUNCH();
@@ -1573,18 +1641,27 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     // linear in the digits, so the products' int16 digits are summed per output limb (still int16)
     // and transformed, multiplied with the key and lifted once per limb instead of once per product
     // (cfg5: 8 instead of 36 products' worth of digit NTTs, MACs and lifts per dbfv_mul)
+    // The primary 31-bit basis when it holds the sums, else the wide one (primes up to 2^31).
     const size_t gu = std::min<size_t>(c->G, c->rlk_keys);
-    const bool sum_ks = c->S32 > 0 && c->ks32 && c->cached_sum_m > 0 && c->cached_sum_m <= c->ks32_sum_max &&
-                        (u64)c->cached_sum_m * (c->gbase / 2) <= 32767 && c->digit16 && c->gbase <= 65536 &&
-                        !c->fused_ks && c->rlk_loaded && gu > 0;
-    const size_t Bd = B * d, Sn = (size_t)c->S32 * c->n;
+    const int m = c->cached_sum_m;
+    const bool on = c->S32 > 0 && c->ks32 && m > 0 && c->digit16 && c->gbase <= 65536 && !c->fused_ks &&
+                    c->rlk_loaded && gu > 0;
+    const bool use_prim = on && m <= c->ks32_sum_max;
+    const bool use_wide = on && !use_prim && c->kw.S > 0 && m <= c->kw.sum_max;
+    const bool sum_ks = use_prim || use_wide;
+    const int S = use_wide ? c->kw.S : c->S32;
+    const Prime32* p32 = use_wide ? c->kw.d_p32 : c->d_p32;
+    const Ks32Tables* kst = use_wide ? c->kw.d_kst : c->d_kst;
+    const bool long_runs = use_wide ? c->kw.long_runs : c->ks32_long_runs;
+    const bool wide = (u64)m * (c->gbase / 2) > 32767;   // digit sums beyond int16
+    const size_t Bd = B * d, Sn = (size_t)S * c->n;
     if (sum_ks) {
         if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
-            grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * sizeof(int16_t), 8)) ||
+            grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * (wide ? 4 : 2), 8)) ||
             grow((u64**)&c->d_dsk, &c->dsk_cap, std::max<size_t>(Bd * gu * Sn * sizeof(uint32_t), 8)) ||
             grow((u64**)&c->d_uk, &c->uk_cap, std::max<size_t>(Bd * 2 * c->L * Sn * sizeof(uint32_t), 8)))
             return EXACTO_ERR_HIP;
-        if (int e = ensure_rs(c)) return e;
+        if (int e = use_wide ? ensure_rs_wide(c) : ensure_rs(c)) return e;
         c->ks_defer = c->d_dall;
     }
     bool coef = false;
@@ -1596,12 +1673,13 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
                         c->stream);
     CHECK_LAUNCH();
     if (sum_ks) {
-        ks32_digit_sum(c->d_dall, npairs, c->d_term_start, c->d_terms, c->d_dk, (int)B, (int)d, (int)gu, c->n,
+        ks32_digit_sum(c->d_dall, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)d, (int)gu, c->n,
                        c->stream);
-        ks32_digits(c->d_dk, c->d_dsk, (int)Bd, (int)gu, c->S32, c->logn, c->d_p32, c->stream);
-        ks32_mac(c->d_dsk, c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, c->S32, c->n, c->d_p32, c->stream);
-        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, c->S32, c->logn, c->d_kst, c->d_p32,
-                 c->d_primes, c->stream);
+        if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
+        else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
+        ks32_mac(c->d_dsk, use_wide ? c->kw.d_rs : c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, S, c->n, p32,
+                 long_runs, c->stream);
+        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
         CHECK_LAUNCH();
     }
     if (coef)
@@ -1881,7 +1959,7 @@ extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, doubl
         c->rlk_keys = num_keys;
         c->rlk_loaded = true;
         c->rlk_s_valid = false;
-        c->rs_valid = false;
+        c->rs_valid = false; c->kw.rs_valid = false;
     }
     return 0;
 }
@@ -2080,7 +2158,7 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
             launch_rows(c->ws_T + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
             CHECK_LAUNCH();
             ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-            ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->stream);
+            ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
             ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
             CHECK_LAUNCH();
             NttBatch rb{};

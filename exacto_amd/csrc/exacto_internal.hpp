@@ -95,7 +95,7 @@ void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, co
 // ---- ks32.hip: relinearisation MAC over the integers in an auxiliary basis of 31-bit primes ----
 #define EXACTO_KS32_MAXS 4
 struct Prime32 {
-    uint32_t p;                 // prime in (2^30, 2^32 / 3), p == 1 mod 2n
+    uint32_t p;                 // prime in (2^30, 2^31), p == 1 mod 2n
     uint32_t n_inv, n_inv_s;    // n^-1 and its Shoup companion floor(w 2^32 / p)
     uint32_t last_w, last_ws;   // psi_inv_rev[1] n^-1 (fused last inverse stage)
     uint32_t c32, c32s;         // 2^32 mod p
@@ -114,12 +114,14 @@ struct Ks32Tables {
 // int16 digits [items][G][n] -> DS [items][G][S][n], NTT mod p_s
 void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
                  hipStream_t st);
+void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+                   hipStream_t st);
 // key rows [rows][n] (coefficient domain, canonical mod q_{row % L}) -> RS [rows][S][n]
 void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
               const PrimeConst* qprimes, hipStream_t st);
 // U [items][2L][S][n] = sum_g DS (.) RS
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
-              const Prime32* primes, hipStream_t st);
+              const Prime32* primes, bool long_runs, hipStream_t st);
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
               const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);
@@ -196,9 +198,9 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const CombineTerm* terms, u64* out, int items, int d, int n, int L,
                          const PrimeConst* primes, hipStream_t s);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
-// coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n]
-void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, int16_t* out,
-                    int items, int d, int gu, int n, hipStream_t st);
+// coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n], int16 or (wide) int32
+void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, void* out,
+                    bool wide, int items, int d, int gu, int n, hipStream_t st);
 
 }  // namespace exacto
 

@@ -174,9 +174,10 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
 
 // ---------------------------------------------------------------- kernels
 
-template <int LOGN>
+// digits [item][g][n] (int16, or int32 for dBFV digit sums beyond int16) -> DS [item][g][s][n]
+template <int LOGN, typename DT>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
-ks32_digit_ntt_kernel(const int16_t* __restrict__ D16, uint32_t* __restrict__ DS, int G, int S,
+ks32_digit_ntt_kernel(const DT* __restrict__ D16, uint32_t* __restrict__ DS, int G, int S,
                       const Prime32* __restrict__ primes) {
     constexpr int N = 1 << LOGN, T = N / 16;
     __shared__ uint32_t lds[N];
@@ -185,7 +186,7 @@ ks32_digit_ntt_kernel(const int16_t* __restrict__ D16, uint32_t* __restrict__ DS
     const int s = (int)(b % (uint32_t)S);
     const long ig = b / (uint32_t)S;           // item * G + g
     const Prime32& P = primes[s];
-    const int16_t* src = D16 + ig * N;
+    const DT* src = D16 + ig * N;
     uint32_t x[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -225,17 +226,17 @@ ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int
     fwd32_store<LOGN>(x, lds, tid, P, RS + (long)b * N);
 }
 
-// Signed 64-bit x -> x mod p, canonical (p in (2^30, 2^32 / 3)): x = hi 2^32 + lo with hi signed;
+// Signed 64-bit x -> x mod p, canonical (p in (2^30, 2^31)): x = hi 2^32 + lo with hi signed;
 // (hi + 2^31) 2^32 by Shoup with 2^32 mod p, lo by two halvings, -2^63 by the constant k63.
 __device__ __forceinline__ uint32_t red_s64(long long x, const Prime32& P) {
     const uint32_t p = P.p;
     const uint32_t hu = (uint32_t)((unsigned long long)x >> 32) ^ 0x80000000u;
     const uint32_t a = red32(shoup32(hu, P.c32, P.c32s, p), p);
     const uint32_t b = red32(red32((uint32_t)x, 2 * p), p);
-    return red32(red32(a + b + P.k63, 2 * p), p);    // a + b + k63 < 3p < 2^32
+    return red32(red32(a + b, p) + P.k63, p);        // every partial sum < 2p < 2^32
 }
 
-// Signed 64-bit x (|x| < 2^63) -> a small non-negative value == x mod p, below 3p + 2^32 < 2^33.2:
+// Signed 64-bit x (|x| < 2^63) -> a small non-negative value == x mod p, below 3p + 2^32 < 2^33.6:
 // (hi + 2^31) 2^32 by Shoup with 2^32 mod p, plus lo, plus (-2^63) mod p.  Carried between runs
 // of signed products (7 VALU instead of red_s64's full reduction).
 __device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P) {
@@ -248,12 +249,12 @@ __device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P)
 // Block: 64 coefficients j of one prime s, CLB consecutive (c, l) pairs starting at cl0, and up to
 // 4 NW items; its key words (G * CLB * 64, balanced) are staged in LDS once.  Lane = coefficient,
 // wave w handles items it0 + w, it0 + w + NW, ...  Digit residues and key are stored balanced by
-// their transforms, |product| < (p/2)^2 < 2^58.9, so twelve signed products plus the carried
-// value (< 2^33.2) stay below 2^63 (one v_mad_i64_i32 each) before a lazy reduction.
+// their transforms, |product| < (p/2)^2 < 2^60, so seven signed products plus the carried value
+// (< 2^33.6) stay below 2^63 (one v_mad_i64_i32 each) before a lazy reduction.
 constexpr int KS_LS = 64;
-constexpr int KS_RUN = 12;  // signed products summed between reductions
-
-template <int CLB, int NW>
+// RUN: signed products summed between reductions: 12 for primes below 2^32 / 3 (products below
+// 2^58.9), 7 for primes up to 2^31 (products below 2^60; 7 * 2^60 + 2^33.6 < 2^63)
+template <int CLB, int NW, int RUN>
 __global__ void __launch_bounds__(NW * 64)
 ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t* __restrict__ U,
                 int G, int CL, int S, int items, int n, const Prime32* __restrict__ primes) {
@@ -277,20 +278,20 @@ ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t
         long long acc[CLB];
 #pragma unroll
         for (int c = 0; c < CLB; ++c) acc[c] = 0;
-        for (int g0 = 0; g0 < G; g0 += KS_RUN) {
+        for (int g0 = 0; g0 < G; g0 += RUN) {
             // unconditional (clamped) loads, all in flight together; digits past G are zeroed after
-            int d[KS_RUN];
+            int d[RUN];
 #pragma unroll
-            for (int e = 0; e < KS_RUN; ++e) d[e] = dp[(long)min(g0 + e, G - 1) * S * n];
+            for (int e = 0; e < RUN; ++e) d[e] = dp[(long)min(g0 + e, G - 1) * S * n];
 #pragma unroll
-            for (int e = 0; e < KS_RUN; ++e) d[e] = g0 + e < G ? d[e] : 0;
+            for (int e = 0; e < RUN; ++e) d[e] = g0 + e < G ? d[e] : 0;
 #pragma unroll
-            for (int e = 0; e < KS_RUN; ++e) {
+            for (int e = 0; e < RUN; ++e) {
                 const int* kg = kl + (min(g0 + e, G - 1) * CLB) * KS_LS + lane;
 #pragma unroll
                 for (int c = 0; c < CLB; ++c) acc[c] += (long long)d[e] * kg[c * KS_LS];
             }
-            if (g0 + KS_RUN < G) {
+            if (g0 + RUN < G) {
 #pragma unroll
                 for (int c = 0; c < CLB; ++c) acc[c] = red_s64_lazy(acc[c], P);
             }
@@ -382,9 +383,10 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
 // Every step after the digits (NTT mod p_s, MAC with the key, lift) is linear in them, so the sum
 // of the products' key switches is the key switch of the summed digits (an integer identity; the
 // basis bound covers the sum, see setup_ks32).  D [item][pair][g][n] -> out [item][k][g][n].
+template <typename OT>
 __global__ void __launch_bounds__(256)
 ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __restrict__ term_start,
-                      const CombineTerm* __restrict__ terms, int16_t* __restrict__ out, int d, int gu, int n,
+                      const CombineTerm* __restrict__ terms, OT* __restrict__ out, int d, int gu, int n,
                       int nsh) {
     // eight consecutive digits per thread (one 16-byte load per term), 2048 per block
     const uint32_t row = blockIdx.x >> nsh;              // (item * d + k) * gu + g
@@ -403,20 +405,31 @@ ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __re
             acc[2 * h + 1] += (int)(int16_t)(v[h] >> 16);
         }
     }
-    uint4 o;
-    uint32_t* op = &o.x;
+    if constexpr (sizeof(OT) == 2) {
+        uint4 o;
+        uint32_t* op = &o.x;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) op[h] = ((uint32_t)acc[2 * h] & 0xFFFF) | ((uint32_t)acc[2 * h + 1] << 16);
-    *reinterpret_cast<uint4*>(out + (long)row * n + j) = o;
+        for (int h = 0; h < 4; ++h) op[h] = ((uint32_t)acc[2 * h] & 0xFFFF) | ((uint32_t)acc[2 * h + 1] << 16);
+        *reinterpret_cast<uint4*>(out + (long)row * n + j) = o;
+    } else {
+        int4* o4 = reinterpret_cast<int4*>(out + (long)row * n + j);
+        o4[0] = make_int4(acc[0], acc[1], acc[2], acc[3]);
+        o4[1] = make_int4(acc[4], acc[5], acc[6], acc[7]);
+    }
 }
 
 // ---------------------------------------------------------------- launchers
 
 template <int LOGN>
-static void ks32_launch_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, const Prime32* primes,
+static void ks32_launch_digits(const void* D, bool wide, uint32_t* DS, int items, int G, int S, const Prime32* primes,
                                hipStream_t st) {
-    hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN>), dim3((unsigned)((long)items * G * S)), dim3((1 << LOGN) / 16), 0,
-                       st, D16, DS, G, S, primes);
+    const dim3 grid((unsigned)((long)items * G * S)), block((1 << LOGN) / 16);
+    if (wide)
+        hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int32_t>), grid, block, 0, st, (const int32_t*)D, DS, G, S,
+                           primes);
+    else
+        hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int16_t>), grid, block, 0, st, (const int16_t*)D, DS, G, S,
+                           primes);
 }
 
 template <int LOGN>
@@ -451,7 +464,15 @@ static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items,
 void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
                  hipStream_t st) {
     if (items <= 0) return;
-#define CALL(L_) ks32_launch_digits<L_>(D16, DS, items, G, S, primes, st)
+#define CALL(L_) ks32_launch_digits<L_>(D16, false, DS, items, G, S, primes, st)
+    KS32_SWITCH(logn, CALL)
+#undef CALL
+}
+
+void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+                   hipStream_t st) {
+    if (items <= 0) return;
+#define CALL(L_) ks32_launch_digits<L_>(D, true, DS, items, G, S, primes, st)
     KS32_SWITCH(logn, CALL)
 #undef CALL
 }
@@ -465,7 +486,7 @@ void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, con
 }
 
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
-              const Prime32* primes, hipStream_t st) {
+              const Prime32* primes, bool long_runs, hipStream_t st) {
     if (items <= 0) return;
     const int CL = 2 * L;
     // (c, l) pairs per block: the largest divisor of 2L whose key slice (G * CLB * 64 words) fits
@@ -478,8 +499,12 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
     const dim3 grid((unsigned)((n / KS_LS) * S * (CL / CLB)), (unsigned)((items + 4 * NW - 1) / (4 * NW)));
     const int* ds = reinterpret_cast<const int*>(DS);
     const int* rs = reinterpret_cast<const int*>(RS);
-#define MAC_(C_, W_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
-#define MAC(C_) do { if (NW == 8) MAC_(C_, 8); else MAC_(C_, 4); } while (0)
+#define MAC_(C_, W_, R_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_, R_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
+#define MAC(C_)                                                  \
+    do {                                                         \
+        if (long_runs) { if (NW == 8) MAC_(C_, 8, 12); else MAC_(C_, 4, 12); } \
+        else { if (NW == 8) MAC_(C_, 8, 7); else MAC_(C_, 4, 7); }          \
+    } while (0)
     switch (CLB) {
         case 8: MAC(8); break;
         case 6: MAC(6); break;
@@ -492,13 +517,18 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
 #undef MAC_
 }
 
-void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, int16_t* out,
-                    int items, int d, int gu, int n, hipStream_t st) {
+void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, void* out,
+                    bool wide, int items, int d, int gu, int n, hipStream_t st) {
     const long rows = (long)items * d * gu;
     if (rows <= 0) return;
     const int nb = n >= 2048 ? n / 2048 : 1;   // n >= 1024, a power of two; 2048 digits per block
-    hipLaunchKernelGGL(ks32_digit_sum_kernel, dim3((unsigned)(rows * nb)), dim3(n >= 2048 ? 256 : n / 8), 0, st, D,
-                       npairs, term_start, terms, out, d, gu, n, __builtin_ctz((unsigned)nb));
+    const dim3 grid((unsigned)(rows * nb)), block(n >= 2048 ? 256 : n / 8);
+    if (wide)
+        hipLaunchKernelGGL(ks32_digit_sum_kernel<int32_t>, grid, block, 0, st, D, npairs, term_start, terms,
+                           (int32_t*)out, d, gu, n, __builtin_ctz((unsigned)nb));
+    else
+        hipLaunchKernelGGL(ks32_digit_sum_kernel<int16_t>, grid, block, 0, st, D, npairs, term_start, terms,
+                           (int16_t*)out, d, gu, n, __builtin_ctz((unsigned)nb));
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
