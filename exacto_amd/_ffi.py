@@ -34,7 +34,7 @@ class CtxInfo(C.Structure):
                 ("num_aux_moduli", C.c_size_t), ("num_internal_aux", C.c_size_t),
                 ("gadget_digits", C.c_size_t), ("gadget_base", C.c_uint64),
                 ("plain_modulus", C.c_uint64), ("mul_path", C.c_int), ("device", C.c_int),
-                ("ks32_primes", C.c_int)]
+                ("ks32_primes", C.c_int), ("psum_max", C.c_int)]
 
 
 _lib = None
@@ -252,6 +252,7 @@ class HipContext:
         self.path = info.mul_path
         self.num_internal_aux = info.num_internal_aux
         self.ks32_primes = info.ks32_primes
+        self.psum_max = info.psum_max
         self.ct_moduli = [int(q) for q in ct_moduli]
         self.plain_modulus = int(info.plain_modulus)
 

@@ -223,6 +223,18 @@ struct exacto_ctx {
     bool ks32_long_runs = false; // every 31-bit prime below 2^32 / 3: 12 MAC products per reduction
     Ks32Basis kw;                // wide basis (primes up to 2^31) for dBFV digit sums the primary cannot hold
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
+    // dBFV psum (EXACTO_PSUM=0: off): an output limb's c0 / c1 scaled once from the sum of its
+    // products' tensors in the auxiliary primes (run_mul, dbfv_mul_core); psum_max = the largest
+    // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
+    bool psum_env = true;
+    int psum_max = 0;
+    struct PsumPlan {
+        bool on = false;
+        int d = 0, npairs = 0;
+        const int* term_start = nullptr;
+        const CombineTerm* terms = nullptr;
+        u64* out = nullptr;       // [B][d][2][L][n], coefficient domain
+    } psum;
     int16_t* d_dall = nullptr;   // dBFV: per-product digits
     void* d_dk = nullptr;        // ... and their per-limb sums (int16, or int32 when m B/2 > 2^15 - 1)
     uint32_t *d_dsk = nullptr, *d_uk = nullptr;   // their residues and key-switch sums in the 31-bit basis
@@ -737,6 +749,18 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
         }
         c->K = (int)c->int_aux.size();
         for (u64 p : c->int_aux) c->primes.push_back(p);
+        // |r| <= p n Q / 2 + 1 for every scaled tensor component (|T| <= n Q^2 / 2), so a sum of m of
+        // them is liftable from P (centred) when m (p n Q + 2) < P
+        Big X(plain);
+        X.mul(n);
+        for (u64 q : c->ctq) X.mul(q);
+        X.add(2);
+        for (u64 m = 1; m <= 64; ++m) {
+            Big Y = X;
+            Y.mul(m);
+            if (Y.cmp(P) >= 0) break;
+            c->psum_max = (int)m;
+        }
     }
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
@@ -764,6 +788,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     if (int rc = setup_ks32(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
@@ -807,6 +832,7 @@ extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
     info->mul_path = c->path;
     info->device = c->device;
     info->ks32_primes = c->ks32 ? c->S32 : 0;
+    info->psum_max = c->psum_env ? c->psum_max : 0;
     return 0;
 }
 
@@ -897,7 +923,7 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     return 0;
 }
 
-static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt) {
+static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only = false) {
     const int NP = c->L + c->K;
     ProfRec rec{};
     if (c->prof) {
@@ -911,7 +937,7 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt) {
         // the fused product (mulmod_near60) needs d = 2^60 - q < 2^24; the asm rounds d < 2^32
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
     }
-    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60);
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only);
     CHECK_LAUNCH();
     if (c->prof) {
         HIP_TRY(hipEventRecord(rec.b, c->stream));
@@ -1108,7 +1134,10 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     const int n = c->n, L = c->L, K = c->K, NP = L + K;
     const long Ln = (long)L * n;
     const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
-    const size_t C = std::min<size_t>(c->chunk, (size_t)P);
+    const exacto_ctx::PsumPlan& ps = c->psum;
+    // psum: chunks hold whole dBFV items (their products are summed inside the chunk)
+    const size_t C = ps.on ? std::max<size_t>(ps.npairs, std::min<size_t>(c->chunk, (size_t)P) / ps.npairs * ps.npairs)
+                           : std::min<size_t>(c->chunk, (size_t)P);
     if (int e = ensure_workspace(c, C)) return e;
     // int16 gadget digits (base <= 2^16, exact path): the scale kernel writes each digit once
     const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
@@ -1156,7 +1185,12 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             o.eb_off += s;
         }
         // 4+5. tensor product in every prime, fused into the inverse NTT of its components
-        if (int e = run_inv_tensor(c, o, cnt)) return e;
+        if (int e = run_inv_tensor(c, o, cnt, ps.on)) return e;
+        if (ps.on) {   // the output limbs' c0 / c1 auxiliary residues, summed over their products
+            launch_inv_tensor_sum(o, c->ws_T, cnt / ps.npairs, ps.d, ps.npairs, ps.term_start, ps.terms, c->logn, L,
+                                  K, c->d_primes, c->stream);
+            CHECK_LAUNCH();
+        }
         // 6. scale-and-round (+ gadget digits of the third component)
         u64* R = out + s * out_stride;
         const int ncomp = relin ? 2 : 3;
@@ -1167,8 +1201,15 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D,
                                d16 ? (c->ks_defer ? c->ks_defer + s * (long)guse * n : c->ws_D16) : nullptr, guse,
                                cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
-                               c->stream, c->h_crt.gshift);
+                               c->stream, c->h_crt.gshift, ps.on);
         CHECK_LAUNCH();
+        if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
+            const long item0 = s / ps.npairs;
+            if (!launch_psum_scale(c->ws_T, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
+                                   ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream))
+                return fail(EXACTO_ERR_HIP, "internal: psum scale not available for these limbs");
+            CHECK_LAUNCH();
+        }
         // 7. forward NTT of the results (and digits)
         NttBatch rb{};
         rb.src = R; rb.src_off = nullptr; rb.src_item_stride = out_stride;
@@ -1664,14 +1705,35 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
         if (int e = use_wide ? ensure_rs_wide(c) : ensure_rs(c)) return e;
         c->ks_defer = c->d_dall;
     }
+    // psum: each output limb's c0 / c1 from one scale of its products' summed tensors (the
+    // auxiliary-prime residues summed in the NTT domain and inverse-transformed once per limb, the
+    // per-product corrections from the ciphertext-prime residues; exact_psum_sp_kernel), written
+    // straight to out: no per-product c0 / c1 and no dbfv_combine pass.  Needs the summed digits
+    // (so the third component is per product only for its digits), shared extensions, special
+    // primes with K = L + 1 (30-bit-limb scale) and the asm tensor kernels.
+    bool near60 = c->ntt_asm && c->ntt_asm_inv;
+    for (u64 q : c->primes) near60 &= q < (1ull << 60) && q > (1ull << 60) - (1ull << 24);
+    const bool psum = sum_ks && c->psum_env && m <= c->psum_max && op.ea != nullptr && near60 &&
+                      (c->logn == 12 || c->logn == 13) && exact_scale_sp_ok(c->L, c->K, crt_mode(c));
+    if (psum) {
+        c->psum.on = true;
+        c->psum.d = (int)d;
+        c->psum.npairs = npairs;
+        c->psum.term_start = c->d_term_start;
+        c->psum.terms = c->d_terms;
+        c->psum.out = out;
+    }
     bool coef = false;
     const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
     c->ks_defer = nullptr;
+    c->psum.on = false;
     if (rc) return rc;
     if (sum_ks && !coef) return fail(EXACTO_ERR_HIP, "internal: ks32 sums without the ks32 key switch");
-    launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L, c->d_primes,
-                        c->stream);
-    CHECK_LAUNCH();
+    if (!psum) {
+        launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L,
+                            c->d_primes, c->stream);
+        CHECK_LAUNCH();
+    }
     if (sum_ks) {
         ks32_digit_sum(c->d_dall, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)d, (int)gu, c->n,
                        c->stream);

@@ -153,8 +153,10 @@ bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period,
 // out = INTT(A (.) B) row by row ([rows][n], row r mod prime r % period); out may alias A or B
 void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period, int logn, bool lazy, bool asm_inv,
                     const PrimeConst* primes, hipStream_t s);
+// p2only: every component of the ciphertext primes, the third only of the auxiliary primes (dBFV
+// psum; asm_inv and n = 4096 / 8192 only)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false);
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);
@@ -169,9 +171,12 @@ void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const Prim
                        int K, hipStream_t s);
 // D16 (or nullptr): gadget digits of the third component as int16 [item][g][n] instead of D;
 // gshift: log2 of the gadget base (-1 if not a power of two), selects the digit code at launch
+// the 30-bit-limb scale kernel (exact_scale_sp_kernel) serves these limb counts and CRT mode
+bool exact_scale_sp_ok(int L, int K, int mode);
+// c2only: the third component's rows alone (its gadget digits; dBFV psum, mode 3 with K = L + 1 only)
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift = -1);
+                        int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);
@@ -197,6 +202,17 @@ struct CombineTerm {
 void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const CombineTerm* terms, u64* out, int items, int d, int n, int L,
                          const PrimeConst* primes, hipStream_t s);
+// dBFV psum (special primes, K = L + 1, n = 4096 / 8192): the auxiliary-prime residues of each output
+// limb's c0 / c1 tensors summed over its products, inverse-transformed into the auxiliary rows of
+// product ib npairs + k of T (ntt.hip); then exact_psum_sp_kernel: the scale of those sums plus the
+// per-product corrections from the ciphertext-prime residues, the centred lift to Q, written to
+// out [items_b][d][2][L][n] (coefficient domain, kernels.hip)
+void launch_inv_tensor_sum(const Operands& op, u64* T, int items_b, int d, int npairs, const int* term_start,
+                           const CombineTerm* terms, int logn, int L, int K, const PrimeConst* primes,
+                           hipStream_t s);
+bool launch_psum_scale(const u64* T, u64* out, int items_b, int d, int npairs, const int* term_start,
+                       const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
+                       hipStream_t s);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
 // coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n], int16 or (wide) int32
 void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, void* out,

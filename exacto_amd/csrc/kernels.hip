@@ -541,12 +541,12 @@ template <int LT, int DIG>
 __global__ void __launch_bounds__(TPB)
 exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
                       u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n,
-                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes, int c2only) {
     ROW_SETUP(n)
     constexpr int L = LT, K = LT + 1, NP = L + K;
-    const long item = row / 3;
-    const int comp = (int)(row - item * 3);
-    const u64* Tin = T + row * NP * n + j;
+    const long item = c2only ? row : row / 3;
+    const int comp = c2only ? 2 : (int)(row - item * 3);
+    const u64* Tin = T + (item * 3 + comp) * NP * n + j;
     u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
@@ -605,10 +605,112 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
     }
 }
 
+// dBFV psum: one output limb k's component c (0 or 1) = sum over its products of their scaled
+// components, computed as one scale.  Per product, r = (p T - s) / Q with s = [p T]_Q centred;
+// in an auxiliary prime p_a that is r = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs (the v_k and
+// negs from the product's ciphertext-prime residues).  The first term is linear in T, so its sum
+// over the products is the summed auxiliary residue (ntt_inv_tensor_sum_kernel); the others are
+// added product by product.  R = sum r is then lifted from P exactly as exact_scale_sp_kernel
+// lifts one r: the context checks m (p n Q + 2) < P (|R| < P / 2, psum_max).  Bit-identical to
+// summing the per-product results mod q_i (dbfv_combine_kernel), which is what it replaces.
+// row = (ib d + k) 2 + c; T as the tensor kernels leave it (summed rows at product ib npairs + k).
+template <int LT>
+__global__ void __launch_bounds__(TPB)
+exact_psum_sp_kernel(const u64* __restrict__ T, u64* __restrict__ out, int d, int npairs,
+                     const int* __restrict__ term_start, const CombineTerm* __restrict__ terms, int n,
+                     const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    constexpr int L = LT, K = LT + 1, NP = L + K;
+    const int c = (int)(row & 1);
+    const long r2 = row >> 1;
+    const int k = (int)(r2 % d);
+    const long ib = r2 / d;
+    u64 carry[K];
+    {
+        const u64* Ts = T + ((ib * npairs + k) * 3 + c) * (long)NP * n + j;
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+            const u64 ta = Ts[(long)(L + a) * n];   // canonical
+            Dot30 A{0, 0, 0};
+            dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->pq_w[a]);
+            carry[a] = dot30_fold(A, primes[L + a].q);
+        }
+    }
+    for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+        const u64* Tin = T + ((ib * npairs + terms[t].pair) * 3 + c) * (long)NP * n + j;
+        u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+        for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
+        garner_q_fast<LT>(v, u, L, C, primes);
+        const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+        uint32_t v0[L], v1[L];
+#pragma unroll
+        for (int kk = 0; kk < L; ++kk) {
+            v0[kk] = (uint32_t)v[kk] & M30;
+            v1[kk] = (uint32_t)(v[kk] >> 30);
+        }
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+            const u64 pa = primes[L + a].q;
+            Dot30 A{carry[a] + (negs ? 1ull : 0ull), 0, 0};   // carry < p_a: a0's constant stays < 2^60
+#pragma unroll
+            for (int kk = 0; kk < L; ++kk) dot30_mac(A, v0[kk], v1[kk], pa - C->qpq_w[kk][a]);
+            carry[a] = dot30_fold(A, pa);
+        }
+    }
+    u64 w[EXACTO_MAX_K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const u64 pa = primes[L + a].q, np = (u64)0 - pa;
+        u64 acc = carry[a];
+#pragma unroll
+        for (int kk = 0; kk < a; ++kk) acc = shoup_mul_nq(acc + 2 * pa - w[kk], C->gp_w[a][kk], C->gp_ws[a][kk], np);
+        w[a] = (a > 0 && acc >= pa) ? acc - pa : acc;
+    }
+    const bool negr = mr_greater<EXACTO_MAX_K>(w, C->halfP_mr, K);
+    uint32_t w0[K], w1[K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        w0[a] = (uint32_t)w[a] & M30;
+        w1[a] = (uint32_t)(w[a] >> 30);
+    }
+    u64* o = out + row * L * (long)n + j;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const u64 q = primes[i].q;
+        Dot30 A{negr ? q - C->ppref_w[K][i] : 0, 0, 0};
+#pragma unroll
+        for (int a = 0; a < K; ++a) dot30_mac(A, w0[a], w1[a], C->ppref_w[a][i]);
+        o[(long)i * n] = dot30_fold(A, q);
+    }
+}
+
+bool launch_psum_scale(const u64* T, u64* out, int items_b, int d, int npairs, const int* term_start,
+                       const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
+                       hipStream_t s) {
+    const long blocks = (long)items_b * d * 2 * blocks_per_row(n);
+    if (blocks == 0) return true;
+#define PSUM_(LT) hipLaunchKernelGGL((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, out, d, npairs, \
+                                     term_start, terms, n, ct, primes)
+    switch (L) {
+        case 1: PSUM_(1); break;
+        case 2: PSUM_(2); break;
+        case 3: PSUM_(3); break;
+        case 4: PSUM_(4); break;
+        case 5: PSUM_(5); break;
+        case 6: PSUM_(6); break;
+        default: return false;
+    }
+#undef PSUM_
+    return true;
+}
+
+bool exact_scale_sp_ok(int L, int K, int mode) { return mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30(); }
+
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift) {
-    const long blocks = (long)items * 3 * blocks_per_row(n);
+                        int K, int mode, hipStream_t s, int gshift, bool c2only) {
+    const long blocks = (long)items * (c2only ? 1 : 3) * blocks_per_row(n);
     if (blocks == 0) return;
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
         // digit code: 0 none, 1 int16 fields of the magnitude (base 2^sh, sh | 32), 2 gadget_digits
@@ -616,7 +718,7 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
                         : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? 1 : 2;
 #define SCALE30_(LT, DG)                                                                                        \
     hipLaunchKernelGGL((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
-                       D16, guse, n, ct, primes)
+                       D16, guse, n, ct, primes, c2only ? 1 : 0)
 #define SCALE30(LT)                         \
     do {                                    \
         if (dig == 1) SCALE30_(LT, 1);      \

@@ -816,7 +816,7 @@ template <int LOGN, bool LAZY, bool ASM = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                      const PrimeConst* __restrict__ primes, int remap) {
+                      const PrimeConst* __restrict__ primes, int remap, int p2only = 0) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
@@ -827,9 +827,13 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     // the three components of one (item, prime) read overlapping inputs (c1 reads c0's and c2's):
     // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
     const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
-    const long item = p / (3 * NP);
-    const int rem = (int)(p - item * 3 * NP);
-    const int t = rem / 3, c = rem - t * 3;
+    // p2only (dBFV sums of P residues, launch_inv_tensor_sum): 3L + K blocks per item, every
+    // component of the ciphertext primes, the third only of the auxiliary primes
+    const int per = p2only ? 3 * L + K : 3 * NP;
+    const long item = p / per;
+    const int rem = (int)(p - item * per);
+    const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);
+    const int c = (!p2only || rem < 3 * L) ? rem - t * 3 : 2;
     const PrimeConst& P = primes[t];
     const u64 *A0, *A1, *B0, *B1;
     if (t < L) {
@@ -1152,7 +1156,7 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(2)))
 ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                       const PrimeConst* __restrict__ primes) {
+                       const PrimeConst* __restrict__ primes, int per) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
@@ -1160,9 +1164,10 @@ ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restric
     __shared__ u64 stash[N];   // c2 while c0 and c1 are transformed (lane-interleaved: no bank conflicts)
     const int tid = threadIdx.x;
     const int NP = L + K;
+    // per = NP, or L (psum: the auxiliary primes' third components by ntt_inv_tensor_c2_kernel)
     const long p = blockIdx.x;
-    const long item = p / NP;
-    const int t = (int)(p - item * NP);
+    const long item = p / per;
+    const int t = (int)(p - item * per);
     const PrimeConst& P = primes[t];
     const u64 *A0, *A1, *B0, *B1;
     if (t < L) {
@@ -1219,9 +1224,116 @@ ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restric
     for (int k = 0; k < 16; ++k) dst[2L * NP * N + elem_index<LAST_LO>(tid, k)] = c2[k];
 }
 
+// psum: the third tensor component alone in the auxiliary primes (shared extensions), block =
+// (item, a): c2 = a1 b1 of prime L + a, inverse-transformed into T[item][2][L + a].
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
+ntt_inv_tensor_c2_kernel(Operands op, u64* __restrict__ Tout, int L, int K, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const long item = blockIdx.x / K;
+    const int a = (int)(blockIdx.x - item * K);
+    const PrimeConst& P = primes[L + a];
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    const ulonglong2* s1 = reinterpret_cast<const ulonglong2*>(op.ea + (long)op.ea_off[item] + (long)(K + a) * N + 16 * tid);
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(op.eb + (long)op.eb_off[item] + (long)(K + a) * N + 16 * tid);
+    u64 x[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const ulonglong2 u = s1[e], v = s2[e];
+        x[2 * e] = mulmod_near60(u.x, v.x, dq);
+        x[2 * e + 1] = mulmod_near60(u.y, v.y, dq);
+    }
+    inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
+    u64* dst = Tout + ((item * 3 + 2) * (L + K) + L + a) * N;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dst[elem_index<LAST_LO>(tid, e)] = x[e];
+}
+
+// dBFV, psum (dbfv_mul_core): the auxiliary-prime residues of an output limb's c0 and c1 tensors
+// summed over its products in the NTT domain, then one inverse transform per (limb, component,
+// prime) instead of one per product.  Every step of the scale up to the Garner over P is linear
+// in T (r = T (p Q^-1) + sum_k v_k (...) + negs mod p_a), so exact_psum_sp_kernel adds the
+// per-product corrections to these sums.  Block = ((ib d + k) 2 + c) K + a; the result goes to
+// the (unused) auxiliary rows of product ib npairs + k of T: [prod][c][L + a][n].
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
+ntt_inv_tensor_sum_kernel(Operands op, u64* __restrict__ Tout, int L, int K, int d, int npairs,
+                          const int* __restrict__ term_start, const CombineTerm* __restrict__ terms,
+                          const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int NP = L + K;
+    const long b = blockIdx.x;
+    const int a = (int)(b % K);
+    const long r1 = b / K;
+    const int c = (int)(r1 & 1);
+    const long r2 = r1 >> 1;
+    const int k = (int)(r2 % d);
+    const long ib = r2 / d;
+    const PrimeConst& P = primes[L + a];
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    const u64 q2 = P.two_q;
+    auto load = [&](const u64* src, u64 (&v)[16]) {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const ulonglong2 w = s2[e];
+            v[2 * e] = w.x;
+            v[2 * e + 1] = w.y;
+        }
+    };
+    // products < 2q (mulmod_near60); the sum is kept below 2q (the inverse rounds take < 4q)
+    auto mac = [&](u64 (&acc)[16], const u64* A, const u64* B) {
+        u64 x[16], y[16];
+        load(A, x);
+        load(B, y);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const u64 v = acc[e] + mulmod_near60(x[e], y[e], dq);
+            acc[e] = v >= q2 ? v - q2 : v;
+        }
+    };
+    u64 acc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0;
+    for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+        const long pr = ib * npairs + terms[t].pair;
+        const u64* EA = op.ea + (long)op.ea_off[pr] + (long)a * N;
+        const u64* EB = op.eb + (long)op.eb_off[pr] + (long)a * N;
+        if (c == 0) {
+            mac(acc, EA, EB);                              // a0 b0
+        } else {
+            mac(acc, EA, EB + (long)K * N);                // a0 b1
+            mac(acc, EA + (long)K * N, EB);                // a1 b0
+        }
+    }
+    inv_rounds_asm<LOGN, 0>(acc, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
+    u64* dst = Tout + (((ib * npairs + k) * 3 + c) * NP + L + a) * N;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dst[elem_index<LAST_LO>(tid, e)] = acc[e];
+}
+
+void launch_inv_tensor_sum(const Operands& op, u64* T, int items_b, int d, int npairs, const int* term_start,
+                           const CombineTerm* terms, int logn, int L, int K, const PrimeConst* primes,
+                           hipStream_t s) {
+    const long blocks = (long)items_b * d * 2 * K;
+    if (blocks == 0) return;
+    if (logn == 12)
+        hipLaunchKernelGGL((ntt_inv_tensor_sum_kernel<12>), dim3(blocks), dim3(256), 0, s, op, T, L, K, d, npairs,
+                           term_start, terms, primes);
+    else if (logn == 13)
+        hipLaunchKernelGGL((ntt_inv_tensor_sum_kernel<13>), dim3(blocks), dim3(512), 0, s, op, T, L, K, d, npairs,
+                           term_start, terms, primes);
+}
+
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -1231,13 +1343,23 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
     const bool t3 = t3env >= 0 ? t3env == 1 : LOGN == 13;
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv && t3) {
-            hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(blocks / 3), dim3(threads), 0, s, op, extP, T, L, K,
-                               primes);
+            // blocks = items * 3 (L + K); psum: the ciphertext primes here, the auxiliary c2 apart
+            const long items = blocks / (3 * (L + K));
+            if (p2only) {
+                hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * L), dim3(threads), 0, s, op, extP, T, L,
+                                   K, primes, L);
+                hipLaunchKernelGGL((ntt_inv_tensor_c2_kernel<LOGN>), dim3(items * K), dim3(threads), 0, s, op, T, L, K,
+                                   primes);
+            } else {
+                hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * (L + K)), dim3(threads), 0, s, op, extP, T,
+                                   L, K, primes, L + K);
+            }
             return;
         }
         if (asm_inv) {
-            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(blocks), dim3(threads), 0, s, op, extP,
-                               T, L, K, primes, remap);
+            const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
+            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
+                               T, L, K, primes, remap, p2only);
             return;
         }
     }
@@ -1250,9 +1372,14 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
+    if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
+        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
+        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
+        return;
+    }
     switch (logn) {
         case 4: launch_it<4>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 5: launch_it<5>(op, extP, T, blocks, L, K, lazy, primes, s); break;

@@ -76,6 +76,7 @@ typedef struct exacto_ctx_info {
     int mul_path;             /* enum exacto_mul_path */
     int device;
     int ks32_primes;          /* primes of the 31-bit key-switch basis in use (0: limb-wise MAC) */
+    int psum_max;             /* dbfv_mul: products per output limb scaled as one sum (0: per product) */
 } exacto_ctx_info;
 
 /* ---- context: replaces BfvParamsBuilder::build + RnsBasis::new + make_plan ----

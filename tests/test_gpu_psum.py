@@ -1,0 +1,85 @@
+"""dBFV psum: each output limb's c0 / c1 scaled once from the sum of its products' tensors
+(ntt_inv_tensor_sum_kernel + exact_psum_sp_kernel) instead of per product and summed after
+(dbfv_combine_kernel, EXACTO_PSUM=0).
+
+Reference: dbfv_mul (src/dbfv/eval.rs:82-149): d^2 bfv_mul_and_relin (src/bfv/eval.rs:73-82, the
+exact tensor-and-round of eval.rs:113-147, 711-831), summed per output limb, then reduce
+(src/dbfv/reduction.rs:15-93).  The sum of the rounded products equals one rounding of the summed
+tensors plus the per-product corrections, an integer identity while |sum| < P / 2 (checked at
+context creation).  Bit-exact: integer work.  Covers both BASELINE dBFV configurations (cfg4: n =
+4096, 3 limbs, per-component tensor kernel; cfg5: n = 8192, 4 limbs, the (item, prime) tensor
+kernel), batches spanning several chunks on both pipeline lanes (chunks hold whole dBFV items),
+chains, and the C restatement of the reference on single products.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle import params as P, cref
+from exacto_amd._ffi import HipContext
+from bridge import uniform_residues
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(prm, psum: bool, chunk=0):
+    old = os.environ.get("EXACTO_PSUM")
+    os.environ["EXACTO_PSUM"] = "1" if psum else "0"
+    try:
+        ctx = HipContext.from_params(prm, device=0)
+    finally:
+        if old is None:
+            del os.environ["EXACTO_PSUM"]
+        else:
+            os.environ["EXACTO_PSUM"] = old
+    if chunk:
+        ctx.set_chunk(chunk)
+    return ctx
+
+
+@pytest.mark.parametrize("B,chunk", [(1, 0), (5, 4), (4, 0)])
+def test_psum_cfg4_matches_per_product(gpu_available, B, chunk):
+    """cfg4 (d = 2, 3 products per item): chunk 4 rounds down to 3 products = one item per chunk."""
+    dp = P.cfg4_params(4096)
+    prm = dp.bfv_params
+    q, n, d = prm.ct_basis.moduli, 4096, 2
+    rng = np.random.default_rng(4040 + B)
+    a = uniform_residues(rng, (B, d, 2), q, n)
+    b = uniform_residues(rng, (B, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    outs = []
+    for on in (True, False):
+        ctx = _ctx(prm, on, chunk)
+        assert (ctx.psum_max >= 2) if on else ctx.psum_max == 0
+        ctx.load_relin_key(rlk)
+        outs.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+    assert np.array_equal(outs[0], outs[1])
+    if cref.available():
+        i = B - 1
+        p01 = cref.bfv_mul_and_relin(prm, a[i:i + 1, 0], b[i:i + 1, 1], rlk, threads=4)[0]
+        p10 = cref.bfv_mul_and_relin(prm, a[i:i + 1, 1], b[i:i + 1, 0], rlk, threads=4)[0]
+        Q = np.array(q, dtype=object)[None, :, None]
+        assert np.array_equal(outs[0][i, 1].astype(object), (p01.astype(object) + p10.astype(object)) % Q)
+
+
+def test_psum_cfg5_chunks_and_chain(gpu_available):
+    """cfg5 (d = 8, 36 products per item, up to 8 per limb): two items in two chunks of 36."""
+    dp = P.cfg5_params(8192)
+    prm = dp.bfv_params
+    q, n, d = prm.ct_basis.moduli, 8192, dp.num_digits
+    rng = np.random.default_rng(5050)
+    a = uniform_residues(rng, (2, d, 2), q, n)
+    b = uniform_residues(rng, (2, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    res = []
+    for on in (True, False):
+        ctx = _ctx(prm, on, 40)
+        assert (ctx.psum_max >= 8) if on else ctx.psum_max == 0
+        ctx.load_relin_key(rlk)
+        out = ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0]
+        chain = ctx.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2)
+        res.append((out, chain))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][1], res[1][1])
