@@ -1186,10 +1186,16 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         }
         // 4+5. tensor product in every prime, fused into the inverse NTT of its components
         if (int e = run_inv_tensor(c, o, cnt, ps.on)) return e;
-        if (ps.on) {   // the output limbs' c0 / c1 auxiliary residues, summed over their products
-            launch_inv_tensor_sum(o, c->ws_T, cnt / ps.npairs, ps.d, ps.npairs, ps.term_start, ps.terms, c->logn, L,
-                                  K, c->d_primes, c->stream);
+        if (ps.on) {
+            // the output limbs' c0 / c1 auxiliary residues, summed over their products, then inverse-
+            // transformed: [ib][k][c][a][n] in extP (unused: the extensions are shared, steps 1-3 skipped)
+            const int ib_cnt = cnt / ps.npairs;
+            launch_dbfv_pairsum(o, c->ws_extP, ib_cnt, ps.d, ps.npairs, ps.term_start, ps.terms, L, K, n, c->d_primes,
+                                c->stream);
             CHECK_LAUNCH();
+            if (int e = run_ntt(c, contiguous(c->ws_extP, (long)ib_cnt * ps.d, 2L * K, L, K, n),
+                                (long)ib_cnt * ps.d * 2 * K, true))
+                return e;
         }
         // 6. scale-and-round (+ gadget digits of the third component)
         u64* R = out + s * out_stride;
@@ -1205,7 +1211,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         CHECK_LAUNCH();
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
             const long item0 = s / ps.npairs;
-            if (!launch_psum_scale(c->ws_T, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
+            if (!launch_psum_scale(c->ws_T, c->ws_extP, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
                                    ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream))
                 return fail(EXACTO_ERR_HIP, "internal: psum scale not available for these limbs");
             CHECK_LAUNCH();

@@ -203,14 +203,13 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const CombineTerm* terms, u64* out, int items, int d, int n, int L,
                          const PrimeConst* primes, hipStream_t s);
 // dBFV psum (special primes, K = L + 1, n = 4096 / 8192): the auxiliary-prime residues of each output
-// limb's c0 / c1 tensors summed over its products, inverse-transformed into the auxiliary rows of
-// product ib npairs + k of T (ntt.hip); then exact_psum_sp_kernel: the scale of those sums plus the
-// per-product corrections from the ciphertext-prime residues, the centred lift to Q, written to
+// limb's c0 / c1 tensors summed over its products (NTT domain) into out [items_b][d][2][K][n]
+// (ntt.hip), then inverse-transformed; exact_psum_sp_kernel: the scale of those sums plus the
+// per-product corrections from the ciphertext-prime residues of T, the centred lift to Q, written to
 // out [items_b][d][2][L][n] (coefficient domain, kernels.hip)
-void launch_inv_tensor_sum(const Operands& op, u64* T, int items_b, int d, int npairs, const int* term_start,
-                           const CombineTerm* terms, int logn, int L, int K, const PrimeConst* primes,
-                           hipStream_t s);
-bool launch_psum_scale(const u64* T, u64* out, int items_b, int d, int npairs, const int* term_start,
+void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int npairs, const int* term_start,
+                         const CombineTerm* terms, int L, int K, int n, const PrimeConst* primes, hipStream_t s);
+bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                        hipStream_t s);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with

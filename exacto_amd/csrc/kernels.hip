@@ -609,14 +609,14 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
 // components, computed as one scale.  Per product, r = (p T - s) / Q with s = [p T]_Q centred;
 // in an auxiliary prime p_a that is r = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs (the v_k and
 // negs from the product's ciphertext-prime residues).  The first term is linear in T, so its sum
-// over the products is the summed auxiliary residue (ntt_inv_tensor_sum_kernel); the others are
+// over the products is the summed auxiliary residue (dbfv_pairsum_kernel + inverse NTT); the others are
 // added product by product.  R = sum r is then lifted from P exactly as exact_scale_sp_kernel
 // lifts one r: the context checks m (p n Q + 2) < P (|R| < P / 2, psum_max).  Bit-identical to
 // summing the per-product results mod q_i (dbfv_combine_kernel), which is what it replaces.
-// row = (ib d + k) 2 + c; T as the tensor kernels leave it (summed rows at product ib npairs + k).
+// row = (ib d + k) 2 + c; T as the tensor kernels leave it, Tsum [ib][k][c][a][n] (launch_dbfv_pairsum).
 template <int LT>
 __global__ void __launch_bounds__(TPB)
-exact_psum_sp_kernel(const u64* __restrict__ T, u64* __restrict__ out, int d, int npairs,
+exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u64* __restrict__ out, int d, int npairs,
                      const int* __restrict__ term_start, const CombineTerm* __restrict__ terms, int n,
                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
@@ -627,10 +627,10 @@ exact_psum_sp_kernel(const u64* __restrict__ T, u64* __restrict__ out, int d, in
     const long ib = r2 / d;
     u64 carry[K];
     {
-        const u64* Ts = T + ((ib * npairs + k) * 3 + c) * (long)NP * n + j;
+        const u64* Ts = Tsum + row * K * (long)n + j;  // [ib][k][c][a][n]
 #pragma unroll
         for (int a = 0; a < K; ++a) {
-            const u64 ta = Ts[(long)(L + a) * n];   // canonical
+            const u64 ta = Ts[(long)a * n];   // canonical (inverse transform output)
             Dot30 A{0, 0, 0};
             dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->pq_w[a]);
             carry[a] = dot30_fold(A, primes[L + a].q);
@@ -685,12 +685,12 @@ exact_psum_sp_kernel(const u64* __restrict__ T, u64* __restrict__ out, int d, in
     }
 }
 
-bool launch_psum_scale(const u64* T, u64* out, int items_b, int d, int npairs, const int* term_start,
+bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                        hipStream_t s) {
     const long blocks = (long)items_b * d * 2 * blocks_per_row(n);
     if (blocks == 0) return true;
-#define PSUM_(LT) hipLaunchKernelGGL((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, out, d, npairs, \
+#define PSUM_(LT) hipLaunchKernelGGL((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d, npairs, \
                                      term_start, terms, n, ct, primes)
     switch (L) {
         case 1: PSUM_(1); break;

@@ -827,7 +827,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     // the three components of one (item, prime) read overlapping inputs (c1 reads c0's and c2's):
     // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
     const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
-    // p2only (dBFV sums of P residues, launch_inv_tensor_sum): 3L + K blocks per item, every
+    // p2only (dBFV psum: the P residues of c0 / c1 summed by launch_dbfv_pairsum): 3L + K blocks per item, every
     // component of the ciphertext primes, the third only of the auxiliary primes
     const int per = p2only ? 3 * L + K : 3 * NP;
     const long item = p / per;
@@ -1252,83 +1252,52 @@ ntt_inv_tensor_c2_kernel(Operands op, u64* __restrict__ Tout, int L, int K, cons
     for (int e = 0; e < 16; ++e) dst[elem_index<LAST_LO>(tid, e)] = x[e];
 }
 
-// dBFV, psum (dbfv_mul_core): the auxiliary-prime residues of an output limb's c0 and c1 tensors
-// summed over its products in the NTT domain, then one inverse transform per (limb, component,
-// prime) instead of one per product.  Every step of the scale up to the Garner over P is linear
-// in T (r = T (p Q^-1) + sum_k v_k (...) + negs mod p_a), so exact_psum_sp_kernel adds the
-// per-product corrections to these sums.  Block = ((ib d + k) 2 + c) K + a; the result goes to
-// the (unused) auxiliary rows of product ib npairs + k of T: [prod][c][L + a][n].
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
-ntt_inv_tensor_sum_kernel(Operands op, u64* __restrict__ Tout, int L, int K, int d, int npairs,
-                          const int* __restrict__ term_start, const CombineTerm* __restrict__ terms,
-                          const PrimeConst* __restrict__ primes) {
-    constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const int NP = L + K;
-    const long b = blockIdx.x;
-    const int a = (int)(b % K);
-    const long r1 = b / K;
-    const int c = (int)(r1 & 1);
-    const long r2 = r1 >> 1;
-    const int k = (int)(r2 % d);
-    const long ib = r2 / d;
-    const PrimeConst& P = primes[L + a];
-    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
-    const u64 q2 = P.two_q;
-    auto load = [&](const u64* src, u64 (&v)[16]) {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const ulonglong2 w = s2[e];
-            v[2 * e] = w.x;
-            v[2 * e + 1] = w.y;
-        }
-    };
-    // products < 2q (mulmod_near60); the sum is kept below 2q (the inverse rounds take < 4q)
-    auto mac = [&](u64 (&acc)[16], const u64* A, const u64* B) {
-        u64 x[16], y[16];
-        load(A, x);
-        load(B, y);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const u64 v = acc[e] + mulmod_near60(x[e], y[e], dq);
-            acc[e] = v >= q2 ? v - q2 : v;
-        }
-    };
-    u64 acc[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0;
+// dBFV, psum (dbfv_mul_core): the auxiliary-prime residues of each output limb's c0 and c1 tensors
+// summed over its products in the NTT domain (c0 = sum a0_i b0_j, c1 = sum a0_i b1_j + a1_i b0_j
+// over the limb's pairs), one coefficient per thread, out [ib][k][c][a][n] canonical; one batched
+// inverse transform per (limb, component, prime) follows instead of one per product.  Every step
+// of the scale up to the Garner over P is linear in T (r = T (p Q^-1) + sum_k v_k (...) + negs mod
+// p_a), so exact_psum_sp_kernel adds the per-product corrections to these sums.  Block = (ib, a, k)
+// x 256 coefficients (consecutive k of one (item, prime) back to back: they re-read the same
+// operands, from L2).
+__global__ void __launch_bounds__(256)
+dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L, int K, int n,
+                    const int* __restrict__ term_start, const CombineTerm* __restrict__ terms,
+                    const PrimeConst* __restrict__ primes) {
+    const int nb = n >> 8;
+    const long row = blockIdx.x / nb;                  // (ib * K + a) * d + k
+    const int j = (int)(blockIdx.x - row * nb) * 256 + (int)threadIdx.x;
+    const int k = (int)(row % d);
+    const long r1 = row / d;
+    const int a = (int)(r1 % K);
+    const long ib = r1 / K;
+    const u64 q = primes[L + a].q, q2 = 2 * q;
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+    const long off_a = (long)a * n + j, off_k = (long)K * n;
+    u64 s0 = 0, s1 = 0;                                // < 2q between terms (products < 2q)
     for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
         const long pr = ib * npairs + terms[t].pair;
-        const u64* EA = op.ea + (long)op.ea_off[pr] + (long)a * N;
-        const u64* EB = op.eb + (long)op.eb_off[pr] + (long)a * N;
-        if (c == 0) {
-            mac(acc, EA, EB);                              // a0 b0
-        } else {
-            mac(acc, EA, EB + (long)K * N);                // a0 b1
-            mac(acc, EA + (long)K * N, EB);                // a1 b0
-        }
+        const u64* EA = op.ea + (long)op.ea_off[pr] + off_a;
+        const u64* EB = op.eb + (long)op.eb_off[pr] + off_a;
+        const u64 a0 = EA[0], a1 = EA[off_k], b0 = EB[0], b1 = EB[off_k];
+        u64 v = s0 + mulmod_near60(a0, b0, dq);
+        s0 = v >= q2 ? v - q2 : v;
+        v = s1 + mulmod_near60(a0, b1, dq);
+        s1 = v >= q2 ? v - q2 : v;
+        v = s1 + mulmod_near60(a1, b0, dq);
+        s1 = v >= q2 ? v - q2 : v;
     }
-    inv_rounds_asm<LOGN, 0>(acc, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
-    u64* dst = Tout + (((ib * npairs + k) * 3 + c) * NP + L + a) * N;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dst[elem_index<LAST_LO>(tid, e)] = acc[e];
+    u64* o = out + (((ib * d + k) * 2) * K + a) * (long)n + j;
+    o[0] = s0 >= q ? s0 - q : s0;
+    o[(long)K * n] = s1 >= q ? s1 - q : s1;
 }
 
-void launch_inv_tensor_sum(const Operands& op, u64* T, int items_b, int d, int npairs, const int* term_start,
-                           const CombineTerm* terms, int logn, int L, int K, const PrimeConst* primes,
-                           hipStream_t s) {
-    const long blocks = (long)items_b * d * 2 * K;
-    if (blocks == 0) return;
-    if (logn == 12)
-        hipLaunchKernelGGL((ntt_inv_tensor_sum_kernel<12>), dim3(blocks), dim3(256), 0, s, op, T, L, K, d, npairs,
-                           term_start, terms, primes);
-    else if (logn == 13)
-        hipLaunchKernelGGL((ntt_inv_tensor_sum_kernel<13>), dim3(blocks), dim3(512), 0, s, op, T, L, K, d, npairs,
-                           term_start, terms, primes);
+void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int npairs, const int* term_start,
+                         const CombineTerm* terms, int L, int K, int n, const PrimeConst* primes, hipStream_t s) {
+    const long blocks = (long)items_b * K * d * (n >> 8);
+    if (blocks == 0 || n < 256) return;
+    hipLaunchKernelGGL(dbfv_pairsum_kernel, dim3(blocks), dim3(256), 0, s, op, out, d, npairs, L, K, n, term_start,
+                       terms, primes);
 }
 
 template <int LOGN>
