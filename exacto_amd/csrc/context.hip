@@ -223,6 +223,8 @@ struct exacto_ctx {
     bool ks32_long_runs = false; // every 31-bit prime below 2^32 / 3: 12 MAC products per reduction
     Ks32Basis kw;                // wide basis (primes up to 2^31) for dBFV digit sums the primary cannot hold
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
+    bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
+    bool digit8_env = true;
     // dBFV psum (EXACTO_PSUM=0: off): an output limb's c0 / c1 scaled once from the sum of its
     // products' tensors in the auxiliary primes (run_mul, dbfv_mul_core); psum_max = the largest
     // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
@@ -789,6 +791,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     if (int rc = setup_ks32(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
@@ -1136,8 +1139,16 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
     const exacto_ctx::PsumPlan& ps = c->psum;
     // psum: chunks hold whole dBFV items (their products are summed inside the chunk)
-    const size_t C = ps.on ? std::max<size_t>(ps.npairs, std::min<size_t>(c->chunk, (size_t)P) / ps.npairs * ps.npairs)
-                           : std::min<size_t>(c->chunk, (size_t)P);
+    size_t C = ps.on ? std::max<size_t>(ps.npairs, std::min<size_t>(c->chunk, (size_t)P) / ps.npairs * ps.npairs)
+                     : std::min<size_t>(c->chunk, (size_t)P);
+    // a batch that fits one chunk still takes two lanes when each half has work enough (>= 64
+    // products): the halves fill each other's launch tails (cfg5, 288 products per dbfv_mul: 1837 ->
+    // 1889 chains/s with two chunks of 144; four chunks of 72 measured 1800)
+    if (c->dual && !c->prof && c->lanes > 1 && (size_t)P <= C && P >= 128) {
+        size_t half = ((size_t)P + 1) / 2;
+        if (ps.on) half = (half + ps.npairs - 1) / ps.npairs * ps.npairs;
+        if (half < (size_t)P) C = half;
+    }
     if (int e = ensure_workspace(c, C)) return e;
     // int16 gadget digits (base <= 2^16, exact path): the scale kernel writes each digit once
     const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
@@ -1205,9 +1216,13 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D,
-                               d16 ? (c->ks_defer ? c->ks_defer + s * (long)guse * n : c->ws_D16) : nullptr, guse,
-                               cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
-                               c->stream, c->h_crt.gshift, ps.on);
+                               d16 ? (c->ks_defer ? (c->ks_defer8
+                                                         ? (int16_t*)((int8_t*)c->ks_defer + s * (long)guse * n)
+                                                         : c->ks_defer + s * (long)guse * n)
+                                                  : c->ws_D16)
+                                   : nullptr,
+                               guse, cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
+                               c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8);
         CHECK_LAUNCH();
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
             const long item0 = s / ps.npairs;
@@ -1710,6 +1725,10 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
             return EXACTO_ERR_HIP;
         if (int e = use_wide ? ensure_rs_wide(c) : ensure_rs(c)) return e;
         c->ks_defer = c->d_dall;
+        // base <= 2^8: every balanced digit fits int8 (half the digit bytes written and summed)
+        const int sh = c->h_crt.gshift;
+        c->ks_defer8 = c->digit8_env && sh > 0 && sh <= 8 && 32 % sh == 0 &&
+                       exact_scale_sp_ok(c->L, c->K, crt_mode(c));
     }
     // psum: each output limb's c0 / c1 from one scale of its products' summed tensors (the
     // auxiliary-prime residues summed in the NTT domain and inverse-transformed once per limb, the
@@ -1732,6 +1751,8 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     bool coef = false;
     const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
     c->ks_defer = nullptr;
+    const bool in8 = c->ks_defer8;
+    c->ks_defer8 = false;
     c->psum.on = false;
     if (rc) return rc;
     if (sum_ks && !coef) return fail(EXACTO_ERR_HIP, "internal: ks32 sums without the ks32 key switch");
@@ -1741,7 +1762,7 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
         CHECK_LAUNCH();
     }
     if (sum_ks) {
-        ks32_digit_sum(c->d_dall, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)d, (int)gu, c->n,
+        ks32_digit_sum(c->d_dall, in8, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)d, (int)gu, c->n,
                        c->stream);
         if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
         else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
