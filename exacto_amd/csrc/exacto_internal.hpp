@@ -176,7 +176,8 @@ bool exact_scale_sp_ok(int L, int K, int mode);
 // c2only: the third component's rows alone (its gadget digits; dBFV psum, mode 3 with K = L + 1 only)
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false);
+                        int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false,
+                        bool digits8 = false);
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
                       int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
                       hipStream_t s);
@@ -214,7 +215,8 @@ bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int
                        hipStream_t s);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
 // coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n], int16 or (wide) int32
-void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, void* out,
+// D: int16 digits, or int8 when in8 (base <= 2^8, exact_scale's digits8)
+void ks32_digit_sum(const void* D, bool in8, int npairs, const int* term_start, const CombineTerm* terms, void* out,
                     bool wide, int items, int d, int gu, int n, hipStream_t st);
 
 }  // namespace exacto

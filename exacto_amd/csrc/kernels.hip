@@ -240,10 +240,10 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
 // the same rule, exactly as the multiword increment does.  The fields are read from the 32-bit
 // words of the magnitude in place: no multiword shift or add per digit.  Digit g goes to
 // D16[g * n].
-template <int LT>
+template <int LT, typename DT = int16_t>
 __device__ __forceinline__ void gadget_digits16_sp(const u64 (&res)[EXACTO_MAX_L], const CrtTables* __restrict__ C,
                                                    const PrimeConst* __restrict__ primes, int n, int guse,
-                                                   int16_t* D16) {
+                                                   DT* D16) {
     constexpr int L = LT;
     u64 z[EXACTO_MAX_L];
     garner_q_fast<LT>(z, res, L, C, primes);
@@ -290,14 +290,14 @@ __device__ __forceinline__ void gadget_digits16_sp(const u64 (&res)[EXACTO_MAX_L
             const uint32_t r = ((word >> o) & mask) + c;
             c = r > thr ? 1u : 0u;
             const int dv = (int)r - (int)(c << sh);
-            D16[(long)g * n] = (int16_t)((dv ^ sgn) - sgn);
+            D16[(long)g * n] = (DT)((dv ^ sgn) - sgn);
         }
     }
     for (; g < guse; ++g) {   // past the magnitude's words: only the carry remains
         const uint32_t r = c;
         c = r > thr ? 1u : 0u;
         const int dv = (int)r - (int)(c << sh);
-        D16[(long)g * n] = (int16_t)((dv ^ sgn) - sgn);
+        D16[(long)g * n] = (DT)((dv ^ sgn) - sgn);
     }
 }
 
@@ -597,6 +597,9 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
     if (comp != 2) return;
     if constexpr (DIG == 1) {
         gadget_digits16_sp<LT>(res, C, primes, n, guse, D16 + item * (long)guse * n + j);
+    } else if constexpr (DIG == 3) {   // int8: base <= 2^8, every balanced digit in [-128, 127]
+        gadget_digits16_sp<LT, int8_t>(res, C, primes, n, guse,
+                                       reinterpret_cast<int8_t*>(D16) + item * (long)guse * n + j);
     } else if constexpr (DIG == 2) {
         if (D16 != nullptr)
             gadget_digits<true, LT>(res, L, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
@@ -709,19 +712,20 @@ bool exact_scale_sp_ok(int L, int K, int mode) { return mode == 3 && K == L + 1 
 
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift, bool c2only) {
+                        int K, int mode, hipStream_t s, int gshift, bool c2only, bool digits8) {
     const long blocks = (long)items * (c2only ? 1 : 3) * blocks_per_row(n);
     if (blocks == 0) return;
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
         // digit code: 0 none, 1 int16 fields of the magnitude (base 2^sh, sh | 32), 2 gadget_digits
         const int dig = (D16 == nullptr && D == nullptr) || guse <= 0 ? 0
-                        : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? 1 : 2;
+                        : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? (digits8 && gshift <= 8 ? 3 : 1) : 2;
 #define SCALE30_(LT, DG)                                                                                        \
     hipLaunchKernelGGL((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
                        D16, guse, n, ct, primes, c2only ? 1 : 0)
 #define SCALE30(LT)                         \
     do {                                    \
         if (dig == 1) SCALE30_(LT, 1);      \
+        else if (dig == 3) SCALE30_(LT, 3); \
         else if (dig == 2) SCALE30_(LT, 2); \
         else SCALE30_(LT, 0);               \
     } while (0)

@@ -383,9 +383,9 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
 // Every step after the digits (NTT mod p_s, MAC with the key, lift) is linear in them, so the sum
 // of the products' key switches is the key switch of the summed digits (an integer identity; the
 // basis bound covers the sum, see setup_ks32).  D [item][pair][g][n] -> out [item][k][g][n].
-template <typename OT>
+template <typename OT, typename IT>
 __global__ void __launch_bounds__(256)
-ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __restrict__ term_start,
+ks32_digit_sum_kernel(const IT* __restrict__ D, int npairs, const int* __restrict__ term_start,
                       const CombineTerm* __restrict__ terms, OT* __restrict__ out, int d, int gu, int n,
                       int nsh) {
     // eight consecutive digits per thread (one 16-byte load per term), 2048 per block
@@ -397,12 +397,20 @@ ks32_digit_sum_kernel(const int16_t* __restrict__ D, int npairs, const int* __re
     const long item = ik / (uint32_t)d;
     int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
-        const uint4 w = *reinterpret_cast<const uint4*>(D + ((item * npairs + terms[t].pair) * gu + g) * (long)n + j);
-        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+        const IT* src = D + ((item * npairs + terms[t].pair) * gu + g) * (long)n + j;
+        if constexpr (sizeof(IT) == 2) {   // one 16-byte load
+            const uint4 w = *reinterpret_cast<const uint4*>(src);
+            const uint32_t v[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            acc[2 * h] += (int)(int16_t)(v[h] & 0xFFFF);
-            acc[2 * h + 1] += (int)(int16_t)(v[h] >> 16);
+            for (int h = 0; h < 4; ++h) {
+                acc[2 * h] += (int)(int16_t)(v[h] & 0xFFFF);
+                acc[2 * h + 1] += (int)(int16_t)(v[h] >> 16);
+            }
+        } else {                           // int8: one 8-byte load
+            const uint2 w = *reinterpret_cast<const uint2*>(src);
+            const uint32_t v[2] = {w.x, w.y};
+#pragma unroll
+            for (int h = 0; h < 8; ++h) acc[h] += (int)(int8_t)(v[h >> 2] >> (8 * (h & 3)));
         }
     }
     if constexpr (sizeof(OT) == 2) {
@@ -517,18 +525,21 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
 #undef MAC_
 }
 
-void ks32_digit_sum(const int16_t* D, int npairs, const int* term_start, const CombineTerm* terms, void* out,
+void ks32_digit_sum(const void* D, bool in8, int npairs, const int* term_start, const CombineTerm* terms, void* out,
                     bool wide, int items, int d, int gu, int n, hipStream_t st) {
     const long rows = (long)items * d * gu;
     if (rows <= 0) return;
     const int nb = n >= 2048 ? n / 2048 : 1;   // n >= 1024, a power of two; 2048 digits per block
     const dim3 grid((unsigned)(rows * nb)), block(n >= 2048 ? 256 : n / 8);
-    if (wide)
-        hipLaunchKernelGGL(ks32_digit_sum_kernel<int32_t>, grid, block, 0, st, D, npairs, term_start, terms,
-                           (int32_t*)out, d, gu, n, __builtin_ctz((unsigned)nb));
-    else
-        hipLaunchKernelGGL(ks32_digit_sum_kernel<int16_t>, grid, block, 0, st, D, npairs, term_start, terms,
-                           (int16_t*)out, d, gu, n, __builtin_ctz((unsigned)nb));
+    const int nsh = __builtin_ctz((unsigned)nb);
+#define DSUM_(OT, IT) hipLaunchKernelGGL((ks32_digit_sum_kernel<OT, IT>), grid, block, 0, st, (const IT*)D, npairs, \
+                                         term_start, terms, (OT*)out, d, gu, n, nsh)
+    if (wide) {
+        if (in8) DSUM_(int32_t, int8_t); else DSUM_(int32_t, int16_t);
+    } else {
+        if (in8) DSUM_(int16_t, int8_t); else DSUM_(int16_t, int16_t);
+    }
+#undef DSUM_
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,

@@ -24,16 +24,16 @@ from bridge import uniform_residues
 pytestmark = pytest.mark.gpu
 
 
-def _ctx(prm, psum: bool, chunk=0):
-    old = os.environ.get("EXACTO_PSUM")
-    os.environ["EXACTO_PSUM"] = "1" if psum else "0"
+def _ctx(prm, psum: bool, chunk=0, var="EXACTO_PSUM"):
+    old = os.environ.get(var)
+    os.environ[var] = "1" if psum else "0"
     try:
         ctx = HipContext.from_params(prm, device=0)
     finally:
         if old is None:
-            del os.environ["EXACTO_PSUM"]
+            del os.environ[var]
         else:
-            os.environ["EXACTO_PSUM"] = old
+            os.environ[var] = old
     if chunk:
         ctx.set_chunk(chunk)
     return ctx
@@ -83,3 +83,21 @@ def test_psum_cfg5_chunks_and_chain(gpu_available):
         res.append((out, chain))
     assert np.array_equal(res[0][0], res[1][0])
     assert np.array_equal(res[0][1], res[1][1])
+
+
+def test_int8_digits_cfg5(gpu_available):
+    """cfg5's gadget base 256: the products' digits summed per limb are written and read as int8
+    (every balanced digit lies in [-128, 127]); identical to the int16 form (EXACTO_DIGIT8=0)."""
+    dp = P.cfg5_params(8192)
+    prm = dp.bfv_params
+    q, n, d = prm.ct_basis.moduli, 8192, dp.num_digits
+    rng = np.random.default_rng(5151)
+    a = uniform_residues(rng, (1, d, 2), q, n)
+    b = uniform_residues(rng, (1, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    res = []
+    for on in (True, False):
+        ctx = _ctx(prm, on, var="EXACTO_DIGIT8")
+        ctx.load_relin_key(rlk)
+        res.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+    assert np.array_equal(res[0], res[1])
