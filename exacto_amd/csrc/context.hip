@@ -225,6 +225,11 @@ struct exacto_ctx {
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
+    // EXACTO_CRT_FWD=2/3: the key switch's lift and the forward NTT of bfv_mul_and_relin's outputs in
+    // one kernel (ks32_crt_fwd_kernel, 2 / 3 waves per SIMD).  Off by default: cfg3 398.3k -> 391.3k/s
+    // (3 waves, a few spills) and 386.5k/s (2 waves): the lift's 126-VGPR phase and the transform do
+    // not share a register budget well, and the separate forward is the persistent LDS-DMA kernel
+    int crt_fwd = 0;
     // dBFV psum (EXACTO_PSUM=0: off): an output limb's c0 / c1 scaled once from the sum of its
     // products' tensors in the auxiliary primes (run_mul, dbfv_mul_core); psum_max = the largest
     // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
@@ -792,6 +797,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_CRT_FWD")) c->crt_fwd = atoi(e);
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     if (int rc = setup_ks32(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
@@ -1254,9 +1260,19 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             if (!c->ks_defer) {   // (deferred: the caller sums the digits of products first, dbfv_mul_core)
                 ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
                 ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
-                ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
-                         c->stream);
+                // lift + the forward NTT of R in one kernel when the asm forward rounds serve R's primes
+                bool fused = false;
+                if (!skip_fwd && c->crt_fwd > 0 && c->ntt_asm && ncomp == 2) {
+                    bool near = true;
+                    for (int l = 0; l < L; ++l) near &= c->primes[l] < (1ull << 60) && c->primes[l] > (1ull << 60) - (1ull << 24);
+                    fused = near && launch_ks32_crt_fwd(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32,
+                                                        c->d_primes, c->stream, c->crt_fwd);
+                }
+                if (!fused)
+                    ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
+                             c->stream);
                 CHECK_LAUNCH();
+                if (fused) continue;   // R is relinearised and in the NTT domain
             }
         }
         if (skip_fwd) continue;

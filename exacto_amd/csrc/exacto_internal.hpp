@@ -125,6 +125,11 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
               const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);
+// ks32_crt followed by the forward NTT of R's rows (row (item, c, l) mod q_l), fused (ntt.hip; n =
+// 4096 / 8192, S = 2 / 3, every q_l 2^60 - d with d < 2^24; false = not launched)
+bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn,
+                         const Ks32Tables* KT, const Prime32* primes, const PrimeConst* qprimes, hipStream_t s,
+                         int waves);
 
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item

@@ -12,6 +12,7 @@
 // oracle/ring.py NttPlan): Cooley-Tukey forward, natural in / bit-reversed out;
 // Gentleman-Sande inverse, bit-reversed in / natural out.
 #include "exacto_internal.hpp"
+#include "ks32_dev.hpp"
 
 namespace exacto {
 
@@ -1014,6 +1015,57 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     u64* dst = out + p * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = xa[k];
+}
+
+// The key switch's lift (ks32_crt_values: S inverse 32-bit transforms, centred Garner lift, + the
+// scaled component) and the forward 60-bit transform of the result in one workgroup per (item, c,
+// l): the coefficient-domain relinearised component never goes to HBM and back (bfv_mul_and_relin's
+// steps 8 and 9).  The lift leaves element k T + tid in x[k], the forward rounds' input layout.
+// W: waves per SIMD the register budget targets (3: 168 VGPRs, a few spilled; 2: no spills)
+template <int LOGN, int S, int W>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(W)))
+ks32_crt_fwd_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
+                    const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
+                    const PrimeConst* __restrict__ qprimes) {
+    constexpr int N = 1 << LOGN, T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;             // (item, cl)
+    u64 x[16];
+    ks32_crt_values<LOGN, S>(x, U, R, r_stride, L, b, reinterpret_cast<uint32_t*>(lds), tid, KT, primes, qprimes);
+    const uint32_t CL = 2 * L;
+    const long item = b / CL;
+    const int cl = (int)(b - (uint32_t)item * CL);
+    const PrimeConst& P = qprimes[cl % L];
+    lds_barrier();   // the lift's last LDS reads are done before the forward rounds reuse lds
+    fwd_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
+    int t2 = tid;
+    asm volatile("" : "+v"(t2));
+    lds_barrier();
+    lds_store_x<0>(lds, x, t2);
+    lds_barrier();
+    lds_load_x<LOGN - 4>(lds, x, t2);
+    u64* dst = R + item * r_stride + (long)cl * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+}
+
+bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn,
+                         const Ks32Tables* KT, const Prime32* primes, const PrimeConst* qprimes, hipStream_t s,
+                         int waves) {
+    const dim3 grid((unsigned)((long)items * 2 * L));
+#define CF_(LG, S_, W_) hipLaunchKernelGGL((ks32_crt_fwd_kernel<LG, S_, W_>), grid, dim3((1 << LG) / 16), 0, s, U, R, \
+                                           r_stride, L, KT, primes, qprimes)
+#define CFW_(LG, S_) do { if (waves == 2) CF_(LG, S_, 2); else CF_(LG, S_, 3); } while (0)
+    if (items <= 0) return true;
+    if (logn == 12 && S == 3) CFW_(12, 3);
+    else if (logn == 13 && S == 3) CFW_(13, 3);
+    else if (logn == 12 && S == 2) CFW_(12, 2);
+    else if (logn == 13 && S == 2) CFW_(13, 2);
+    else return false;
+#undef CFW_
+#undef CF_
+    return true;
 }
 
 bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,
