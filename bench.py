@@ -3,39 +3,54 @@
 
 Workload (default, BASELINE configs[2]): bfv_mul_and_relin at n=4096, 3x60-bit RNS limbs,
 p=65537, gadget base 2^16 (G=12), a batch of 1024 independent ciphertext pairs per GPU
-(weak scaling).  A "step" is one pass of the whole batch through the path, with inputs
-already resident in HBM.  Synthetic data: uniform canonical residues per limb (the path
-is deterministic given (ct1, ct2, rlk), so encrypted vs uniform inputs cost the same).
+(weak scaling).  Synthetic data: uniform canonical residues per limb (the path is deterministic
+given (ct1, ct2, rlk), so encrypted vs uniform inputs cost the same), resident in HBM before the
+timed region starts.
 
-Multi-GPU: one process per GPU (torchrun).  The relinearisation key is generated on rank 0
-and broadcast over RCCL (xGMI); every rank then processes its own batch shard with no
-data-path collective.  value = total products over all ranks / max-over-ranks step time.
+A step is `reps` passes of the hot path, each over one whole batch (the input batches rotate over
+two resident copies).  `reps` is chosen after the warm-up so that the K timed steps last at least
+--min-time seconds (default 2 s): the BASELINE batch (1024 products, ~2.5 ms) is far shorter than
+anything a wall-clock or GPU-busy sampler can see.  value = units processed / timed seconds.
+
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the
+environment) starts `torch.distributed.run --nproc-per-node N` on itself as a CHILD process, before
+touching any GPU, and exits with its status; under torchrun WORLD_SIZE must equal --gpus.
+  --split batch (default): every rank processes its own batch shard, no data-path collective; the
+      relinearisation key is made on rank 0 and broadcast by the library's RCCL (ncclBroadcast into
+      each rank's resident key).  value = total units over all ranks / max-over-ranks time (weak).
+  --split limbs (dBFV configs): ONE dbfv_mul batch (the same B items on every rank) with its d output
+      limbs split across the ranks by product count (dbfv/eval.rs:109-132: limb k sums the pairs
+      i + j = k, so whole limbs need no cross-GPU sum); each rank computes its limbs, then an
+      all-gather assembles every limb on every rank (the next chain step needs them all).  value =
+      B units / max-over-ranks time (strong scaling: the total work is fixed).
+  --dry: no HIP calls at all (gloo on CPU, a stand-in step on CPU tensors of the same shapes): checks
+      the launcher, the sharding / limb partition + gather and the timing path on a machine without
+      a GPU.  Its numbers measure nothing.
 
 Also reported on the same JSON line:
-  roofline     — the dominant kernel (forward NTT of the pipeline), algorithmic bytes
-                 16*n per residue polynomial over its summed launch time,
-                 measured with HIP events around each of its launches on the pipeline's
-                 stream, vs the 8 TB/s HBM peak;
-  cpu_baseline — the CPU restatement of the reference algorithm (oracle/, exact BigInt
-                 schoolbook tensor, eval.rs:113-147) on a bounded sample, rank 0 at N=1.
+  roofline     — the kernel family with the largest share of one profiled batch (HIP events around
+                 each of its launches, on the stream it runs on), its ALGORITHMIC bytes per launch
+                 (each operand read once, each result written once) over its average
+                 launch time, vs the 8 TB/s HBM peak; `ntt` = the same for the forward NTT, and
+                 `kernels` the whole profiled breakdown;
+  cpu_baseline — the C restatement of the reference algorithm (oracle/c: exact BigInt schoolbook
+                 tensor, eval.rs:113-147; dbfv_mul with all d^2 products) on a bounded sample of the
+                 same workload, on the host cores, rank 0 at N=1 only.
 """
 
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from exacto_amd._ffi import HipContext  # noqa: E402
 
 Q3 = [1152921504606830593, 1152921504606748673, 1152921504606683137]
 Q4 = Q3 + [1152921504606601217]
@@ -53,8 +68,13 @@ CONFIGS = {
 }
 DEFAULT_BATCH = {"cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8, "galois": 1024}
 
+# profiled kernel families (exacto_hip.h exacto_prof_read kinds, context.hip ProfKind)
+KINDS = {0: "fwd_ntt", 1: "inv_ntt", 2: "tensor_inv", 3: "polymul", 4: "exact_lift", 5: "exact_scale",
+         6: "ks32_digit_ntt", 7: "ks32_mac", 8: "ks32_crt", 9: "dbfv_pairsum", 10: "psum_scale",
+         11: "tensor_c2_inv", 12: "ks32_digit_sum", 13: "dbfv_combine"}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -62,244 +82,391 @@ def parse():
     ap.add_argument("--batch", type=int, default=0, help="work items per GPU (0 = config default)")
     ap.add_argument("--chunk", type=int, default=0, help="products per pipeline chunk (0 = library default)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--split", default="batch", choices=("batch", "limbs"))
+    ap.add_argument("--min-time", type=float, default=2.0, help="lower bound of the timed region, seconds")
+    ap.add_argument("--reps", type=int, default=0, help="batches per step (0 = from --min-time)")
+    ap.add_argument("--dry", action="store_true", help="no HIP calls: CPU/gloo stand-in of the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0, help="products timed for the CPU baseline (0 = auto)")
-    return ap.parse_args()
+    ap.add_argument("--cpu-sample", type=int, default=0, help="units timed for the CPU baseline (0 = auto)")
+    return ap.parse_args(argv)
 
 
-def uniform_dev(shape_prefix, moduli, n, gen, device):
-    out = torch.empty(tuple(shape_prefix) + (len(moduli), n), dtype=torch.int64, device=device)
-    for i, q in enumerate(moduli):
-        out[..., i, :] = torch.randint(0, q, tuple(shape_prefix) + (n,), generator=gen,
-                                       dtype=torch.int64, device=device)
-    return out
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def cpu_baseline(n, moduli, plain, gbase, sample, threads=1):
-    """Time the CPU restatement of the reference algorithm on `sample` products, batch-parallel
-    over `threads` OpenMP threads (the reference fans dbfv_mul out over rayon the same way)."""
-    from oracle import params as P
-    from oracle import bfv as obfv
+def relaunch(args) -> int:
+    """--gpus N > 1 outside torchrun: run torchrun on this script as a child (no exec: the parent
+    has not touched the GPU and only waits), return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def kernel_names(n, L, S, cfg, env=os.environ):
+    """Kernel (template instance) behind each profiled family for this configuration, as rocprofv3
+    names it (context.hip / ntt.hip launch choices)."""
+    logn = n.bit_length() - 1
+    on = lambda k: env.get(k, "1") != "0"
+    asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
+    fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and on("EXACTO_NTT_PIPE")
+           else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>")
+    inv = f"ntt_inv_asm_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}, true>"
+    t3 = env.get("EXACTO_TENSOR3", "1" if logn == 13 else "0") == "1"
+    tensor = f"ntt_inv_tensor3_kernel<{logn}>" if t3 else f"ntt_inv_tensor_kernel<{logn}, true, true>"
+    return {0: fwd, 1: inv, 2: tensor, 3: f"ntt_polymul_kernel<{logn}>", 4: f"exact_lift_sp_kernel<{L}>",
+            5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
+            8: f"ks32_crt_kernel<{logn}, {S}>", 9: "dbfv_pairsum_kernel", 10: f"exact_psum_sp_kernel<{L}>",
+            11: f"ntt_inv_tensor_c2_kernel<{logn}>", 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel"}
+
+
+def _entry(rec, name, share=None):
+    ms, nl, by = rec["ms"], max(rec["launches"], 1), rec["bytes"]
+    achieved = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    e = {"kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "launches": rec["launches"],
+         "avg_launch_us": round(ms * 1000.0 / nl, 2), "bytes_per_launch": by / nl}
+    if share is not None:
+        e["share_of_profiled_batch"] = round(share, 4)
+    return e
+
+
+def roofline_block(ctx, step_one, cfg, n, L, S):
+    """One profiled batch (single lane: per-kernel events time each kernel alone), every family."""
+    ctx.prof_enable(True)
+    step_one()
+    import torch
+    torch.cuda.synchronize()
+    recs = {k: ctx.prof_read(k) for k in KINDS}
+    ctx.prof_enable(False)
+    names = kernel_names(n, L, S, cfg)
+    total = sum(r["ms"] for r in recs.values())
+    table = {KINDS[k]: _entry(r, names[k], r["ms"] / total if total else 0.0) for k, r in recs.items() if r["launches"]}
+    top = max(recs, key=lambda k: recs[k]["ms"])
+    roof = {"bound": "hbm"}
+    roof.update(_entry(recs[top], names[top], recs[top]["ms"] / total if total else 0.0))
+    roof["family"] = KINDS[top]
+    roof["traffic"] = None
+    # HBM bytes per launch from the committed PMC passes over this bench configuration
+    # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch with the gfx950 corrections)
+    tfile = os.path.join(ROOT, "profiles", f"r3_{cfg}_traffic.json")
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tr = json.load(f).get("kernels", {})
+        hit = [v for k, v in tr.items() if names[top].split("<")[0] in k]
+        if hit:
+            roof["traffic"] = round(hit[0]["traffic_bytes_avg"], 1)
+            roof["traffic_over_algorithmic"] = round(hit[0]["traffic_bytes_avg"] / roof["bytes_per_launch"], 4)
+            roof["traffic_source"] = os.path.relpath(tfile, ROOT)
+    # the compute-side ceiling (integer modular arithmetic: VALU issue, not MFMA) from the committed
+    # PMC pass: VALU wave-instructions and GPU cycles per dispatch, ~4.4 cycles per integer
+    # multiply-class wave-instruction per SIMD (tools/op_rate.hip), 1024 SIMDs
+    vfile = os.path.join(ROOT, "profiles", f"r3_{cfg}_valu_counters.json")
+    if os.path.exists(vfile):
+        with open(vfile) as f:
+            vc = json.load(f).get("kernels", {})
+        hit = [v for k, v in vc.items() if names[top].split("<")[0] in k]
+        if hit:
+            v = hit[0]
+            need = v["valu_insts"] * 4.4 / 1024.0
+            roof["compute"] = {"bound": "valu", "valu_insts_per_launch": round(v["valu_insts"]),
+                               "cycles_per_valu": 4.4, "gpu_cycles_per_launch": round(v["gpu_cycles"]),
+                               "frac": round(need / v["gpu_cycles"], 3), "source": os.path.relpath(vfile, ROOT)}
+    ntt = table.get("fwd_ntt")
+    return roof, ntt, table
+
+
+def cpu_baseline(cfg, n, moduli, plain, gbase, dbfv, depth, sample):
+    """The C restatement of the reference algorithm (oracle/c) on a bounded sample of the workload,
+    OpenMP over the products (the reference fans dbfv_mul's d^2 products out over rayon the same
+    way), on the host cores this job may use (16 on the GPU box, whose os.cpu_count() reports the
+    whole machine)."""
+    import numpy as np
+    from oracle import params as P, cref
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from bridge import uniform_residues, np_to_ct, np_to_rlk
-    try:
-        from oracle import cref
-        use_c = cref.available()
-    except Exception:
-        use_c = False
+    from bridge import uniform_residues
+    if not cref.available():
+        return {"value": None, "error": "oracle/c/liboracle.so not built"}
+    threads = min(16, os.cpu_count() or 1)
     prm = P.BfvParamsBuilder().ring_degree(n).plain_modulus(plain).ct_moduli(moduli).gadget_base(gbase).build()
     rng = np.random.default_rng(7)
-    ct1 = uniform_residues(rng, (sample, 2), moduli, n)
-    ct2 = uniform_residues(rng, (sample, 2), moduli, n)
     rlk = uniform_residues(rng, (prm.gadget_digits, 2), moduli, n)
-    if use_c:
+    impl = "oracle/c (C restatement, exact multiword schoolbook tensor)"
+    if dbfv is None:
+        sample = sample or 8 * threads
+        ct1 = uniform_residues(rng, (sample, 2), moduli, n)
+        ct2 = uniform_residues(rng, (sample, 2), moduli, n)
         t0 = time.perf_counter()
         cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=threads)
         dt = time.perf_counter() - t0
-        impl = "oracle/c (C restatement, exact multiword schoolbook tensor)"
-    else:
-        threads = 1
-        rk = np_to_rlk(rlk, prm)
+        return {"value": sample / dt, "unit": "bfv_mul_and_relin/s", "cores": threads, "kind": "port",
+                "sample": f"{sample} bfv_mul_and_relin of the same workload (n={n}, L={len(moduli)}), "
+                          f"{threads} threads, {impl}; {dt:.2f} s"}
+    d, base, dplain = dbfv
+    dp = P.DbfvParams(prm, base, d, dplain)
+    if depth == 1:
+        # whole dbfv_mul items (all d^2 products, sums, reduce)
+        sample = sample or max(1, (4 * threads) // (d * d))
+        a = uniform_residues(rng, (sample, d, 2), moduli, n)
+        b = uniform_residues(rng, (sample, d, 2), moduli, n)
         t0 = time.perf_counter()
-        for b in range(sample):
-            obfv.bfv_mul_and_relin(np_to_ct(ct1[b], prm), np_to_ct(ct2[b], prm), rk)
+        cref.dbfv_mul(dp, a, b, rlk, threads=threads)
         dt = time.perf_counter() - t0
-        impl = "oracle/ (Python exact-integer restatement)"
-    return {"value": sample / dt, "unit": "bfv_mul_and_relin/s", "cores": threads, "kind": "port",
-            "sample": f"{sample} bfv_mul_and_relin of the same workload (n={n}, L={len(moduli)}), "
-                      f"{threads} thread(s), {impl}; {dt:.2f} s"}
+        return {"value": sample / dt, "unit": "dbfv_mul/s", "cores": threads, "kind": "port",
+                "sample": f"{sample} dbfv_mul (d={d}, all {d * d} products each, n={n}, L={len(moduli)}), "
+                          f"{threads} threads, {impl}; {dt:.2f} s"}
+    # chains: one product per thread timed, scaled to the chain (depth dbfv_mul of d^2 products each):
+    # a whole chain item is minutes of CPU work at n = 8192
+    sample = sample or threads
+    ct1 = uniform_residues(rng, (sample, 2), moduli, n)
+    ct2 = uniform_residues(rng, (sample, 2), moduli, n)
+    t0 = time.perf_counter()
+    cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=threads)
+    dt = time.perf_counter() - t0
+    per_chain = depth * d * d
+    return {"value": sample / dt / per_chain, "unit": f"dbfv_mul_chain(depth {depth})/s", "cores": threads,
+            "kind": "port", "sample": f"{sample} bfv_mul_and_relin products of the chain's parameters (n={n}, "
+                                      f"L={len(moduli)}, base {gbase}) in {dt:.2f} s with {threads} threads, {impl}; "
+                                      f"scaled by {per_chain} products per chain (depth {depth} x d^2 = {d * d})"}
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(relaunch(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
-    if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+
+    import numpy as np  # noqa: F401
+    import torch
+    import torch.distributed as dist
+    from exacto_amd import dist as xdist
 
     n, moduli, aux, plain, gbase, dbfv, depth = CONFIGS[args.config]
     L = len(moduli)
     B = args.batch or DEFAULT_BATCH[args.config]
-    ctx = HipContext(n, moduli, aux, plain, gbase, device=local)
-    stream = torch.cuda.current_stream(device)
-    ctx.set_stream(stream.cuda_stream)
-    if args.chunk:
-        ctx.set_chunk(args.chunk)
-    G = ctx.G
+    if args.split == "limbs" and dbfv is None:
+        print("bench.py: --split limbs needs a dBFV config (cfg4, cfg5)", file=sys.stderr)
+        sys.exit(2)
+    distributed = world > 1
+    if args.dry:
+        device = torch.device("cpu")
+        if distributed:
+            dist.init_process_group("gloo")
+    else:
+        if distributed:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        device = torch.device("cuda", local)
+        torch.cuda.set_device(device)
+    backend = dist.get_backend() if distributed else None
+
+    def sync():
+        if not args.dry:
+            torch.cuda.synchronize(device)
+
+    ctx = None
+    G = None
+    S = 0
+    if not args.dry:
+        from exacto_amd._ffi import HipContext
+        ctx = HipContext(n, moduli, aux, plain, gbase, device=local)
+        ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        if args.chunk:
+            ctx.set_chunk(args.chunk)
+        G, S = ctx.G, ctx.ks32_primes
+    else:   # compute_gadget_digits (params/mod.rs:126-140): the fewest g with base^g >= Q
+        Q, G = math.prod(moduli), 0
+        while gbase ** G < Q:
+            G += 1
 
     gen = torch.Generator(device=device)
-    gen.manual_seed(0xE7AC7003 + rank)
-    kgen = torch.Generator(device=device)
-    kgen.manual_seed(0xE7AC7003)
-    if args.config == "cfg2":
-        a = uniform_dev((B,), moduli, n, gen, device)
-        b = uniform_dev((B,), moduli, n, gen, device)
+    gen.manual_seed(0xE7AC7003 + (rank if args.split == "batch" else 0))
 
-        # EXACTO_BENCH_CFG2: "polymul" (default) one fused kernel per product (exacto_rns_polymul_dev);
-        # "mulinv" forward transforms + product fused into the inverse; "unfused" the four API calls
+    def uniform(shape_prefix, g=None):
+        out = torch.empty(tuple(shape_prefix) + (L, n), dtype=torch.int64, device=device)
+        for i, q in enumerate(moduli):
+            out[..., i, :] = torch.randint(0, q, tuple(shape_prefix) + (n,), generator=g or gen, dtype=torch.int64,
+                                           device=device)
+        return out
+
+    # relinearisation key: made on rank 0 only, broadcast by the library's RCCL into every rank's
+    # resident key (ncclBroadcast over xGMI)
+    key_collective = None
+    if args.config != "cfg2":
+        kgen = torch.Generator(device=device)
+        kgen.manual_seed(0xE7AC7003)
+        if args.dry:
+            rlk = uniform((G, 2), kgen) if rank == 0 else torch.zeros((G, 2, L, n), dtype=torch.int64)
+            if distributed:
+                dist.broadcast(rlk, src=0)
+                key_collective = "torch.distributed.broadcast (gloo, dry)"
+        else:
+            if rank == 0:
+                rlk = uniform((G, 2), kgen)
+                sync()
+                ctx.load_relin_key_dev(rlk, G)
+            if distributed:
+                comm = xdist.rccl_comm_for(ctx, local)
+                ctx.broadcast_relin_key(comm, 0, G)
+                key_collective = "exacto_ctx_broadcast_relin_key (ncclBroadcast, library RCCL communicator)"
+            sync()
+
+    # ---- the step: one pass over one batch (`one(i)`, i = input copy), timed `reps` times per step
+    nbuf = 2
+    parts = None
+    if args.config == "cfg2":
+        a = [uniform((B,)) for _ in range(nbuf)]
+        b = [uniform((B,)) for _ in range(nbuf)]
+        outs = [torch.empty_like(a[0]) for _ in range(nbuf)]
         mode = os.environ.get("EXACTO_BENCH_CFG2", "polymul")
 
-        def step():  # fwd NTT of both operands, pointwise product, inverse NTT
-            if mode == "polymul":
-                ctx.rns_polymul_dev(a, b, a, B)
-                return
-            ctx.rns_fwd_dev(a, B)
-            ctx.rns_fwd_dev(b, B)
-            if mode == "mulinv":
-                ctx.rns_mul_inv_dev(a, b, a, B)
+        def one(i):   # fwd NTT of both operands, pointwise product, inverse NTT
+            if args.dry:
+                torch.add(a[i], b[i], out=outs[i])
+            elif mode == "polymul":
+                ctx.rns_polymul_dev(a[i], b[i], outs[i], B)
             else:
-                ctx.rns_mul_dev(a, b, a, B)
-                ctx.rns_inv_dev(a, B)
-        units_per_step = B
+                outs[i].copy_(a[i])
+                ctx.rns_fwd_dev(outs[i], B)
+                ctx.rns_fwd_dev(b[i], B)
+                if mode == "mulinv":
+                    ctx.rns_mul_inv_dev(outs[i], b[i], outs[i], B)
+                else:
+                    ctx.rns_mul_dev(outs[i], b[i], outs[i], B)
+                    ctx.rns_inv_dev(outs[i], B)
         unit = "poly_mul/s"
         metric = "NTT-based negacyclic poly muls/sec (fwd NTT x2 + pointwise + inv NTT)"
+    elif args.config == "galois":
+        ct = [uniform((B, 2)) for _ in range(nbuf)]
+        gk = uniform((G, 2))
+        outs = [torch.empty_like(ct[0]) for _ in range(nbuf)]
+
+        def one(i):
+            if args.dry:
+                torch.add(ct[i], 1, out=outs[i])
+            else:
+                ctx.bfv_apply_automorphism_dev(ct[i], 5, gk, G, outs[i], B)
+        unit = "bfv_apply_automorphism/s"
+        metric = "Galois automorphisms/sec (bfv_apply_automorphism, key switched)"
+    elif dbfv is None:
+        ct1 = [uniform((B, 2)) for _ in range(nbuf)]
+        ct2 = [uniform((B, 2)) for _ in range(nbuf)]
+        outs = [torch.empty_like(ct1[0]) for _ in range(nbuf)]
+
+        def one(i):
+            if args.dry:
+                torch.add(ct1[i], ct2[i], out=outs[i])
+            else:
+                ctx.bfv_mul_and_relin_dev(ct1[i], ct2[i], outs[i], B)
+        unit = "bfv_mul_and_relin/s"
+        metric = "ciphertext muls/sec (bfv_mul_and_relin)"
     else:
-        # relinearisation key: made once on rank 0, RCCL-broadcast to every GPU
-        rlk = uniform_dev((G, 2), moduli, n, kgen, device) if rank == 0 else \
-            torch.empty((G, 2, L, n), dtype=torch.int64, device=device)
-        if distributed:
-            dist.broadcast(rlk, src=0)
-        torch.cuda.synchronize(device)
-        ctx.load_relin_key_dev(rlk, G)
-        if args.config == "galois":
-            ct1 = uniform_dev((B, 2), moduli, n, gen, device)
-            gk = uniform_dev((G, 2), moduli, n, kgen, device)
-            out = torch.empty_like(ct1)
+        d, base, dplain = dbfv
+        x = [uniform((B, d, 2)) for _ in range(nbuf)]
+        y = [uniform((B, d, 2)) for _ in range(nbuf)]
+        outs = [torch.empty_like(x[0]) for _ in range(nbuf)]
+        if args.split == "limbs":
+            parts = xdist.limb_partition(d, world) if distributed else [list(range(d))]
+            mine = parts[rank]
+            compact = torch.zeros((B, max(len(mine), 1), 2, L, n), dtype=torch.int64, device=device)
+            acc = [torch.empty_like(x[0]), torch.empty_like(x[0])]
 
-            def step():
-                ctx.bfv_apply_automorphism_dev(ct1, 5, gk, G, out, B)
-            units_per_step = B
-            unit = "bfv_apply_automorphism/s"
-            metric = "Galois automorphisms/sec (bfv_apply_automorphism, key switched)"
-        elif dbfv is None:
-            ct1 = uniform_dev((B, 2), moduli, n, gen, device)
-            ct2 = uniform_dev((B, 2), moduli, n, gen, device)
-            out = torch.empty_like(ct1)
+            def limbs_mul(src, yy, dst):
+                # this rank's output limbs, then every limb on every rank
+                if mine:
+                    if args.dry:   # stand-in: limb k <- src[:, k] + yy[:, k] (checks the gather below)
+                        torch.add(src[:, mine], yy[:, mine], out=compact[:, : len(mine)])
+                    else:
+                        ctx.dbfv_mul_limbs_dev(d, base, dplain, src, yy, compact, B, mine)
+                if distributed:
+                    xdist.gather_limbs(compact[:, : len(mine)] if mine else compact[:, :0], parts, d, out=dst)
+                else:
+                    dst.copy_(compact)
 
-            def step():
-                ctx.bfv_mul_and_relin_dev(ct1, ct2, out, B)
-            units_per_step = B
-            unit = "bfv_mul_and_relin/s"
-            metric = "ciphertext muls/sec (bfv_mul_and_relin)"
+            def one(i):
+                # depth-`depth` chain (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220)
+                src = x[i]
+                for s in range(depth):
+                    dst = outs[i] if s == depth - 1 else acc[s % 2]
+                    limbs_mul(src, y[i], dst)
+                    src = dst
         else:
-            d, base, dplain = dbfv
-            x = uniform_dev((B, d, 2), moduli, n, gen, device)
-            y = uniform_dev((B, d, 2), moduli, n, gen, device)
-            bufs = [torch.empty_like(x), torch.empty_like(x)]
-
-            def step():
+            def one(i):
                 # depth-`depth` chain: acc <- dbfv_mul(acc, y), mul_depth reset before every step
                 # (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220), one native call
-                if depth == 1:
-                    ctx.dbfv_mul_dev(d, base, dplain, x, y, bufs[0], B)
+                if args.dry:
+                    torch.add(x[i], y[i], out=outs[i])
+                elif depth == 1:
+                    ctx.dbfv_mul_dev(d, base, dplain, x[i], y[i], outs[i], B)
                 else:
-                    ctx.dbfv_mul_chain_dev(d, base, dplain, x, y, bufs[0], B, depth)
-            units_per_step = B
-            unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
-            metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else \
-                f"dbfv_mul chains/sec (depth {depth})"
-    torch.cuda.synchronize(device)
+                    ctx.dbfv_mul_chain_dev(d, base, dplain, x[i], y[i], outs[i], B, depth)
+        unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
+        metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else f"dbfv_mul chains/sec (depth {depth})"
+    sync()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
+    for w in range(args.warmup):
+        one(w % nbuf)
+    sync()
+    # batches per step: the K timed steps last >= --min-time (the slowest rank decides)
+    reps = args.reps
+    if reps <= 0:
+        t0 = time.perf_counter()
+        for i in range(nbuf):
+            one(i)
+        sync()
+        per = (time.perf_counter() - t0) / nbuf
+        per = xdist.max_over_ranks(per, device=device if backend == "nccl" else None)
+        reps = max(1, math.ceil(args.min_time / max(args.steps * per, 1e-9)))
+
+    def step():
+        for r in range(reps):
+            one(r % nbuf)
+
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(device)
+    sync()
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = xdist.max_over_ranks(elapsed, device=device if backend == "nccl" else None)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = world * units_per_step * args.steps / elapsed
+    units_per_step = B * reps
+    total_units = (world if args.split == "batch" else 1) * units_per_step * args.steps
+    value = total_units / elapsed
 
-    # roofline of the dominant kernel: one profiled step, HIP events around every NTT launch
-    ctx.prof_enable(True)
-    step()
-    torch.cuda.synchronize(device)
-    fwd = ctx.prof_read(0)
-    inv = ctx.prof_read(1)
-    fused = ctx.prof_read(3)
-    ctx.prof_enable(False)
-    logn = n.bit_length() - 1
-    # every BASELINE prime lies in (2^60 - 2^32, 2^60): n = 4096 / 8192 take the hand-scheduled
-    # kernels (n = 4096 forward: the persistent LDS-DMA form)
-    on = lambda k: os.environ.get(k, "1") != "0"
-    asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    fwd_name = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and on("EXACTO_NTT_PIPE")
-                else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}>")
-    inv_name = f"ntt_inv_asm_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}>"
-    dom, dom_name = (fwd, fwd_name) if fwd["ms"] >= inv["ms"] else (inv, inv_name)
-    if fused["ms"] > dom["ms"]:   # cfg2's fused product kernel (3 transforms; bytes: a, b in, product out)
-        dom, dom_name = fused, f"ntt_polymul_kernel<{logn}>"
-    achieved = dom["bytes"] / (dom["ms"] * 1e-3) / 1e9 if dom["ms"] > 0 else 0.0
-    per_launch_ms = dom["ms"] / max(dom["launches"], 1)
-    roofline = {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
-        "kernel": dom_name,
-        "launches_per_step": dom["launches"],
-        "avg_launch_us": round(per_launch_ms * 1000.0, 2),
-        "bytes_per_launch": dom["bytes"] / max(dom["launches"], 1),
-        "polys_per_step": dom["polys"],
-        "ntt_share_of_step": round((fwd["ms"] + inv["ms"] + fused["ms"]) / ms_per_step, 3),
-    }
-    # HBM bytes per launch from the committed PMC passes over this same bench configuration
-    # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch, gfx950 corrections, averaged
-    # over every forward-NTT dispatch: the same launch mix per step as the timed one)
-    tfile = os.path.join(ROOT, "profiles", f"r2_{args.config}_fwd_traffic.json")
-    if dom_name.startswith("ntt_fwd") and os.path.exists(tfile):
-        with open(tfile) as f:
-            tr = json.load(f)
-        roofline["traffic"] = round(tr["traffic_bytes_avg"], 1)
-        roofline["traffic_over_algorithmic"] = round(tr["traffic_bytes_avg"] / roofline["bytes_per_launch"], 4)
-        roofline["traffic_source"] = os.path.relpath(tfile, ROOT)
+    dry_check = None
+    if args.dry and args.split == "limbs":
+        # stand-in chain: every step adds y, so the assembled output is x + depth * y on every limb
+        dry_check = bool(torch.equal(outs[(reps - 1) % nbuf], x[(reps - 1) % nbuf] + depth * y[(reps - 1) % nbuf]))
 
-    # the compute-side ceiling of the same kernel (integer modular arithmetic: the VALU issue rate,
-    # not MFMA): VALU wave-instructions and GPU cycles per dispatch from the committed PMC pass
-    # over this bench (tools/r2_evidence.sh), at the measured ~4.4 cycles per integer
-    # multiply-class wave-instruction per SIMD (tools/op_rate.hip, 1024 SIMDs)
-    vfile = os.path.join(ROOT, "profiles", f"r2_{args.config}_valu_counters.json")
-    if os.path.exists(vfile):
-        with open(vfile) as f:
-            vc = json.load(f)["kernels"]
-        hit = [v for k, v in vc.items() if dom_name.split("<")[0] in k]
-        if hit:
-            v = hit[0]
-            need = v["valu_insts"] * 4.4 / 1024.0
-            roofline["compute"] = {"bound": "valu", "valu_insts_per_launch": round(v["valu_insts"]),
-                                   "cycles_per_valu": 4.4, "gpu_cycles_per_launch": round(v["gpu_cycles"]),
-                                   "frac": round(need / v["gpu_cycles"], 3),
-                                   "source": os.path.relpath(vfile, ROOT)}
+    roofline, ntt, kernels = None, None, None
+    if not args.dry:
+        roofline, ntt, kernels = roofline_block(ctx, lambda: one(0), args.config, n, L, S)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "cfg3":
-        # all the host cores this job may use (16 on the GPU box, whose os.cpu_count() reports the
-        # whole machine), one product per thread; the single-thread figure rides along
-        threads = min(16, os.cpu_count() or 1)
-        try:
-            # about 10-15 s of CPU work: 8 products per thread
-            cpu = cpu_baseline(n, moduli, plain, gbase, args.cpu_sample or 8 * threads, threads)
-            one = cpu_baseline(n, moduli, plain, gbase, 2, 1)
-            cpu["single_thread"] = {"value": one["value"], "sample": one["sample"]}
-        except Exception as e:  # the baseline is informative; never fail the bench on it
+    if (rank == 0 and world == 1 and not args.dry and not args.no_cpu_baseline
+            and args.config in ("cfg3", "cfg4", "cfg5")):
+        try:   # informative; never fail the bench on it
+            cpu = cpu_baseline(args.config, n, moduli, plain, gbase, dbfv, depth, args.cpu_sample)
+        except Exception as e:
             cpu = {"value": None, "error": repr(e)}
 
     if rank == 0:
@@ -318,20 +485,33 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.split == "batch" else "strong",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (uniform canonical residues per limb, seeded; rlk broadcast over RCCL)",
+            "data": "synthetic (uniform canonical residues per limb, seeded; two resident input copies "
+                    "rotated; rlk made on rank 0 and broadcast)" + ("; DRY RUN: no GPU work" if args.dry else ""),
             "config": {"workload": workload, "ring_degree": n, "ct_limbs": L, "limb_bits": 60,
                        "plain_modulus": plain, "gadget_base": gbase, "gadget_digits": G,
-                       "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"batch-shard x{world}"},
+                       "batch_per_gpu": B, "global_batch": B * (world if args.split == "batch" else 1),
+                       "batches_per_step": reps, "units_per_step": units_per_step,
+                       "parallelism": (f"batch-shard x{world}" if args.split == "batch"
+                                       else f"dbfv output-limb split x{world}: {parts}")},
+            "world_size": world,
+            "backend": backend,
+            "key_broadcast": key_collective,
+            "timed_s": round(elapsed, 3),
             "roofline": roofline,
+            "ntt": ntt,
+            "kernels": kernels,
             "cpu_baseline": cpu,
         }
         if dbfv is not None:
             line["config"].update({"dbfv_digits": dbfv[0], "dbfv_base": dbfv[1],
                                    "dbfv_plain_modulus": dbfv[2] or "2^64", "chain_depth": depth})
+        if args.dry:
+            line["dry"] = True
+            if dry_check is not None:
+                line["dry_gather_ok"] = dry_check
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()

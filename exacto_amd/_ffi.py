@@ -66,9 +66,12 @@ _SIGS = [
     ("exacto_rns_mul_inv_dev", [_P, _P, _P, _P, _SZ], C.c_int),
     ("exacto_rns_polymul_dev", [_P, _P, _P, _P, _SZ], C.c_int),
     ("exacto_rns_scalar_mul_dev", [_P, _P, _U64, _P, _SZ], C.c_int),
-    ("exacto_bfv_add_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
-    ("exacto_bfv_sub_dev", [_P, _P, _P, _P, _SZ, _SZ], C.c_int),
-    ("exacto_bfv_neg_dev", [_P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_bfv_add", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_add_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_sub", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_sub_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_neg", [_P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_bfv_neg_dev", [_P, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_mul_no_relin", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_mul_no_relin_dev", [_P, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_relinearize", [_P, _P, _SZ, _P, _SZ], C.c_int),
@@ -79,6 +82,8 @@ _SIGS = [
     ("exacto_dbfv_mul", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
     ("exacto_dbfv_mul_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _P, _P], C.c_int),
     ("exacto_dbfv_mul_chain", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _SZ], C.c_int),
+    ("exacto_dbfv_mul_limbs", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_dbfv_mul_limbs_dev", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_decrypt", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
     ("exacto_bfv_decrypt_dev", [_P, _P, _SZ, _P, _P, _SZ], C.c_int),
     ("exacto_dbfv_decrypt", [_P, _SZ, _U64, _U64, _P, _P, _P, _SZ], C.c_int),
@@ -125,6 +130,12 @@ _SIGS = [
     ("exacto_bootstrap_key_material_dev", [_P, _P, _P, _P, _P], C.c_int),
     ("exacto_bfv_bootstrap", [_P, _P, _P, _SZ, _P, _P, _SZ, _U64, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
     ("exacto_bfv_bootstrap_dev", [_P, _P, _P, _SZ, _P, _P, _SZ, _U64, _P, _SZ, _P, _SZ, _P, _SZ], C.c_int),
+    ("exacto_rccl_unique_id", [_P], C.c_int),
+    ("exacto_rccl_comm_init", [C.POINTER(_P), C.c_int, _P, C.c_int, C.c_int], C.c_int),
+    ("exacto_rccl_comm_destroy", [_P], C.c_int),
+    ("exacto_ctx_broadcast_relin_key", [_P, _P, C.c_int, _SZ], C.c_int),
+    ("exacto_broadcast_galois_key", [_P, _P, C.c_int, _P, _SZ], C.c_int),
+    ("exacto_rccl_allgather_u64", [_P, _P, _P, _P, _SZ], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
@@ -203,6 +214,33 @@ def bfv_bootstrap_raw(orig: "HipContext", boot: "HipContext", ct, bsk, rpoly, q_
                                       gks.ctypes.data if E else None, gks.shape[1] if E else 0, out.ctypes.data,
                                       ct.shape[0]))
     return out
+
+
+def rccl_unique_id() -> bytes:
+    """ncclGetUniqueId (128 bytes) through the library's RCCL (exacto_rccl_unique_id)."""
+    buf = (C.c_uint8 * 128)()
+    check(load().exacto_rccl_unique_id(buf))
+    return bytes(buf)
+
+
+class RcclComm:
+    """An RCCL communicator (ncclComm_t) made by the library (exacto_rccl_comm_init) on `device`."""
+
+    def __init__(self, nranks: int, uid: bytes, rank: int, device: int = 0):
+        lib = load()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib.exacto_rccl_comm_init(C.byref(h), nranks, buf, rank, device))
+        self._h, self._lib, self.nranks, self.rank = h, lib, nranks, rank
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            check(self._lib.exacto_rccl_comm_destroy(self._h))
+            self._h = None
 
 
 def required_trace_elements(n: int) -> list[int]:
@@ -336,6 +374,28 @@ class HipContext:
         out = np.zeros((B, 2, self.L, self.n), dtype=np.uint64)
         check(self._lib.exacto_bfv_mul_and_relin(self._h, ct1.ctypes.data, ct2.ctypes.data,
                                                  out.ctypes.data, B))
+        return out
+
+    def _addsub(self, fn, ct1, ct2):
+        ct1, ct2 = _u64(ct1), _u64(ct2)
+        B = ct1.shape[0]
+        out = np.zeros((B, max(ct1.shape[1], ct2.shape[1]), self.L, self.n), dtype=np.uint64)
+        check(fn(self._h, ct1.ctypes.data, ct1.shape[1], ct2.ctypes.data, ct2.shape[1], out.ctypes.data, B))
+        return out
+
+    def bfv_add(self, ct1: np.ndarray, ct2: np.ndarray) -> np.ndarray:
+        """eval.rs:14-31 batched: ct1 [B][p1][L][n] + ct2 [B][p2][L][n] -> [B][max][L][n]."""
+        return self._addsub(self._lib.exacto_bfv_add, ct1, ct2)
+
+    def bfv_sub(self, ct1: np.ndarray, ct2: np.ndarray) -> np.ndarray:
+        """eval.rs:34-51 batched (ct2's extra components negated)."""
+        return self._addsub(self._lib.exacto_bfv_sub, ct1, ct2)
+
+    def bfv_neg(self, ct: np.ndarray) -> np.ndarray:
+        """eval.rs:54-60 batched."""
+        ct = _u64(ct)
+        out = np.zeros_like(ct)
+        check(self._lib.exacto_bfv_neg(self._h, ct.ctypes.data, ct.shape[1], out.ctypes.data, ct.shape[0]))
         return out
 
     def dbfv_mul(self, d, base, plain, a: np.ndarray, b: np.ndarray, depth_a=None, depth_b=None):
@@ -610,14 +670,14 @@ class HipContext:
     def rns_scalar_mul_dev(self, a, scalar, out, count):
         check(self._lib.exacto_rns_scalar_mul_dev(self._h, self._p(a), scalar, self._p(out), count))
 
-    def bfv_add_dev(self, a, b, out, batch, polys=2):
-        check(self._lib.exacto_bfv_add_dev(self._h, self._p(a), self._p(b), self._p(out), batch, polys))
+    def bfv_add_dev(self, a, polys1, b, polys2, out, batch):
+        check(self._lib.exacto_bfv_add_dev(self._h, self._p(a), polys1, self._p(b), polys2, self._p(out), batch))
 
-    def bfv_sub_dev(self, a, b, out, batch, polys=2):
-        check(self._lib.exacto_bfv_sub_dev(self._h, self._p(a), self._p(b), self._p(out), batch, polys))
+    def bfv_sub_dev(self, a, polys1, b, polys2, out, batch):
+        check(self._lib.exacto_bfv_sub_dev(self._h, self._p(a), polys1, self._p(b), polys2, self._p(out), batch))
 
-    def bfv_neg_dev(self, a, out, batch, polys=2):
-        check(self._lib.exacto_bfv_neg_dev(self._h, self._p(a), self._p(out), batch, polys))
+    def bfv_neg_dev(self, a, polys, out, batch):
+        check(self._lib.exacto_bfv_neg_dev(self._h, self._p(a), polys, self._p(out), batch))
 
     def bfv_mul_no_relin_dev(self, ct1, ct2, out, batch):
         check(self._lib.exacto_bfv_mul_no_relin_dev(self._h, self._p(ct1), 2, self._p(ct2), 2,
@@ -643,6 +703,32 @@ class HipContext:
         db = np.ascontiguousarray(depth_b, dtype=np.uint32) if depth_b is not None else None
         check(self._lib.exacto_dbfv_mul_dev(self._h, d, base, plain, self._p(a), self._p(b),
                                             self._p(out), batch, _ptr(da), _ptr(db), None))
+
+    def dbfv_mul_limbs(self, d, base, plain, a: np.ndarray, b: np.ndarray, limbs) -> np.ndarray:
+        """One GPU's output limbs of a split dbfv_mul: [B][len(limbs)][2][L][n], slot s = limb limbs[s]."""
+        a, b = _u64(a), _u64(b)
+        ls = np.ascontiguousarray(np.asarray(limbs, dtype=np.uint32))
+        out = np.zeros((a.shape[0], ls.size, 2, self.L, self.n), dtype=np.uint64)
+        check(self._lib.exacto_dbfv_mul_limbs(self._h, d, base, plain, a.ctypes.data, b.ctypes.data, out.ctypes.data,
+                                              a.shape[0], ls.ctypes.data if ls.size else None, ls.size))
+        return out
+
+    def dbfv_mul_limbs_dev(self, d, base, plain, a, b, out, batch, limbs):
+        ls = np.ascontiguousarray(np.asarray(limbs, dtype=np.uint32))
+        check(self._lib.exacto_dbfv_mul_limbs_dev(self._h, d, base, plain, self._p(a), self._p(b), self._p(out),
+                                                  batch, ls.ctypes.data if ls.size else None, ls.size))
+
+    # ---- RCCL collectives (exacto_hip.h; comm = RcclComm)
+    def broadcast_relin_key(self, comm: "RcclComm", root: int, num_keys: int):
+        """Root's resident relinearisation key -> this context's resident key (ncclBroadcast, in place)."""
+        check(self._lib.exacto_ctx_broadcast_relin_key(self._h, comm.handle, root, num_keys))
+
+    def broadcast_galois_key(self, comm: "RcclComm", root: int, gk_dev, num_keys: int):
+        check(self._lib.exacto_broadcast_galois_key(self._h, comm.handle, root, self._p(gk_dev), num_keys))
+
+    def allgather_u64(self, comm: "RcclComm", send, recv, count: int):
+        """recv = [nranks][count] u64 (ncclAllGather on the context stream)."""
+        check(self._lib.exacto_rccl_allgather_u64(self._h, comm.handle, self._p(send), self._p(recv), count))
 
     def dbfv_mul_chain_dev(self, d, base, plain, x, y, out, batch, depth):
         check(self._lib.exacto_dbfv_mul_chain_dev(self._h, d, base, plain, self._p(x), self._p(y),

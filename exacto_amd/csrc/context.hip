@@ -307,6 +307,7 @@ struct exacto_ctx {
     size_t cached_B = 0, cached_d = 0;
     u64 cached_base = 0, cached_p = 0;
     int cached_npairs = 0;
+    std::vector<int> cached_limbs;   // output limbs of the cached plan (all d, or a subset: exacto_dbfv_mul_limbs)
     int cached_sum_m = 0;        // max products per dBFV output limb when all combine terms are sums, else -1
     int* d_term_start = nullptr;
     CombineTerm* d_terms = nullptr;
@@ -904,14 +905,35 @@ extern "C" int exacto_ctx_load_relin_key(exacto_ctx* c, const uint64_t* rlk, siz
 
 // ============================================================== NTT helper (+ profiling)
 
+// Kernel families timed by exacto_prof_enable (HIP events around each launch on the launching
+// stream; the bench's roofline takes the family with the largest share of a profiled step).
+// Bytes are ALGORITHMIC: each operand read once and each result written once.
+enum ProfKind : int {
+    PK_FWD = 0, PK_INV = 1, PK_TENSOR = 2, PK_POLYMUL = 3, PK_LIFT = 4, PK_SCALE = 5, PK_KS_DIGITS = 6,
+    PK_KS_MAC = 7, PK_KS_CRT = 8, PK_PAIRSUM = 9, PK_PSUM_SCALE = 10, PK_TENSOR_C2 = 11, PK_DIGIT_SUM = 12,
+    PK_COMBINE = 13, PK_COUNT = 14
+};
+
+struct ProfScope {
+    exacto_ctx* c;
+    ProfRec rec{};
+    bool on;
+    ProfScope(exacto_ctx* c_, int kind, u64 units, double bytes) : c(c_), on(c_->prof) {
+        if (!on) return;
+        rec.kind = kind; rec.polys = units; rec.bytes = bytes;
+        if (hipEventCreate(&rec.a) != hipSuccess || hipEventCreate(&rec.b) != hipSuccess ||
+            hipEventRecord(rec.a, c->stream) != hipSuccess)
+            on = false;
+    }
+    ~ProfScope() {
+        if (on && hipEventRecord(rec.b, c->stream) == hipSuccess) c->recs.push_back(rec);
+    }
+};
+
 static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) {
     if (count <= 0) return 0;
-    ProfRec rec{};
-    if (c->prof) {
-        HIP_TRY(hipEventCreate(&rec.a));
-        HIP_TRY(hipEventCreate(&rec.b));
-        HIP_TRY(hipEventRecord(rec.a, c->stream));
-    }
+    // algorithmic bytes: one read of the source (int16 digits: 2 B per coefficient) + one 8 B write
+    ProfScope ps(c, inverse ? PK_INV : PK_FWD, (u64)count, ((nb.src16 ? 2.0 : 8.0) + 8.0) * c->n * (double)count);
     bool lazy = true, near60 = c->ntt_asm;
     for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) {
         lazy &= c->primes[t] < (1ull << 60);
@@ -920,41 +942,38 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, c->ntt_pipe,
                near60 && c->ntt_asm_inv);
     CHECK_LAUNCH();
-    if (c->prof) {
-        HIP_TRY(hipEventRecord(rec.b, c->stream));
-        rec.kind = inverse ? 1 : 0;
-        rec.polys = (u64)count;
-        // algorithmic bytes: one read of the source (int16 digits: 2 B per coefficient) + one
-        // 8 B write per coefficient
-        rec.bytes = ((nb.src16 ? 2.0 : 8.0) + 8.0) * c->n * (double)count;
-        c->recs.push_back(rec);
-    }
     return 0;
 }
 
 static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only = false) {
     const int NP = c->L + c->K;
-    ProfRec rec{};
-    if (c->prof) {
-        HIP_TRY(hipEventCreate(&rec.a));
-        HIP_TRY(hipEventCreate(&rec.b));
-        HIP_TRY(hipEventRecord(rec.a, c->stream));
-    }
     bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
     for (int t = 0; t < NP; ++t) {
         lazy &= c->primes[t] < (1ull << 60);
         // the fused product (mulmod_near60) needs d = 2^60 - q < 2^24; the asm rounds d < 2^32
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
     }
-    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only);
-    CHECK_LAUNCH();
-    if (c->prof) {
-        HIP_TRY(hipEventRecord(rec.b, c->stream));
-        rec.kind = 2;  // fused tensor + inverse
-        rec.polys = (u64)cnt * 3 * NP;
-        rec.bytes = 8.0 * c->n * 11.0 * cnt * NP;  // 8 operand reads + 3 writes per (item, prime)
-        c->recs.push_back(rec);
+    // algorithmic bytes per (item, prime): the four operands a0, a1, b0, b1 in and the three
+    // components out (7 polys); psum's auxiliary primes only c2 = a1 b1 (2 in, 1 out)
+    const double pb = 8.0 * c->n;
+    if (p2only && inverse_tensor_split(c->logn)) {
+        {   // ciphertext primes: all three components
+            ProfScope ps(c, PK_TENSOR, (u64)cnt * 3 * c->L, pb * 7.0 * cnt * c->L);
+            launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60,
+                              p2only, 0);
+            CHECK_LAUNCH();
+        }
+        ProfScope ps(c, PK_TENSOR_C2, (u64)cnt * c->K, pb * 3.0 * cnt * c->K);
+        launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60,
+                          p2only, 1);
+        CHECK_LAUNCH();
+        return 0;
     }
+    const double per_item = p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP;
+    ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), per_item * cnt);
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
+                      -1);
+    CHECK_LAUNCH();
     return 0;
 }
 
@@ -1140,7 +1159,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     if (c->deferred_code) return fail(c->deferred_code, c->deferred_msg);
     if (relin && !c->rlk_loaded) return fail(EXACTO_ERR_MISSING_KEY, "key not available: relinearization key not loaded");
     if (P <= 0) return 0;
-    const int n = c->n, L = c->L, K = c->K, NP = L + K;
+    const int n = c->n, L = c->L, K = c->K;
     const long Ln = (long)L * n;
     const int guse = relin ? (int)std::min<size_t>(c->G, c->rlk_keys) : 0;
     const exacto_ctx::PsumPlan& ps = c->psum;
@@ -1191,9 +1210,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // 2. extension to the auxiliary primes
             if (c->path == EXACTO_PATH_HPS)
                 launch_hps_extend(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_primes, K, c->stream);
-            else
+            else {
+                ProfScope pl(c, PK_LIFT, 4ull * cnt, 8.0 * (L + K) * n * 4.0 * cnt);
                 launch_exact_lift(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_crt, c->d_primes, L, K,
                                   crt_mode(c), c->stream);
+            }
             CHECK_LAUNCH();
             // 3. forward NTT of the extended polynomials
             if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
@@ -1207,8 +1228,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // the output limbs' c0 / c1 auxiliary residues, summed over their products, then inverse-
             // transformed: [ib][k][c][a][n] in extP (unused: the extensions are shared, steps 1-3 skipped)
             const int ib_cnt = cnt / ps.npairs;
-            launch_dbfv_pairsum(o, c->ws_extP, ib_cnt, ps.d, ps.npairs, ps.term_start, ps.terms, L, K, n, c->d_primes,
-                                c->stream);
+            {   // per (item, prime): the 2d input ciphertexts' two polys in, 2 sums per output limb out
+                ProfScope pp(c, PK_PAIRSUM, (u64)ib_cnt * K * ps.d, 8.0 * n * K * ib_cnt * (4.0 * ps.d + 2.0 * ps.d));
+                launch_dbfv_pairsum(o, c->ws_extP, ib_cnt, ps.d, ps.npairs, ps.term_start, ps.terms, L, K, n,
+                                    c->d_primes, c->stream);
+            }
             CHECK_LAUNCH();
             if (int e = run_ntt(c, contiguous(c->ws_extP, (long)ib_cnt * ps.d, 2L * K, L, K, n),
                                 (long)ib_cnt * ps.d * 2 * K, true))
@@ -1218,6 +1242,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         u64* R = out + s * out_stride;
         const int ncomp = relin ? 2 : 3;
         u64* D = relin ? c->ws_D : nullptr;
+        // scale bytes per item: the three components' L+K residues in; c0, c1 (L residues each) out
+        // (psum: c2 only), and the third component's digits (int16 / int8) or its L residues
+        const double dig_b = d16 ? (c->ks_defer && c->ks_defer8 ? 1.0 : 2.0) * guse : 8.0 * L * (relin ? guse : 1);
+        ProfScope psc(c, PK_SCALE, (u64)cnt, (double)n * cnt *
+                      ((ps.on ? 1.0 : 3.0) * 8.0 * (L + K) + (ps.on ? 0.0 : 16.0 * L) + (relin ? dig_b : 8.0 * L)));
         if (c->path == EXACTO_PATH_HPS)
             launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
         else
@@ -1232,6 +1261,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         CHECK_LAUNCH();
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
             const long item0 = s / ps.npairs;
+            const double ib = (double)(cnt / ps.npairs);
+            // per item: each limb's summed auxiliary residues (K) and its products' ciphertext-prime
+            // residues (L each) in, the limb's L residues out, for c0 and c1
+            ProfScope pq(c, PK_PSUM_SCALE, (u64)(cnt / ps.npairs) * ps.d,
+                         ib * 2.0 * n * 8.0 * (ps.d * (double)(K + L) + (double)ps.npairs * L));
             if (!launch_psum_scale(c->ws_T, c->ws_extP, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
                                    ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream))
                 return fail(EXACTO_ERR_HIP, "internal: psum scale not available for these limbs");
@@ -1258,8 +1292,14 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             // key in the same basis, inverse NTT + centred lift, added to R mod q_l in the
             // coefficient domain; the forward NTT of R below then yields the relinearised result
             if (!c->ks_defer) {   // (deferred: the caller sums the digits of products first, dbfv_mul_core)
-                ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-                ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
+                {   // int16 digit in (2 B), 31-bit residue out (4 B) per coefficient and prime
+                    ProfScope pd(c, PK_KS_DIGITS, (u64)cnt * guse * c->S32, 6.0 * n * cnt * guse * c->S32);
+                    ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
+                }
+                {   // per (item, prime, coefficient): G digit residues in, 2L sums out (the key slice from LDS)
+                    ProfScope pm(c, PK_KS_MAC, (u64)cnt * c->S32, 4.0 * n * cnt * c->S32 * (guse + 2.0 * L));
+                    ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
+                }
                 // lift + the forward NTT of R in one kernel when the asm forward rounds serve R's primes
                 bool fused = false;
                 if (!skip_fwd && c->crt_fwd > 0 && c->ntt_asm && ncomp == 2) {
@@ -1268,9 +1308,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                     fused = near && launch_ks32_crt_fwd(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32,
                                                         c->d_primes, c->stream, c->crt_fwd);
                 }
-                if (!fused)
+                if (!fused) {   // per (item, component, limb): S 31-bit sums in, R in and out
+                    ProfScope pc(c, PK_KS_CRT, (u64)cnt * 2 * L, (double)n * cnt * 2 * L * (4.0 * c->S32 + 16.0));
                     ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
                              c->stream);
+                }
                 CHECK_LAUNCH();
                 if (fused) continue;   // R is relinearised and in the NTT domain
             }
@@ -1387,22 +1429,11 @@ extern "C" int exacto_rns_polymul_dev(exacto_ctx* c, const uint64_t* a, const ui
         near60 &= c->ctq[t] < (1ull << 60) && c->ctq[t] > (1ull << 60) - (1ull << 24);
     }
     const long rows = (long)count * c->L;
-    ProfRec rec{};
     if (near60 && (c->logn == 12 || c->logn == 13)) {
-        if (c->prof) {
-            HIP_TRY(hipEventCreate(&rec.a));
-            HIP_TRY(hipEventCreate(&rec.b));
-            HIP_TRY(hipEventRecord(rec.a, c->stream));
-        }
+        // fused product: 3 transforms, algorithmic bytes a + b in, product out
+        ProfScope pp(c, PK_POLYMUL, (u64)rows, 24.0 * c->n * (double)rows);
         launch_polymul(a, b, o, rows, c->L, c->logn, c->d_primes, c->stream);
         CHECK_LAUNCH();
-        if (c->prof) {
-            HIP_TRY(hipEventRecord(rec.b, c->stream));
-            rec.kind = 3;   // fused product: 3 transforms, algorithmic bytes a + b in, product out
-            rec.polys = (u64)rows;
-            rec.bytes = 24.0 * c->n * (double)rows;
-            c->recs.push_back(rec);
-        }
         return 0;
     }
     Scratch sa, sb;
@@ -1429,15 +1460,34 @@ extern "C" int exacto_rns_scalar_mul_dev(exacto_ctx* c, const uint64_t* a, uint6
     return pw(c, PwOp::ScalarMul, a, nullptr, o, (long)n * c->L, c->d_scal);
 }
 
-// bfv_add / bfv_sub / bfv_neg over equal-degree ciphertexts (eval.rs:14-60)
-extern "C" int exacto_bfv_add_dev(exacto_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* o, size_t B, size_t polys) {
-    return pw(c, PwOp::Add, x, y, o, (long)B * polys * (c ? c->L : 0), nullptr);
+// bfv_add / bfv_sub / bfv_neg (eval.rs:14-60), batched: ct1 [B][p1][L][n], ct2 [B][p2][L][n] ->
+// out [B][max(p1, p2)][L][n].  Components beyond the shorter operand pass through from the longer
+// one, negated when they are ct2's under subtraction (eval.rs:21-22, 41-42).
+static int bfv_addsub(exacto_ctx* c, bool sub, const u64* x, size_t p1, const u64* y, size_t p2, u64* o, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    const size_t pm = std::max(p1, p2);
+    if (!B || !pm) return 0;
+    if ((p1 && !x) || (p2 && !y) || !o) return invalid_param("null ciphertext pointer");
+    // in place only over an operand laid out like the output
+    if ((o == x && p1 != pm) || (o == y && p2 != pm))
+        return invalid_param("output may alias an input only when it has as many components as the output");
+    launch_bfv_addsub(sub, x, (int)p1, y, (int)p2, o, (long)B, c->n, c->L, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    return 0;
 }
-extern "C" int exacto_bfv_sub_dev(exacto_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* o, size_t B, size_t polys) {
-    return pw(c, PwOp::Sub, x, y, o, (long)B * polys * (c ? c->L : 0), nullptr);
+extern "C" int exacto_bfv_add_dev(exacto_ctx* c, const uint64_t* x, size_t p1, const uint64_t* y, size_t p2, uint64_t* o,
+                                  size_t B) {
+    return bfv_addsub(c, false, x, p1, y, p2, o, B);
 }
-extern "C" int exacto_bfv_neg_dev(exacto_ctx* c, const uint64_t* x, uint64_t* o, size_t B, size_t polys) {
-    return pw(c, PwOp::Neg, x, nullptr, o, (long)B * polys * (c ? c->L : 0), nullptr);
+extern "C" int exacto_bfv_sub_dev(exacto_ctx* c, const uint64_t* x, size_t p1, const uint64_t* y, size_t p2, uint64_t* o,
+                                  size_t B) {
+    return bfv_addsub(c, true, x, p1, y, p2, o, B);
+}
+extern "C" int exacto_bfv_neg_dev(exacto_ctx* c, const uint64_t* x, size_t polys, uint64_t* o, size_t B) {
+    if (int e = check_ctx(c)) return e;
+    if (!B || !polys) return 0;
+    if (!x || !o) return invalid_param("null ciphertext pointer");
+    return pw(c, PwOp::Neg, x, nullptr, o, (long)B * polys * c->L, nullptr);
 }
 
 // ============================================================== C ABI: BFV
@@ -1566,6 +1616,27 @@ extern "C" int exacto_relinearize(exacto_ctx* c, const uint64_t* ct, size_t poly
 // ============================================================== C ABI: dBFV
 
 // lattice.rs:104-122 compute_simple + decomposition.rs:8-16 digit_decompose
+extern "C" int exacto_bfv_add(exacto_ctx* c, const uint64_t* ct1, size_t p1, const uint64_t* ct2, size_t p2,
+                              uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t pb = c->L * poly_bytes(c);
+    return host_call(c, {{ct1, B * p1 * pb}, {ct2, B * p2 * pb}}, B * std::max(p1, p2) * pb, out,
+                     [&](std::vector<u64*>& in, u64* o) { return exacto_bfv_add_dev(c, in[0], p1, in[1], p2, o, B); });
+}
+extern "C" int exacto_bfv_sub(exacto_ctx* c, const uint64_t* ct1, size_t p1, const uint64_t* ct2, size_t p2,
+                              uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t pb = c->L * poly_bytes(c);
+    return host_call(c, {{ct1, B * p1 * pb}, {ct2, B * p2 * pb}}, B * std::max(p1, p2) * pb, out,
+                     [&](std::vector<u64*>& in, u64* o) { return exacto_bfv_sub_dev(c, in[0], p1, in[1], p2, o, B); });
+}
+extern "C" int exacto_bfv_neg(exacto_ctx* c, const uint64_t* ct, size_t polys, uint64_t* out, size_t B) {
+    if (!c) return invalid_param("null context");
+    const size_t bytes = B * polys * c->L * poly_bytes(c);
+    return host_call(c, {{ct, bytes}}, bytes, out,
+                     [&](std::vector<u64*>& in, u64* o) { return exacto_bfv_neg_dev(c, in[0], polys, o, B); });
+}
+
 static std::vector<std::vector<i64>> small_reps(u64 base, size_t d, u64 p) {
     std::vector<std::vector<i64>> reps;
     for (size_t j = d; j + 1 < 2 * d; ++j) {
@@ -1584,37 +1655,43 @@ static std::vector<std::vector<i64>> small_reps(u64 base, size_t d, u64 p) {
     return reps;
 }
 
-static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
-    if (c->cached_B == B && c->cached_d == d && c->cached_base == base && c->cached_p == plain && c->d_off) return 0;
+// The product list and combine terms of a dbfv_mul batch (dbfv/eval.rs:109-132 + reduce,
+// reduction.rs:34-52) for the output limbs `limbs` (all of 0..d-1, or the subset one GPU computes
+// when the limbs of one dbfv_mul are split across GPUs): output slot s = limb limbs[s] gets the sum
+// over pairs (i, j) with i + j == limbs[s] plus the reps folding of the high limbs i + j >= d.  Only
+// the pairs some listed limb uses are multiplied.
+static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain, const std::vector<int>& limbs) {
+    if (c->cached_B == B && c->cached_d == d && c->cached_base == base && c->cached_p == plain && c->d_off &&
+        c->cached_limbs == limbs)
+        return 0;
     const auto reps = small_reps(base, d, plain);
+    const size_t dout = limbs.size();
+    auto coef_of = [&](size_t i, size_t j, size_t ko) -> i64 {
+        const size_t k = i + j;
+        return k == ko ? 1 : k >= d ? reps[k - d][ko] : 0;
+    };
     std::vector<std::pair<int, int>> pairs;
     for (size_t i = 0; i < d; ++i)
         for (size_t j = 0; j < d; ++j) {
-            const size_t k = i + j;
-            bool needed = k < d;
-            if (!needed)
-                for (i64 v : reps[k - d]) needed |= (v != 0);
+            bool needed = false;
+            for (int ko : limbs) needed |= coef_of(i, j, (size_t)ko) != 0;
             if (needed) pairs.push_back({(int)i, (int)j});
         }
     const int npairs = (int)pairs.size();
-    // combine terms: out limb k' <- sum over pairs with i+j == k' (coef 1) and reps folding
-    std::vector<int> start(d + 1, 0);
+    std::vector<int> start(dout + 1, 0);
     std::vector<CombineTerm> terms;
-    for (size_t ko = 0; ko < d; ++ko) {
-        start[ko] = (int)terms.size();
+    for (size_t so = 0; so < dout; ++so) {
+        start[so] = (int)terms.size();
         for (int pi = 0; pi < npairs; ++pi) {
-            const size_t k = pairs[pi].first + pairs[pi].second;
-            i64 coef = 0;
-            if (k == ko) coef = 1;
-            else if (k >= d) coef = reps[k - d][ko];
+            const i64 coef = coef_of(pairs[pi].first, pairs[pi].second, (size_t)limbs[so]);
             if (coef != 0) terms.push_back({pi, 0, coef});
         }
     }
-    start[d] = (int)terms.size();
+    start[dout] = (int)terms.size();
     // ks32 sums before the lift: every combine term a plain sum (zero reps), at most this many per limb
     int sum_m = 0;
     for (const CombineTerm& t : terms) if (t.coef != 1) sum_m = -1;
-    for (size_t ko = 0; ko < d && sum_m >= 0; ++ko) sum_m = std::max(sum_m, start[ko + 1] - start[ko]);
+    for (size_t so = 0; so < dout && sum_m >= 0; ++so) sum_m = std::max(sum_m, start[so + 1] - start[so]);
     const long Ln2 = 2L * c->L * c->n, Kn2 = 2L * c->K * c->n;
     // [0, BP): a offsets, [BP, 2BP): b offsets (ciphertexts), [2BP, 4BP): the same into the
     // per-ciphertext extension buffers
@@ -1640,6 +1717,7 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain) {
         if (int e_ = upload(c, c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm))) return e_;
     c->cached_B = B; c->cached_d = d; c->cached_base = base; c->cached_p = plain;
     c->cached_npairs = npairs;
+    c->cached_limbs = limbs;
     c->cached_sum_m = sum_m;
     return 0;
 }
@@ -1688,9 +1766,17 @@ static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
 }
 
 // b_extended: c->ext_b already holds the extensions of b (a chain's constant right operand)
+// out = [B][dout][2][L][n] for the output limbs `limbs` (nullptr: all d, dout = d)
 static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
-                         const uint64_t* b, uint64_t* out, size_t B, bool b_extended) {
-    if (int e = dbfv_plan(c, B, d, base, plain)) return e;
+                         const uint64_t* b, uint64_t* out, size_t B, bool b_extended,
+                         const std::vector<int>* limbs = nullptr) {
+    std::vector<int> all;
+    if (!limbs) {
+        for (size_t k = 0; k < d; ++k) all.push_back((int)k);
+        limbs = &all;
+    }
+    const size_t dout = limbs->size();
+    if (int e = dbfv_plan(c, B, d, base, plain, *limbs)) return e;
     const int npairs = c->cached_npairs;
     const long Ln2 = 2L * c->L * c->n;
     const long P = (long)B * npairs;
@@ -1732,7 +1818,7 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     const Ks32Tables* kst = use_wide ? c->kw.d_kst : c->d_kst;
     const bool long_runs = use_wide ? c->kw.long_runs : c->ks32_long_runs;
     const bool wide = (u64)m * (c->gbase / 2) > 32767;   // digit sums beyond int16
-    const size_t Bd = B * d, Sn = (size_t)S * c->n;
+    const size_t Bd = B * dout, Sn = (size_t)S * c->n;
     if (sum_ks) {
         if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
             grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * (wide ? 4 : 2), 8)) ||
@@ -1758,7 +1844,7 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
                       (c->logn == 12 || c->logn == 13) && exact_scale_sp_ok(c->L, c->K, crt_mode(c));
     if (psum) {
         c->psum.on = true;
-        c->psum.d = (int)d;
+        c->psum.d = (int)dout;
         c->psum.npairs = npairs;
         c->psum.term_start = c->d_term_start;
         c->psum.terms = c->d_terms;
@@ -1773,22 +1859,36 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     if (rc) return rc;
     if (sum_ks && !coef) return fail(EXACTO_ERR_HIP, "internal: ks32 sums without the ks32 key switch");
     if (!psum) {
-        launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)d, c->n, c->L,
+        ProfScope pk(c, PK_COMBINE, (u64)B * dout, 8.0 * c->n * B * 2 * c->L * (double)(npairs + dout));
+        launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)dout, c->n, c->L,
                             c->d_primes, c->stream);
         CHECK_LAUNCH();
     }
     if (sum_ks) {
-        ks32_digit_sum(c->d_dall, in8, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)d, (int)gu, c->n,
-                       c->stream);
-        if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
-        else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
-        ks32_mac(c->d_dsk, use_wide ? c->kw.d_rs : c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, S, c->n, p32,
-                 long_runs, c->stream);
-        ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
+        const double nn = c->n, ds = wide ? 4.0 : 2.0;
+        {   // every product's digits in (1 or 2 B), one sum per (limb, digit) out
+            ProfScope pd(c, PK_DIGIT_SUM, (u64)Bd, nn * gu * ((double)B * npairs * (in8 ? 1.0 : 2.0) + (double)Bd * ds));
+            ks32_digit_sum(c->d_dall, in8, npairs, c->d_term_start, c->d_terms, c->d_dk, wide, (int)B, (int)dout, (int)gu,
+                           c->n, c->stream);
+        }
+        {
+            ProfScope pn(c, PK_KS_DIGITS, (u64)Bd * gu * S, nn * Bd * gu * S * (ds + 4.0));
+            if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
+            else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
+        }
+        {
+            ProfScope pm(c, PK_KS_MAC, (u64)Bd * S, 4.0 * nn * Bd * S * (gu + 2.0 * c->L));
+            ks32_mac(c->d_dsk, use_wide ? c->kw.d_rs : c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, S, c->n, p32,
+                     long_runs, c->stream);
+        }
+        {
+            ProfScope pc(c, PK_KS_CRT, (u64)Bd * 2 * c->L, nn * Bd * 2 * c->L * (4.0 * S + 16.0));
+            ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
+        }
         CHECK_LAUNCH();
     }
     if (coef)
-        if (int e = run_ntt(c, contiguous(out, (long)B * d, 2L * c->L, 0, c->L, c->n), (long)B * d * 2 * c->L, false))
+        if (int e = run_ntt(c, contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n), (long)B * dout * 2 * c->L, false))
             return e;
     return 0;
 }
@@ -1810,6 +1910,36 @@ extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint6
     if (depth_out)
         for (size_t i = 0; i < B; ++i) depth_out[i] = 1;
     return 0;
+}
+
+// One GPU's share of a dbfv_mul whose output limbs are split across GPUs (dbfv/eval.rs:109-132): the
+// output limbs limbs[0..nlimbs) only, out = [B][nlimbs][2][L][n] (slot s = limb limbs[s]), each exactly
+// as exacto_dbfv_mul computes it (its pairs i + j = k, relinearised and summed, and the reduce
+// folding of the high limbs).  Distinct limbs need no cross-GPU sum: the caller gathers the slots.
+extern "C" int exacto_dbfv_mul_limbs_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                                         const uint64_t* b, uint64_t* out, size_t B, const uint32_t* limbs,
+                                         size_t nlimbs) {
+    if (int e = check_ctx(c)) return e;
+    if (int e = dbfv_params_check(d, base, plain)) return e;
+    if (nlimbs && !limbs) return invalid_param("null limb list");
+    std::vector<int> ls;
+    for (size_t s = 0; s < nlimbs; ++s) {
+        if (limbs[s] >= d) return invalid_param("output limb " + std::to_string(limbs[s]) + " >= d = " + std::to_string(d));
+        if (std::find(ls.begin(), ls.end(), (int)limbs[s]) != ls.end()) return invalid_param("repeated output limb");
+        ls.push_back((int)limbs[s]);
+    }
+    if (B == 0 || ls.empty()) return 0;
+    return dbfv_mul_core(c, d, base, plain, a, b, out, B, false, &ls);
+}
+
+extern "C" int exacto_dbfv_mul_limbs(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                                     const uint64_t* b, uint64_t* out, size_t B, const uint32_t* limbs, size_t nlimbs) {
+    if (!c) return invalid_param("null context");
+    const size_t ctb = B * d * 2 * c->L * poly_bytes(c);
+    return host_call(c, {{a, ctb}, {b, ctb}}, B * nlimbs * 2 * c->L * poly_bytes(c), out,
+                     [&](std::vector<u64*>& in, u64* o) {
+                         return exacto_dbfv_mul_limbs_dev(c, d, base, plain, in[0], in[1], o, B, limbs, nlimbs);
+                     });
 }
 
 // ============================================================== decryption
@@ -2989,6 +3119,134 @@ extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, dou
     if (total_ms) *total_ms = ms;
     if (total_bytes) *total_bytes = by;
     if (polys) *polys = np;
+    return 0;
+}
+
+// ============================================================== RCCL collectives
+//
+// Keys are made once and broadcast over xGMI to every GPU (the reference builds them on one host,
+// keygen.rs:123-209); the limbs of a split dbfv_mul are gathered (never summed: an RCCL sum of
+// residues would overflow mod q).  librccl is opened at first use (dlopen of librccl.so.1, or
+// EXACTO_RCCL_LIB), so a process that already loaded RCCL (torch) shares that instance and the
+// library has no link-time dependency on it.  Communicators are plain ncclComm_t handles, passed as
+// void*: made here (exacto_rccl_comm_init) or by the caller's own RCCL.
+
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+namespace {
+struct Rccl {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        const char* env = getenv("EXACTO_RCCL_LIB");
+        void* h = dlopen(env ? env : "librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) { x.why = std::string("cannot open RCCL: ") + dlerror(); return x; }
+        bool all = true;
+        auto sym = [&](auto& f, const char* name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            all &= f != nullptr;
+        };
+        sym(x.get_unique_id, "ncclGetUniqueId");
+        sym(x.comm_init_rank, "ncclCommInitRank");
+        sym(x.comm_destroy, "ncclCommDestroy");
+        sym(x.comm_count, "ncclCommCount");
+        sym(x.broadcast, "ncclBroadcast");
+        sym(x.all_gather, "ncclAllGather");
+        sym(x.error_string, "ncclGetErrorString");
+        x.ok = all;
+        if (!all) x.why = "RCCL library lacks a required symbol";
+        return x;
+    }();
+    return r;
+}
+}  // namespace
+
+#define RCCL_TRY(x)                                                                                      \
+    do {                                                                                                 \
+        const ncclResult_t r_ = (x);                                                                     \
+        if (r_ != ncclSuccess)                                                                           \
+            return fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(r_) + " (" #x ")"); \
+    } while (0)
+
+static int rccl_ready() {
+    if (!rccl().ok) return fail(EXACTO_ERR_HIP, "RCCL error: " + rccl().why);
+    return 0;
+}
+
+extern "C" int exacto_rccl_unique_id(uint8_t* id) {
+    if (!id) return invalid_param("null id buffer");
+    if (int e = rccl_ready()) return e;
+    ncclUniqueId u;
+    RCCL_TRY(rccl().get_unique_id(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+extern "C" int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id, int rank, int device) {
+    if (!comm || !id) return invalid_param("null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return invalid_param("rank out of range");
+    if (int e = rccl_ready()) return e;
+    HIP_TRY(hipSetDevice(device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t cm = nullptr;
+    RCCL_TRY(rccl().comm_init_rank(&cm, nranks, u, rank));
+    *comm = cm;
+    return 0;
+}
+
+extern "C" int exacto_rccl_comm_destroy(void* comm) {
+    if (!comm) return 0;
+    if (int e = rccl_ready()) return e;
+    RCCL_TRY(rccl().comm_destroy((ncclComm_t)comm));
+    return 0;
+}
+
+// In-place broadcast of `words` u64 at buf from root's buffer, enqueued on the context stream.
+static int rccl_bcast(exacto_ctx* c, void* comm, int root, u64* buf, size_t words) {
+    if (!comm) return invalid_param("null communicator");
+    if (int e = rccl_ready()) return e;
+    int nr = 0;
+    RCCL_TRY(rccl().comm_count((ncclComm_t)comm, &nr));
+    if (root < 0 || root >= nr) return invalid_param("root out of range");
+    if (!words) return 0;
+    RCCL_TRY(rccl().broadcast(buf, buf, words, ncclUint64, root, (ncclComm_t)comm, c->stream));
+    return 0;
+}
+
+extern "C" int exacto_ctx_broadcast_relin_key(exacto_ctx* c, void* comm, int root, size_t num_keys) {
+    if (int e = check_ctx(c)) return e;
+    // the root's resident key stays as loaded; every other rank's buffer is (re)sized first
+    u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
+    if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
+    return rccl_bcast(c, comm, root, dst, num_keys * 2 * c->L * (size_t)c->n);
+}
+
+extern "C" int exacto_broadcast_galois_key(exacto_ctx* c, void* comm, int root, uint64_t* gk, size_t num_keys) {
+    if (int e = check_ctx(c)) return e;
+    if (num_keys && !gk) return invalid_param("null Galois key");
+    return rccl_bcast(c, comm, root, gk, num_keys * 2 * c->L * (size_t)c->n);
+}
+
+extern "C" int exacto_rccl_allgather_u64(exacto_ctx* c, void* comm, const uint64_t* send, uint64_t* recv, size_t count) {
+    if (int e = check_ctx(c)) return e;
+    if (!comm) return invalid_param("null communicator");
+    if (count && (!send || !recv)) return invalid_param("null buffer");
+    if (int e = rccl_ready()) return e;
+    if (!count) return 0;
+    RCCL_TRY(rccl().all_gather(send, recv, count, ncclUint64, (ncclComm_t)comm, c->stream));
     return 0;
 }
 

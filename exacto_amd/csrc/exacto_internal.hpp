@@ -161,7 +161,11 @@ void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period,
 // p2only: every component of the ciphertext primes, the third only of the auxiliary primes (dBFV
 // psum; asm_inv and n = 4096 / 8192 only)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false);
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false,
+                       int part = -1);
+// psum (p2only) at this size runs as two launches (the ciphertext primes' three components, then the
+// auxiliary primes' third): launch_inv_tensor part 0 / part 1 time them apart
+bool inverse_tensor_split(int logn);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);
@@ -199,6 +203,8 @@ enum class PwOp : int { Add = 0, Sub = 1, Neg = 2, Mul = 3, ScalarMul = 4, Copy 
 void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys, int n, int L,
                       const u64* scalar_mod /*[L] or null*/, const PrimeConst* primes,
                       hipStream_t s);
+void launch_bfv_addsub(bool sub, const u64* a, int p1, const u64* b, int p2, u64* out, long items, int n, int L,
+                       const PrimeConst* primes, hipStream_t s);
 
 struct CombineTerm {
     int pair;      // product index inside the item

@@ -1167,6 +1167,37 @@ void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys,
                        scalar_mod, primes);
 }
 
+// bfv_add / bfv_sub of ciphertexts with p1 and p2 components (eval.rs:14-51): component i <
+// min(p1, p2) is a +/- b; beyond it the longer operand's component passes through, negated when
+// it is ct2's under subtraction.  ct1 [B][p1][L][n], ct2 [B][p2][L][n], out [B][max][L][n]; row =
+// (item * max + comp) * L + limb.  out may alias ct1 or ct2 only when its component count equals
+// that operand's (same strides).
+__global__ void __launch_bounds__(TPB)
+bfv_addsub_kernel(int sub, const u64* __restrict__ a, int p1, const u64* __restrict__ b, int p2,
+                  u64* __restrict__ out, int n, int L, const PrimeConst* __restrict__ primes) {
+    ROW_SETUP(n)
+    const int pm = p1 > p2 ? p1 : p2;
+    const int limb = (int)(row % L);
+    const long r1 = row / L;
+    const int comp = (int)(r1 % pm);
+    const long item = r1 / pm;
+    const u64 q = primes[limb].q;
+    const long ia = ((item * p1 + comp) * L + limb) * (long)n + j;
+    const long ib = ((item * p2 + comp) * L + limb) * (long)n + j;
+    u64 r;
+    if (comp < p1 && comp < p2) r = sub ? sub_mod(a[ia], b[ib], q) : add_mod(a[ia], b[ib], q);
+    else if (comp < p1) r = a[ia];
+    else r = sub ? neg_mod(b[ib], q) : b[ib];
+    out[row * n + j] = r;
+}
+
+void launch_bfv_addsub(bool sub, const u64* a, int p1, const u64* b, int p2, u64* out, long items, int n, int L,
+                       const PrimeConst* primes, hipStream_t s) {
+    const long blocks = items * (p1 > p2 ? p1 : p2) * L * blocks_per_row(n);
+    if (blocks == 0) return;
+    hipLaunchKernelGGL(bfv_addsub_kernel, dim3(blocks), dim3(TPB), 0, s, sub ? 1 : 0, a, p1, b, p2, out, n, L, primes);
+}
+
 // ---------------------------------------------------------------- dBFV combine
 
 __global__ void __launch_bounds__(TPB)

@@ -1352,25 +1352,33 @@ void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int n
                        terms, primes);
 }
 
+// one workgroup per (item, prime) at n = 8192 (cfg5 +1.6 % A/B); at n = 4096 the per-component
+// form at 3 waves per SIMD is faster (327 vs 335 us per cfg3 chunk).  EXACTO_TENSOR3=0/1 forces.
+static bool tensor3_at(int logn) {
+    static const int t3env = [] { const char* e = std::getenv("EXACTO_TENSOR3"); return e ? (e[0] == '1') : -1; }();
+    return t3env >= 0 ? t3env == 1 : logn == 13;
+}
+
+bool inverse_tensor_split(int logn) { return (logn == 12 || logn == 13) && tensor3_at(logn); }
+
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int part = -1) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
-    // one workgroup per (item, prime) at n = 8192 (cfg5 +1.6 % A/B); at n = 4096 the per-component
-    // form at 3 waves per SIMD is faster (327 vs 335 us per cfg3 chunk).  EXACTO_TENSOR3=0/1 forces.
-    static const int t3env = [] { const char* e = std::getenv("EXACTO_TENSOR3"); return e ? (e[0] == '1') : -1; }();
-    const bool t3 = t3env >= 0 ? t3env == 1 : LOGN == 13;
+    const bool t3 = tensor3_at(LOGN);
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv && t3) {
             // blocks = items * 3 (L + K); psum: the ciphertext primes here, the auxiliary c2 apart
             const long items = blocks / (3 * (L + K));
             if (p2only) {
-                hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * L), dim3(threads), 0, s, op, extP, T, L,
-                                   K, primes, L);
-                hipLaunchKernelGGL((ntt_inv_tensor_c2_kernel<LOGN>), dim3(items * K), dim3(threads), 0, s, op, T, L, K,
-                                   primes);
+                if (part != 1)
+                    hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * L), dim3(threads), 0, s, op, extP, T,
+                                       L, K, primes, L);
+                if (part != 0)
+                    hipLaunchKernelGGL((ntt_inv_tensor_c2_kernel<LOGN>), dim3(items * K), dim3(threads), 0, s, op, T, L,
+                                       K, primes);
             } else {
                 hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * (L + K)), dim3(threads), 0, s, op, extP, T,
                                    L, K, primes, L + K);
@@ -1393,12 +1401,12 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int part) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
-        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
-        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
+        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, part);
+        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, part);
         return;
     }
     switch (logn) {

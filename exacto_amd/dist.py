@@ -1,11 +1,16 @@
 """Multi-GPU layer: one process per GPU, batches sharded across ranks, keys broadcast.
 
 The path shards embarrassingly (every bfv_mul_and_relin / dbfv_mul in a batch is
-independent), so there is NO data-path collective: each rank owns a
-contiguous slice of the batch.  The only collective is the one-time RCCL broadcast of
-the relinearisation key over xGMI (2.25 MiB at cfg3/4, 15 MiB at cfg5).  Results can be
-gathered to one rank with ``gather_to`` (all_gather of equal-sized shards); an RCCL
-ncclSum would overflow mod q and is never used.
+independent), so batch sharding has NO data-path collective: each rank owns a
+contiguous slice of the batch.  The only collective there is the one-time broadcast of the
+relinearisation key over xGMI (2.25 MiB at cfg3/4, 15 MiB at cfg5), made by the library itself
+(``HipContext.broadcast_relin_key``: ncclBroadcast into the resident key) or by torch.distributed.
+
+One dbfv_mul can also be split across GPUs (north_star: "the d^2 digit-pair muls of a single
+dbfv_mul shard across the GPUs"): output limb k = sum over pairs (i, j) with i + j = k
+(dbfv/eval.rs:109-132), so assigning whole output limbs to ranks needs no cross-GPU sum
+(``limb_partition``); each rank computes its limbs (``HipContext.dbfv_mul_limbs_dev``) and
+``gather_limbs`` all-gathers them (never an RCCL sum, which would overflow mod q).
 """
 
 from __future__ import annotations
@@ -35,6 +40,18 @@ def load_key_everywhere(ctx, key: torch.Tensor, num_keys: int, src: int = 0):
     ctx.load_relin_key_dev(key, num_keys)
 
 
+def rccl_comm_for(ctx, device: int):
+    """An RCCL communicator of the library (exacto_rccl_comm_init) over the torch.distributed
+    group: rank 0's unique id is broadcast over the default group, every rank joins on ``device``."""
+    from exacto_amd._ffi import RcclComm, rccl_unique_id
+    world, rank = dist.get_world_size(), dist.get_rank()
+    uid = rccl_unique_id() if rank == 0 else bytes(128)
+    be = dist.get_backend()
+    t = torch.tensor(list(uid), dtype=torch.uint8, device=torch.device("cuda", device) if be == "nccl" else "cpu")
+    dist.broadcast(t, src=0)
+    return RcclComm(world, bytes(t.cpu().tolist()), rank, device)
+
+
 def max_over_ranks(value: float, device=None) -> float:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return value
@@ -44,15 +61,62 @@ def max_over_ranks(value: float, device=None) -> float:
 
 
 def gather_to(shard_out: torch.Tensor, total: int, dst: int = 0):
-    """Collect every rank's output shard on ``dst`` (returns the concatenation there, None elsewhere).
-    Shards are padded to the largest shard size for the collective."""
+    """Collect every rank's output shard on ``dst`` only (returns the concatenation there, None
+    elsewhere): a gather, so no other rank holds the whole batch.  Shards are padded to the largest
+    shard size for the collective."""
     world = dist.get_world_size()
     rank = dist.get_rank()
     maxc = shard(total, 0, world)[1]
     pad = torch.zeros((maxc,) + tuple(shard_out.shape[1:]), dtype=shard_out.dtype, device=shard_out.device)
     pad[: shard_out.shape[0]] = shard_out
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, parts, dst=dst)
     if rank != dst:
         return None
     return torch.cat([parts[r][: shard(total, r, world)[1]] for r in range(world)])
+
+
+def limb_products(d: int) -> list[int]:
+    """Products per output limb k < d of a dbfv_mul with all-zero small representatives (every
+    BASELINE dBFV config): the pairs (i, j) with i + j = k, i.e. k + 1 of them."""
+    return [k + 1 for k in range(d)]
+
+
+def limb_partition(d: int, world: int, weights=None) -> list[list[int]]:
+    """Output limbs of one dbfv_mul per rank, balanced by product count (longest-processing-time
+    greedy: heaviest limb first onto the least-loaded rank, ties to the lower rank).  Every limb
+    goes to exactly one rank; ranks beyond d limbs get none.  Deterministic, so every rank
+    computes the same partition without communicating."""
+    w = limb_products(d) if weights is None else list(weights)
+    load = [0] * world
+    parts: list[list[int]] = [[] for _ in range(world)]
+    for k in sorted(range(d), key=lambda k: (-w[k], k)):
+        r = min(range(world), key=lambda r: (load[r], r))
+        parts[r].append(k)
+        load[r] += w[k]
+    return [sorted(p) for p in parts]
+
+
+def gather_limbs(compact: torch.Tensor, parts: list[list[int]], d: int, out: torch.Tensor | None = None):
+    """All-gather every rank's output limbs and assemble them on every rank.
+
+    compact: this rank's limbs, ``[B][len(parts[rank])][...]`` (slot s = limb parts[rank][s]).
+    Returns ``[B][d][...]`` (written into ``out`` when given).  The collective moves each limb once
+    per receiving rank; limbs are concatenated, never summed."""
+    world = dist.get_world_size()
+    B = compact.shape[0]
+    tail = tuple(compact.shape[2:])
+    m = max(len(p) for p in parts)
+    if compact.shape[1] == m:
+        pad = compact.contiguous()
+    else:
+        pad = torch.zeros((B, m) + tail, dtype=compact.dtype, device=compact.device)
+        pad[:, : compact.shape[1]] = compact
+    got = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(got, pad)
+    if out is None:
+        out = torch.empty((B, d) + tail, dtype=compact.dtype, device=compact.device)
+    for r, ls in enumerate(parts):
+        if ls:
+            out[:, ls] = got[r][:, : len(ls)]
+    return out

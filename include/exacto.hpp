@@ -223,6 +223,44 @@ inline BfvCiphertext bfv_mul_and_relin(const BfvCiphertext& a, const BfvCipherte
     return bfv_mul_and_relin(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b}, rlk)[0];
 }
 
+// bfv_add / bfv_sub (eval.rs:14-51): each batch has one component count; the two counts may differ
+// (the longer operand's extra components pass through, ct2's negated under subtraction)
+namespace detail {
+inline std::vector<BfvCiphertext> addsub(bool sub, const std::vector<BfvCiphertext>& a,
+                                         const std::vector<BfvCiphertext>& b) {
+    if (a.empty()) return {};
+    if (a.size() != b.size()) throw ExactoError(1, "invalid parameter: batch sizes differ");
+    const BfvParamsPtr& prm = a[0].params;
+    const size_t p1 = a[0].c.size(), p2 = b[0].c.size(), pm = p1 > p2 ? p1 : p2;
+    auto fa = flatten(a, p1), fb = flatten(b, p2);
+    std::vector<uint64_t> out(a.size() * pm * prm->num_limbs() * prm->ring_degree);
+    check((sub ? exacto_bfv_sub : exacto_bfv_add)(prm->ctx(), fa.data(), p1, fb.data(), p2, out.data(), a.size()));
+    return unflatten(out, a.size(), pm, prm);
+}
+}  // namespace detail
+inline std::vector<BfvCiphertext> bfv_add(const std::vector<BfvCiphertext>& a, const std::vector<BfvCiphertext>& b) {
+    return detail::addsub(false, a, b);
+}
+inline std::vector<BfvCiphertext> bfv_sub(const std::vector<BfvCiphertext>& a, const std::vector<BfvCiphertext>& b) {
+    return detail::addsub(true, a, b);
+}
+inline std::vector<BfvCiphertext> bfv_neg(const std::vector<BfvCiphertext>& cts) {
+    if (cts.empty()) return {};
+    const BfvParamsPtr& prm = cts[0].params;
+    const size_t polys = cts[0].c.size();
+    auto f = detail::flatten(cts, polys);
+    std::vector<uint64_t> out(f.size());
+    detail::check(exacto_bfv_neg(prm->ctx(), f.data(), polys, out.data(), cts.size()));
+    return detail::unflatten(out, cts.size(), polys, prm);
+}
+inline BfvCiphertext bfv_add(const BfvCiphertext& a, const BfvCiphertext& b) {
+    return bfv_add(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b})[0];
+}
+inline BfvCiphertext bfv_sub(const BfvCiphertext& a, const BfvCiphertext& b) {
+    return bfv_sub(std::vector<BfvCiphertext>{a}, std::vector<BfvCiphertext>{b})[0];
+}
+inline BfvCiphertext bfv_neg(const BfvCiphertext& ct) { return bfv_neg(std::vector<BfvCiphertext>{ct})[0]; }
+
 // decrypt (src/bfv/encrypt.rs:111-178), batched over ciphertexts of one degree.
 inline std::vector<CoeffPoly> decrypt(const std::vector<BfvCiphertext>& cts, const SecretKey& sk) {
     if (cts.empty()) return {};

@@ -134,10 +134,21 @@ int exacto_rns_mul_inv_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b
 int exacto_rns_polymul_dev(exacto_ctx* ctx, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t count);
 
 /* ---- BFV ciphertext ops (bfv/eval.rs).  Degree-1 ct batches [B][2][L][n]. ---- */
-/* bfv_add / bfv_sub / bfv_neg (eval.rs:14-60) on equal-degree ciphertexts of `polys` polys. */
-int exacto_bfv_add_dev(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, size_t batch, size_t polys);
-int exacto_bfv_sub_dev(exacto_ctx* ctx, const uint64_t* ct1, const uint64_t* ct2, uint64_t* out, size_t batch, size_t polys);
-int exacto_bfv_neg_dev(exacto_ctx* ctx, const uint64_t* ct, uint64_t* out, size_t batch, size_t polys);
+/* bfv_add / bfv_sub / bfv_neg (eval.rs:14-60), batched.  ct1 = [B][polys1][L][n], ct2 =
+ * [B][polys2][L][n] -> out = [B][max(polys1, polys2)][L][n]: component i < min is the pointwise
+ * sum / difference; the longer operand's further components pass through (eval.rs:21-22), negated
+ * when they are ct2's under subtraction (eval.rs:41-42).  out may alias an input only when that
+ * input has max(polys1, polys2) components. */
+int exacto_bfv_add(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2, size_t polys2,
+                   uint64_t* out, size_t batch);
+int exacto_bfv_add_dev(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2, size_t polys2,
+                       uint64_t* out, size_t batch);
+int exacto_bfv_sub(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2, size_t polys2,
+                   uint64_t* out, size_t batch);
+int exacto_bfv_sub_dev(exacto_ctx* ctx, const uint64_t* ct1, size_t polys1, const uint64_t* ct2, size_t polys2,
+                       uint64_t* out, size_t batch);
+int exacto_bfv_neg(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
+int exacto_bfv_neg_dev(exacto_ctx* ctx, const uint64_t* ct, size_t polys, uint64_t* out, size_t batch);
 
 /* bfv_mul_no_relin (eval.rs:89-108): out = [B][3][L][n].  `polys1`/`polys2` are the
  * input ciphertexts' component counts (must be 2: "multiplication requires degree-1
@@ -178,6 +189,19 @@ int exacto_dbfv_mul(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plai
 int exacto_dbfv_mul_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
                         const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch,
                         const uint32_t* depth_a, const uint32_t* depth_b, uint32_t* depth_out);
+
+/* One GPU's share of a dbfv_mul whose d output limbs are split across GPUs (the d^2 digit-pair
+ * products of dbfv/eval.rs:109-122 partitioned by output limb k = i + j, so no cross-GPU sum is
+ * needed): only the output limbs limbs[0..nlimbs) (host array, distinct, < d) are computed, out =
+ * [B][nlimbs][2][L][n] with slot s holding limb limbs[s] exactly as exacto_dbfv_mul computes it
+ * (including the reduce folding of limbs >= d, reduction.rs:34-52).  The caller gathers the slots of
+ * all GPUs (exacto_rccl_allgather_u64) into [B][d][2][L][n].  Inputs at mul_depth 0. */
+int exacto_dbfv_mul_limbs(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                          const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch, const uint32_t* limbs,
+                          size_t nlimbs);
+int exacto_dbfv_mul_limbs_dev(exacto_ctx* ctx, size_t d, uint64_t base, uint64_t dbfv_plain_modulus,
+                              const uint64_t* a, const uint64_t* b, uint64_t* out, size_t batch, const uint32_t* limbs,
+                              size_t nlimbs);
 
 /* dBFV multiplication chain, device-resident (paper_repro.rs:203-236 guard-bypass semantics;
  * bfv_host.rs:258-288 without the bootstrap): out = (((x*y)*y)...*y), `depth` dbfv_mul steps,
@@ -350,6 +374,27 @@ int exacto_bfv_bootstrap_dev(exacto_ctx* orig, exacto_ctx* boot, const uint64_t*
                              const uint64_t* bsk, const uint64_t* rpoly, size_t m, uint64_t q_prime,
                              const uint64_t* elements, size_t E, const uint64_t* gks, size_t num_keys, uint64_t* out,
                              size_t batch);
+
+/* ---- RCCL collectives over xGMI ----
+ * Replace the host-side key distribution of the reference (keys built once, keygen.rs:123-209, and
+ * shared by every rayon worker) with one broadcast per key to every GPU, and gather the output limbs
+ * of a split dbfv_mul.  `comm` is an ncclComm_t (RCCL), as void*: made by exacto_rccl_comm_init or by
+ * the caller's own RCCL.  RCCL is opened at first use (librccl.so.1, or $EXACTO_RCCL_LIB); failures
+ * return EXACTO_ERR_HIP with an "RCCL error: ..." message.  All collectives are enqueued on the
+ * context's stream.
+ *   exacto_rccl_unique_id      ncclGetUniqueId -> id[128] (rank 0; share it out of band)
+ *   exacto_rccl_comm_init      ncclCommInitRank on `device`
+ *   exacto_ctx_broadcast_relin_key   root's resident relinearisation key -> every rank's resident key
+ *                              (in place; non-root ranks need no prior load), num_keys = [G] rows
+ *   exacto_broadcast_galois_key      a device Galois key buffer [num_keys][2][L][n], in place
+ *   exacto_rccl_allgather_u64  recv = [nranks][count] u64 (never a reduction: residues are not summable
+ *                              by RCCL) */
+int exacto_rccl_unique_id(uint8_t* id);
+int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id, int rank, int device);
+int exacto_rccl_comm_destroy(void* comm);
+int exacto_ctx_broadcast_relin_key(exacto_ctx* ctx, void* comm, int root, size_t num_keys);
+int exacto_broadcast_galois_key(exacto_ctx* ctx, void* comm, int root, uint64_t* gk_dev, size_t num_keys);
+int exacto_rccl_allgather_u64(exacto_ctx* ctx, void* comm, const uint64_t* send, uint64_t* recv, size_t count);
 
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read

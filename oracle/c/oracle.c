@@ -23,6 +23,7 @@ typedef uint64_t u64;
 typedef uint32_t u32;
 typedef unsigned __int128 u128;
 typedef __int128 i128;
+typedef int64_t i64;
 
 #define MAXL 8
 #define MAXW 20 /* multiword accumulator words */
@@ -526,6 +527,53 @@ static void mul_hps(const octx_t* c, const u64* ct1, const u64* ct2, u64* r /* [
 
 /* ------------------------------------------------------------------ public entry points */
 
+/* One product (eval.rs:73-108 + keyswitch.rs:59-101): ct1, ct2 = [2][L][n] -> o = [2][L][n] (relin)
+ * or [3][L][n], NTT domain. */
+static void bfv_mul_one(const octx_t* c, int hps, const u64* ct1, const u64* ct2, const u64* rlk, int guse,
+                        int relin, u64* o) {
+    const int n = c->n, L = c->L, G = c->G;
+    u64* r = (u64*)malloc(sizeof(u64) * 3 * L * n);
+    if (hps) mul_hps(c, ct1, ct2, r);
+    else mul_generic(c, ct1, ct2, r);
+    if (!relin) {
+        memcpy(o, r, sizeof(u64) * 3 * L * n);
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < L; ++i) ntt_fwd(&c->plan[i], o + ((size_t)k * L + i) * n);
+    } else {
+        memcpy(o, r, sizeof(u64) * 2 * L * n);
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < L; ++i) ntt_fwd(&c->plan[i], o + ((size_t)k * L + i) * n);
+        /* relinearize: c2 coefficients -> CRT -> centred -> digits (keyswitch.rs:76-95) */
+        u64* dig = (u64*)malloc(sizeof(u64) * (size_t)(G > 0 ? G : 1) * L * n);
+        for (int j = 0; j < n; ++j) {
+            u64 res[MAXL], x[MAXL], mg[MAXL], dj[64 * MAXL];
+            int neg;
+            for (int i = 0; i < L; ++i) res[i] = r[((size_t)2 * L + i) * n + j];
+            if (L == 1) memcpy(x, res, sizeof(u64));
+            else crt(c, res, x);
+            centre(c, x, mg, &neg);
+            gadget(c, mg, neg, guse, dj);
+            for (int g = 0; g < guse; ++g)
+                for (int i = 0; i < L; ++i) dig[((size_t)g * L + i) * n + j] = dj[g * L + i];
+        }
+        for (int g = 0; g < guse; ++g)
+            for (int i = 0; i < L; ++i) {
+                u64* d = dig + ((size_t)g * L + i) * n;
+                ntt_fwd(&c->plan[i], d);
+                const u64* k0 = rlk + (((size_t)g * 2 + 0) * L + i) * n;
+                const u64* k1 = rlk + (((size_t)g * 2 + 1) * L + i) * n;
+                u64* o0 = o + (size_t)i * n;
+                u64* o1 = o + ((size_t)L + i) * n;
+                for (int j = 0; j < n; ++j) {
+                    o0[j] = (o0[j] + mulmod(d[j], k0[j], c->q[i])) % c->q[i];
+                    o1[j] = (o1[j] + mulmod(d[j], k1[j], c->q[i])) % c->q[i];
+                }
+            }
+        free(dig);
+    }
+    free(r);
+}
+
 /* ct1, ct2 = [B][2][L][n]; rlk = [nkeys][2][L][n]; out = [B][2][L][n] (relin) or [B][3][L][n] */
 int oracle_bfv_mul(int n, int L, const u64* q, int K, const u64* aux, u64 plain, u64 gbase, int G,
                    const u64* ct1, const u64* ct2, const u64* rlk, int nkeys, u64* out, int B, int relin,
@@ -540,50 +588,79 @@ int oracle_bfv_mul(int n, int L, const u64* q, int K, const u64* aux, u64 plain,
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
-    for (int b = 0; b < B; ++b) {
-        u64* r = (u64*)malloc(sizeof(u64) * 3 * L * n);
-        if (hps) mul_hps(&c, ct1 + b * ctw, ct2 + b * ctw, r);
-        else mul_generic(&c, ct1 + b * ctw, ct2 + b * ctw, r);
-        if (!relin) {
-            u64* o = out + (size_t)b * 3 * L * n;
-            memcpy(o, r, sizeof(u64) * 3 * L * n);
-            for (int k = 0; k < 3; ++k)
-                for (int i = 0; i < L; ++i) ntt_fwd(&c.plan[i], o + ((size_t)k * L + i) * n);
-        } else {
-            u64* o = out + (size_t)b * 2 * L * n;
-            memcpy(o, r, sizeof(u64) * 2 * L * n);
-            for (int k = 0; k < 2; ++k)
-                for (int i = 0; i < L; ++i) ntt_fwd(&c.plan[i], o + ((size_t)k * L + i) * n);
-            /* relinearize: c2 coefficients -> CRT -> centred -> digits (keyswitch.rs:76-95) */
-            u64* dig = (u64*)malloc(sizeof(u64) * (size_t)(G > 0 ? G : 1) * L * n);
-            for (int j = 0; j < n; ++j) {
-                u64 res[MAXL], x[MAXL], mg[MAXL], dj[64 * MAXL];
-                int neg;
-                for (int i = 0; i < L; ++i) res[i] = r[((size_t)2 * L + i) * n + j];
-                if (L == 1) memcpy(x, res, sizeof(u64));
-                else crt(&c, res, x);
-                centre(&c, x, mg, &neg);
-                gadget(&c, mg, neg, guse, dj);
-                for (int g = 0; g < guse; ++g)
-                    for (int i = 0; i < L; ++i) dig[((size_t)g * L + i) * n + j] = dj[g * L + i];
-            }
-            for (int g = 0; g < guse; ++g)
-                for (int i = 0; i < L; ++i) {
-                    u64* d = dig + ((size_t)g * L + i) * n;
-                    ntt_fwd(&c.plan[i], d);
-                    const u64* k0 = rlk + (((size_t)g * 2 + 0) * L + i) * n;
-                    const u64* k1 = rlk + (((size_t)g * 2 + 1) * L + i) * n;
-                    u64* o0 = o + (size_t)i * n;
-                    u64* o1 = o + ((size_t)L + i) * n;
-                    for (int j = 0; j < n; ++j) {
-                        o0[j] = (o0[j] + mulmod(d[j], k0[j], c.q[i])) % c.q[i];
-                        o1[j] = (o1[j] + mulmod(d[j], k1[j], c.q[i])) % c.q[i];
+    for (int b = 0; b < B; ++b)
+        bfv_mul_one(&c, hps, ct1 + b * ctw, ct2 + b * ctw, rlk, guse, relin, out + (size_t)b * (relin ? 2 : 3) * L * n);
+    octx_free(&c);
+    return 0;
+}
+
+/* dbfv_mul (dbfv/eval.rs:82-149) + reduce (reduction.rs:15-93) of B item pairs a, b = [B][d][2][L][n]
+ * -> out [B][d][2][L][n], literally: ALL d^2 products bfv_mul_and_relin(a_i, b_j) in parallel over
+ * (item, i, j) (the reference's rayon par_iter, eval.rs:117-122), summed per k = i + j in order
+ * (eval.rs:124-132), then limbs j >= d folded into limbs i < d with the small representatives of
+ * base^j mod p (lattice.rs:104-122; p = 0 is 2^64 by wrapping_pow), scaled by |coef| (NTT-domain
+ * scalar_mul) and negated for coef < 0 (reduction.rs:65-93).  Depth guard: the caller's. */
+int oracle_dbfv_mul(int n, int L, const u64* q, u64 plain, u64 gbase, int G, int d, u64 base, u64 dplain,
+                    const u64* a, const u64* b, const u64* rlk, int nkeys, u64* out, int B, int threads) {
+    if (L > MAXL || L < 1 || d < 1) return 1;
+    octx_t c;
+    octx_init(&c, n, L, q, 0, NULL, plain, gbase, G);
+    const size_t ctw = (size_t)2 * L * n;
+    const int guse = G < nkeys ? G : nkeys;
+    const int R = 2 * d - 1;
+    u64* prod = (u64*)malloc(sizeof(u64) * (size_t)B * d * d * ctw);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (long w = 0; w < (long)B * d * d; ++w) {
+        const long item = w / (d * d);
+        const int i = (int)(w % (d * d)) / d, j = (int)(w % d);
+        bfv_mul_one(&c, 0, a + ((size_t)item * d + i) * ctw, b + ((size_t)item * d + j) * ctw, rlk, guse, 1,
+                    prod + (size_t)w * ctw);
+    }
+    u64* limbs = (u64*)calloc((size_t)R * ctw, sizeof(u64));
+    for (int item = 0; item < B; ++item) {
+        memset(limbs, 0, sizeof(u64) * (size_t)R * ctw);
+        for (int i = 0; i < d; ++i)
+            for (int j = 0; j < d; ++j) {
+                const u64* p = prod + (((size_t)item * d + i) * d + j) * ctw;
+                u64* l = limbs + (size_t)(i + j) * ctw;
+                for (int t = 0; t < 2 * L; ++t) {
+                    const u64 qm = c.q[t % L];
+                    for (int x = 0; x < n; ++x) {
+                        const u64 v = l[(size_t)t * n + x] + p[(size_t)t * n + x];
+                        l[(size_t)t * n + x] = v >= qm ? v - qm : v;
                     }
                 }
-            free(dig);
+            }
+        /* reduce: reps_j = base-b digits of (base^j mod p), j = d .. 2d-2 */
+        for (int jj = d; jj < R; ++jj) {
+            u64 val = 1;
+            if (dplain == 0) for (int e = 0; e < jj; ++e) val *= base;
+            else val = powmod(base, (u64)jj, dplain);
+            for (int i = 0; i < d; ++i) {
+                const i64 coef = (i64)(val % base);
+                val /= base;
+                if (coef == 0) continue;
+                const u64 mag = (u64)(coef < 0 ? -coef : coef);
+                const u64* src = limbs + (size_t)jj * ctw;
+                u64* dst = limbs + (size_t)i * ctw;
+                for (int t = 0; t < 2 * L; ++t) {
+                    const u64 qm = c.q[t % L];
+                    for (int x = 0; x < n; ++x) {
+                        u64 s = mulmod(src[(size_t)t * n + x], mag % qm, qm);
+                        if (coef < 0 && s) s = qm - s;
+                        const u64 v = dst[(size_t)t * n + x] + s;
+                        dst[(size_t)t * n + x] = v >= qm ? v - qm : v;
+                    }
+                }
+            }
         }
-        free(r);
+        memcpy(out + (size_t)item * d * ctw, limbs, sizeof(u64) * (size_t)d * ctw);
     }
+    free(limbs);
+    free(prod);
     octx_free(&c);
     return 0;
 }

@@ -28,6 +28,8 @@ def _load():
         lib.oracle_bfv_mul.restype = I
         lib.oracle_ntt.argtypes = [I, U, P, I, I, I]
         lib.oracle_ntt.restype = I
+        lib.oracle_dbfv_mul.argtypes = [I, I, P, U, U, I, I, U, U, P, P, P, I, P, I, I]
+        lib.oracle_dbfv_mul.restype = I
         _lib = lib
     return _lib
 
@@ -59,6 +61,23 @@ def bfv_mul(params, ct1, ct2, rlk=None, relin=True, threads=1):
 
 def bfv_mul_and_relin(params, ct1, ct2, rlk, threads=1):
     return bfv_mul(params, ct1, ct2, rlk, True, threads)
+
+
+def dbfv_mul(dparams, a, b, rlk, threads=1):
+    """dbfv_mul + reduce (dbfv/eval.rs:82-149, reduction.rs:15-93) of batches a, b = [B][d][2][L][n]
+    (NTT domain), all d^2 products, depth guard left to the caller (paper_repro's chains reset it)."""
+    lib = _load()
+    prm = dparams.bfv_params
+    a, b, rlk = _u64(a), _u64(b), _u64(rlk)
+    B, d, _, L, n = a.shape
+    q = _u64(prm.ct_basis.moduli)
+    out = np.zeros_like(a)
+    rc = lib.oracle_dbfv_mul(n, L, q.ctypes.data, prm.plain_modulus, prm.gadget_base, prm.gadget_digits, d,
+                             dparams.base, dparams.plain_modulus, a.ctypes.data, b.ctypes.data,
+                             rlk.ctypes.data if rlk.size else None, rlk.shape[0], out.ctypes.data, B, threads)
+    if rc != 0:
+        raise ValueError("oracle_dbfv_mul: unsupported parameters")
+    return out
 
 
 def ntt(n, q, polys, inverse=False, threads=1):

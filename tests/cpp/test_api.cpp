@@ -186,6 +186,15 @@ static int keygen_case() {
     auto c3 = encrypt_sk_with_rng(encode_scalar(3, prm), sk, prm, rng);
     auto c7 = encrypt_pk_with_rng(encode_scalar(7, prm), pk, prm, rng);
     if (decode_scalar(decrypt(bfv_mul_and_relin(c3, c7, rlk), sk)) != 21) return 23;
+    // eval.rs:14-60: add / sub / neg, equal and mixed degrees (degree-2 product + degree-1 ct)
+    if (decode_scalar(decrypt(bfv_add(c3, c7), sk)) != 10) return 25;
+    if (decode_scalar(decrypt(bfv_sub(c3, c7), sk)) != 257 - 4) return 26;
+    if (decode_scalar(decrypt(bfv_neg(c3), sk)) != 257 - 3) return 27;
+    auto c21 = bfv_mul_no_relin(c3, c7);
+    auto mixed = bfv_add(c21, c3);
+    if (mixed.c.size() != 3 || decode_scalar(decrypt(mixed, sk)) != 24) return 28;
+    auto mixed2 = bfv_sub(c3, c21);
+    if (mixed2.c.size() != 3 || decode_scalar(decrypt(mixed2, sk)) != 257 - 18) return 29;
     // eval.rs:954-976: sigma_3(1 + 2X) = 1 + 2X^3
     CoeffPoly m;
     m.coeffs.assign(prm->ring_degree, 0);

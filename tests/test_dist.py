@@ -64,3 +64,91 @@ def test_gloo_world2_broadcast_shard_gather():
     assert all(p.exitcode == 0 for p in procs)
     for rank, ok_key, ok_gather, t in res:
         assert ok_key and ok_gather and t == 2.0
+
+
+# ---------------------------------------------------------------- one dbfv_mul split by output limb
+
+from exacto_amd.dist import gather_limbs, limb_partition, limb_products  # noqa: E402
+
+
+def test_limb_partition_covers_and_balances():
+    for d in (1, 2, 3, 8):
+        for world in (1, 2, 3, 4, 8, 16):
+            parts = limb_partition(d, world)
+            assert len(parts) == world
+            assert sorted(k for p in parts for k in p) == list(range(d))
+            loads = [sum(limb_products(d)[k] for k in p) for p in parts]
+            # LPT bound: no rank above the mean by more than the heaviest limb
+            assert max(loads) <= sum(loads) / world + d
+    assert limb_partition(8, 2) == [[0, 3, 4, 7], [1, 2, 5, 6]]   # 18 + 18 of cfg5's 36 products
+    assert limb_partition(2, 2) == [[1], [0]]                     # cfg4: 2 products / 1 product
+
+
+def _limb_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        d, B = 5, 3
+        parts = limb_partition(d, world)
+        full = torch.arange(B * d * 4, dtype=torch.int64).reshape(B, d, 4)   # "limb k of item b"
+        mine = parts[rank]
+        compact = full[:, mine].clone()                                    # this rank's computed limbs
+        out = gather_limbs(compact, parts, d)
+        q.put((rank, bool(torch.equal(out, full))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_limbs(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_limb_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res)
+
+
+# ---------------------------------------------------------------- bench.py's own launcher, sharding and timing
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=ROOT)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r
+
+
+def test_bench_dry_gpus2_relaunches_torchrun():
+    rc, line, r = _bench("--gpus", "2", "--dry", "--config", "cfg3", "--batch", "4", "--steps", "2", "--warmup", "1",
+                         "--min-time", "0.1")
+    assert rc == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    assert line["scaling"] == "weak" and line["config"]["global_batch"] == 8 and line["dry"] is True
+
+
+def test_bench_dry_gpus2_limb_split_gathers_every_limb():
+    rc, line, r = _bench("--gpus", "2", "--dry", "--config", "cfg5", "--split", "limbs", "--batch", "2",
+                         "--steps", "2", "--warmup", "1", "--min-time", "0.1")
+    assert rc == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["dry_gather_ok"] is True
+    assert "[[0, 3, 4, 7], [1, 2, 5, 6]]" in line["config"]["parallelism"]
+
+
+def test_bench_world_size_mismatch_exits_nonzero():
+    rc, line, _ = _bench("--gpus", "2", "--dry", env_extra={"WORLD_SIZE": "1"})
+    assert rc != 0 and line is None

@@ -315,3 +315,27 @@ def test_monomial_mul_poly_kat():
     assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 3, 4).coeffs == [15, 14, 0, 1]
     assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 4, 4).coeffs == [16, 15, 14, 0]
     assert obfv.monomial_mul_poly(CoeffPoly([1, 2, 3, 0], 17), 8, 4).coeffs == [1, 2, 3, 0]
+
+
+@pytest.mark.parametrize("base,d,p", [(256, 2, 65536), (7, 4, 1000)])
+def test_c_dbfv_mul_matches_python(base, d, p):
+    """oracle/c oracle_dbfv_mul (all d^2 products, per-limb sums, reduce with reps) == the Python
+    restatement (dbfv/eval.rs:82-149, reduction.rs:15-93); (7, 4, 1000) has non-zero reps."""
+    if not cref.available():
+        pytest.skip("oracle/c not built")
+    from bridge import np_to_ct, ct_to_np, np_to_rlk, uniform_residues
+    n = 16
+    prm = P.BfvParamsBuilder().ring_degree(n).plain_modulus(1009).ct_moduli(P.Q3).build()
+    dp = P.DbfvParams(prm, base, d, p)
+    rng = np.random.default_rng(5)
+    q = prm.ct_basis.moduli
+    a = uniform_residues(rng, (2, d, 2), q, n)
+    b = uniform_residues(rng, (2, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    got = cref.dbfv_mul(dp, a, b, rlk, threads=2)
+    rk = np_to_rlk(rlk, prm)
+    for it in range(2):
+        ca = odbfv.DbfvCiphertext([np_to_ct(a[it, i], prm) for i in range(d)], d, 0, dp)
+        cb = odbfv.DbfvCiphertext([np_to_ct(b[it, i], prm) for i in range(d)], d, 0, dp)
+        want = np.stack([ct_to_np(l) for l in odbfv.dbfv_mul(ca, cb, rk).limbs])
+        assert np.array_equal(got[it], want)
