@@ -312,6 +312,10 @@ struct exacto_ctx {
     int* d_term_start = nullptr;
     CombineTerm* d_terms = nullptr;
     size_t terms_cap = 0;
+    // per-call scratch: the context's own stream-ordered pool (Scratch)
+    hipMemPool_t pool = nullptr;
+    bool debug_scratch = false;
+    size_t dbfv_group_bytes = (size_t)4096 << 20;   // dbfv_mul item groups (EXACTO_DBFV_GROUP_MB)
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -321,15 +325,13 @@ static void free_dev(void* p) {
     if (p) (void)hipFree(p);
 }
 
-// Per-call scratch from the stream-ordered pool (hipMallocAsync / hipFreeAsync on the stream that
-// uses it; no device-wide synchronisation).  EXACTO_DEBUG_SCRATCH=1 fills every block with 0xFF
-// when it is handed out, so a kernel that reads scratch it never wrote gives wrong results at once
-// instead of whatever the previous owner of the block left there.
-static const bool g_debug_scratch = [] {
-    const char* e = getenv("EXACTO_DEBUG_SCRATCH");
-    return e && atoi(e) != 0;
-}();
-
+// Per-call scratch from the context's own stream-ordered pool (hipMallocFromPoolAsync / hipFreeAsync
+// on the stream that uses it; no device-wide synchronisation).  The pool belongs to the context
+// (hipMemPoolCreate), so its release threshold -- freed blocks stay mapped for the next call -- does
+// not change the device's default pool that other libraries in the process use.
+// EXACTO_DEBUG_SCRATCH=1 (read when a context is created) fills every block with 0xFF when it is
+// handed out, so a kernel that reads scratch it never wrote gives wrong results at once instead of
+// whatever the previous owner of the block left there.
 struct Scratch {
     void* p = nullptr;
     hipStream_t s = nullptr;
@@ -339,10 +341,11 @@ struct Scratch {
     ~Scratch() {
         if (p) (void)hipFreeAsync(p, s);
     }
-    hipError_t alloc(size_t bytes, hipStream_t st) {
+    hipError_t alloc(size_t bytes, hipStream_t st, hipMemPool_t pool, bool debug) {
         s = st;
-        hipError_t e = hipMallocAsync(&p, std::max<size_t>(bytes, 8), st);
-        if (e == hipSuccess && g_debug_scratch) e = hipMemsetAsync(p, 0xFF, std::max<size_t>(bytes, 8), st);
+        hipError_t e = pool ? hipMallocFromPoolAsync(&p, std::max<size_t>(bytes, 8), pool, st)
+                            : hipMallocAsync(&p, std::max<size_t>(bytes, 8), st);
+        if (e == hipSuccess && debug) e = hipMemsetAsync(p, 0xFF, std::max<size_t>(bytes, 8), st);
         return e;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }
@@ -414,7 +417,7 @@ static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
 // 2^30) with prod p > `bound`, its twiddles, constants and Garner tables on the device.  sum_max:
 // how many key-switch sums (dBFV products of one output limb) the basis lifts exactly when they
 // are added first.  S = 0 when no basis of at most EXACTO_KS32_MAXS primes exists.
-static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
+static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
     b->S = 0;
     std::vector<u64> ps;
     Big P(1);
@@ -507,6 +510,19 @@ static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound,
     return 0;
 }
 
+static void free_basis(Ks32Basis* b) {
+    free_dev(b->d_p32); free_dev(b->d_tw32); free_dev(b->d_kst); free_dev(b->d_rs);
+    *b = Ks32Basis{};
+}
+
+// build_ks32_basis_impl, releasing whatever it allocated when a later step fails (the basis is not
+// attached to the context yet, so exacto_ctx_destroy would not free it)
+static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
+    const int e = build_ks32_basis_impl(c, pmax, qmax, bound, b);
+    if (e) free_basis(b);
+    return e;
+}
+
 // ks32.hip's auxiliary bases, bounding |sum_g d_g * r_g| <= G n floor(B/2) floor(q_max/2) (digits
 // balanced in [-B/2, B/2), key coefficients balanced).  Eligible: exact path, gadget base <= 2^16
 // (int16 digits), every ciphertext prime 2^60 - d with d < 2^24 (ks32_crt reduces with
@@ -536,13 +552,15 @@ static int setup_ks32(exacto_ctx* c) {
     Ks32Basis prim;
     if (int e = build_ks32_basis(c, wide_mode == 2 ? (1ull << 31) : (1ull << 32) / 3, qmax, bound, &prim)) return e;
     if (wide_mode == 1) {
-        if (int e = build_ks32_basis(c, 1ull << 31, qmax, bound, &c->kw)) return e;
+        if (int e = build_ks32_basis(c, 1ull << 31, qmax, bound, &c->kw)) {
+            free_basis(&prim);
+            return e;
+        }
         if (prim.S == 0 && c->kw.S > 0) {   // only the wide range holds the bound: it is the primary
             prim = c->kw;
             c->kw = Ks32Basis{};
         } else if (c->kw.S > 0 && c->kw.sum_max <= prim.sum_max) {
-            free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst);
-            c->kw = Ks32Basis{};
+            free_basis(&c->kw);
         }
     }
     if (prim.S == 0) return 0;
@@ -776,17 +794,25 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
     c->own_stream = true;
     {
-        // Per-call scratch (Scratch) comes from the device's default stream-ordered pool.  Keep its
-        // freed blocks mapped for reuse instead of returning them to the driver at every
-        // synchronisation (release threshold 0, the default): no map/unmap per call, and on this
-        // ROCm 7.2 stack blocks re-acquired after such a release gave wrong results at n = 16
-        // ("Scratch"), which keeping them mapped avoids.
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        // Per-call scratch (Scratch) comes from a stream-ordered pool of the context's own.  Its freed
+        // blocks stay mapped for reuse instead of going back to the driver at every synchronisation
+        // (release threshold 0 is the default): no map/unmap per call, and on this ROCm 7.2 stack
+        // blocks re-acquired after such a release gave wrong results at n = 16 (DESIGN.md §3,
+        // "Scratch"), which keeping them mapped avoids.  Only this pool is configured; the device's
+        // default pool keeps its settings for everything else in the process.
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = device;
+        if (hipMemPoolCreate(&c->pool, &props) == hipSuccess) {
             uint64_t thr = ~0ull;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr);
+        } else {
+            c->pool = nullptr;   // Scratch falls back to the device's default pool
         }
     }
+    if (const char* e = getenv("EXACTO_DEBUG_SCRATCH")) c->debug_scratch = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_DBFV_GROUP_MB")) c->dbfv_group_bytes = (size_t)std::max(1, atoi(e)) << 20;
     if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
@@ -827,6 +853,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->pool) (void)hipMemPoolDestroy(c->pool);
     delete c;
 }
 
@@ -1107,7 +1134,7 @@ static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t
     if (grow((u64**)dst, cap, std::max<size_t>((size_t)rows * S * c->n * sizeof(uint32_t), 8)))
         return EXACTO_ERR_HIP;
     Scratch ks;
-    HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream));
+    HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream, c->pool, c->debug_scratch));
     NttBatch nb{};
     nb.src = key; nb.src_item_stride = 2L * c->L * c->n;
     nb.dst = ks.as<u64>(); nb.dst_item_stride = 2L * c->L * c->n;
@@ -1184,7 +1211,9 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     if (skip_fwd) *coef = true;
     if (relin && guse > 0) {
         // both before the second lane forks: its kernels read these too
-        if (int e = k32 ? ensure_rs(c) : ensure_rlk_companions(c)) return e;
+        // (a deferred key switch -- dbfv_mul_core's digit sums -- has already made the key for the basis
+        // it uses, which may be the wide one: the primary form would be built and never read)
+        if (int e = k32 ? (c->ks_defer ? 0 : ensure_rs(c)) : ensure_rlk_companions(c)) return e;
     }
     // two chunks or more: odd chunks on the second lane (profiling keeps one lane so its per-kernel
     // events time each kernel alone)
@@ -1347,7 +1376,10 @@ static int check_ctx(exacto_ctx* c) {
 static int ntt_dev(exacto_ctx* c, uint64_t* polys, size_t count, size_t limb, bool inverse) {
     if (int e = check_ctx(c)) return e;
     if (limb >= (size_t)c->L)
-        return fail(EXACTO_ERR_DIMENSION_MISMATCH, "dimension mismatch: expected limb < " + std::to_string(c->L) + ", got " + std::to_string(limb));
+        // the reference's Display text ("expected {expected}, got {got}", error.rs:8-9): the context's
+        // limb count and the limb index asked for
+        return fail(EXACTO_ERR_DIMENSION_MISMATCH, "dimension mismatch: expected " + std::to_string(c->L) + ", got " +
+                                                       std::to_string(limb));
     return run_ntt(c, contiguous(polys, count, 1, (int)limb, 1, c->n), (long)count, inverse);
 }
 
@@ -1437,8 +1469,8 @@ extern "C" int exacto_rns_polymul_dev(exacto_ctx* c, const uint64_t* a, const ui
         return 0;
     }
     Scratch sa, sb;
-    HIP_TRY(sa.alloc((size_t)rows * poly_bytes(c), c->stream));
-    HIP_TRY(sb.alloc((size_t)rows * poly_bytes(c), c->stream));
+    HIP_TRY(sa.alloc((size_t)rows * poly_bytes(c), c->stream, c->pool, c->debug_scratch));
+    HIP_TRY(sb.alloc((size_t)rows * poly_bytes(c), c->stream, c->pool, c->debug_scratch));
     NttBatch nb = contiguous(sa.as<u64>(), count, c->L, 0, c->L, c->n);
     nb.src = a;
     if (int e = run_ntt(c, nb, rows, false)) return e;
@@ -1766,15 +1798,10 @@ static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
 }
 
 // b_extended: c->ext_b already holds the extensions of b (a chain's constant right operand)
-// out = [B][dout][2][L][n] for the output limbs `limbs` (nullptr: all d, dout = d)
-static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
-                         const uint64_t* b, uint64_t* out, size_t B, bool b_extended,
-                         const std::vector<int>* limbs = nullptr) {
-    std::vector<int> all;
-    if (!limbs) {
-        for (size_t k = 0; k < d; ++k) all.push_back((int)k);
-        limbs = &all;
-    }
+// out = [B][dout][2][L][n] for the output limbs `limbs` (dout = limbs.size()), one group of items
+static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                          const uint64_t* b, uint64_t* out, size_t B, bool b_extended,
+                          const std::vector<int>* limbs) {
     const size_t dout = limbs->size();
     if (int e = dbfv_plan(c, B, d, base, plain, *limbs)) return e;
     const int npairs = c->cached_npairs;
@@ -1890,6 +1917,38 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     if (coef)
         if (int e = run_ntt(c, contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n), (long)B * dout * 2 * c->L, false))
             return e;
+    return 0;
+}
+
+// Every buffer of a dbfv_mul pass grows with its item count (the products' results and digits, their
+// per-limb digit sums and 31-bit residues, the shared extensions: ~81 MB per item at cfg5, ~2.5 MB
+// at cfg4), so a batch runs in groups of whole items whose buffers stay within EXACTO_DBFV_GROUP_MB
+// (default 4096 MB; the BASELINE batches are one group).  Items are independent: the groups give the
+// same results as one pass.  out = [B][dout][2][L][n] for the output limbs `limbs` (nullptr: all d).
+static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
+                         const uint64_t* b, uint64_t* out, size_t B, bool b_extended,
+                         const std::vector<int>* limbs = nullptr) {
+    std::vector<int> all;
+    if (!limbs) {
+        for (size_t k = 0; k < d; ++k) all.push_back((int)k);
+        limbs = &all;
+    }
+    const size_t dout = limbs->size();
+    const size_t budget = c->dbfv_group_bytes;
+    const size_t n = c->n, L = c->L, K = c->K, G = c->G, S = std::max(c->S32, c->kw.S);
+    const size_t per_item = 8 * n * (d * d * 2 * L + 2 * d * 2 * K) +       // products, both extensions
+                            n * G * (d * d * 2 + d * (4 + 4 * S)) +         // digits, sums, residues
+                            4 * n * d * 2 * L * S;                          // key-switch sums
+    const size_t Bg = std::max<size_t>(1, budget / std::max<size_t>(per_item, 1));
+    if (B <= Bg) return dbfv_mul_group(c, d, base, plain, a, b, out, B, b_extended, limbs);
+    const size_t ctw = 2 * L * n;
+    for (size_t g0 = 0; g0 < B; g0 += Bg) {
+        const size_t cnt = std::min(Bg, B - g0);
+        // b's extensions are per group here (a chain recomputes them for each group)
+        if (int e = dbfv_mul_group(c, d, base, plain, a + g0 * d * ctw, b + g0 * d * ctw, out + g0 * dout * ctw, cnt,
+                                   false, limbs))
+            return e;
+    }
     return 0;
 }
 
@@ -2533,7 +2592,7 @@ static int trace_core(exacto_ctx* c, const u64* src, u64* r, const std::vector<u
     if (ks.empty()) return 0;
     const long Ln = (long)c->L * c->n;
     Scratch rs;
-    HIP_TRY(rs.alloc(B * 2 * Ln * sizeof(u64), c->stream));
+    HIP_TRY(rs.alloc(B * 2 * Ln * sizeof(u64), c->stream, c->pool, c->debug_scratch));
     u64* rot = rs.as<u64>();
     int rc = 0;
     for (size_t e = 0; e < ks.size() && rc == 0; ++e) {
@@ -2607,7 +2666,7 @@ extern "C" int exacto_extract_coefficients_dev(exacto_ctx* c, const uint64_t* ct
     CHECK_LAUNCH();
     if (int e = ntt_items(c, c->pl_buf, (long)J, Ln, c->L)) return e;
     Scratch ss;
-    if (naive) HIP_TRY(ss.alloc(J * 2 * Ln * sizeof(u64), c->stream));
+    if (naive) HIP_TRY(ss.alloc(J * 2 * Ln * sizeof(u64), c->stream, c->pool, c->debug_scratch));
     u64* shifted = naive ? ss.as<u64>() : out;
     launch_plain_apply(PLAIN_MUL, ct, 0, shifted, (long)J, 2, c->pl_buf, Ln, n, c->L, c->d_primes, c->stream);
     int rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: monomial launch");
@@ -2801,7 +2860,7 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
     // workspace: baby[0], baby[2..k] (baby[1] is ct), one group accumulator, a Horner ping buffer
     const size_t nbuf = k + 3;
     Scratch wss;
-    HIP_TRY(wss.alloc(nbuf * words * sizeof(u64), c->stream));
+    HIP_TRY(wss.alloc(nbuf * words * sizeof(u64), c->stream, c->pool, c->debug_scratch));
     u64* ws = wss.as<u64>();
     std::vector<const u64*> baby(k + 1);
     auto slot = [&](size_t i) { return ws + i * words; };
@@ -2867,7 +2926,7 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
     if (!sk || !boot_sk || !s_pt) return invalid_param("null argument");
     const int n = o->n;
     Scratch ts;
-    HIP_TRY(ts.alloc(2 * n * sizeof(u64), o->stream));
+    HIP_TRY(ts.alloc(2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch));
     u64* tmp = ts.as<u64>();
     HIP_TRY(hipMemcpyAsync(tmp, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream));
     int rc = run_ntt(o, contiguous(tmp, 1, 1, 0, 1, n), 1, true);  // sk.poly.components[0].to_coeff_poly()
@@ -2926,8 +2985,8 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         if (rc == 0 && e != hipSuccess) rc = fail(EXACTO_ERR_HIP, std::string("HIP error: ") + what);
     };
     // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
-    ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream), "alloc");
-    ok(flags_s.alloc(B * sizeof(int), o->stream), "alloc");
+    ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch), "alloc");
+    ok(flags_s.alloc(B * sizeof(int), o->stream, o->pool, o->debug_scratch), "alloc");
     if (rc) return rc;
     u64* coef = coef_s.as<u64>();
     int* flags = flags_s.as<int>();
@@ -2944,7 +3003,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
     // 2. phase = TrivialEnc(c0') + bsk * c1' (b), written into out
     // [B][n] copies of c0' and c1' rows in the plaintext layout
-    if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream), "alloc");
+    if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
     u64* c0pt = c0pt_s.as<u64>();
     u64* c1pt = c0pt + B * n;
     if (rc == 0) {
@@ -2965,7 +3024,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     }
     // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
     const size_t ctw = 2 * Lbn;
-    if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream), "alloc");
+    if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
     u64* phase = phase_s.as<u64>();
     u64 *slots = nullptr, *rounded = nullptr;
     for (size_t i = 0; i < B && rc == 0; ++i) {
@@ -2977,7 +3036,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
             continue;
         }
         if (!slots) {  // once per call, on the first item that takes the ring path
-            ok(slots_s.alloc(2 * (size_t)n * ctw * sizeof(u64), b->stream), "alloc");
+            ok(slots_s.alloc(2 * (size_t)n * ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
             if (rc) break;
             slots = slots_s.as<u64>();
             rounded = slots + (size_t)n * ctw;

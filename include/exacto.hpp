@@ -757,4 +757,59 @@ inline DbfvCiphertext dbfv_mul_chain(const DbfvCiphertext& x, const DbfvCipherte
     return res;
 }
 
+
+// One GPU's share of a dbfv_mul split by output limb (dbfv/eval.rs:109-132): the limbs `limbs` of each
+// product a[i] * b[i] (mul_depth 0 inputs), as BfvCiphertexts [item][slot] (exacto_dbfv_mul_limbs).
+inline std::vector<std::vector<BfvCiphertext>> dbfv_mul_limbs(const std::vector<DbfvCiphertext>& a,
+                                                             const std::vector<DbfvCiphertext>& b,
+                                                             const RelinKey& rlk, const std::vector<uint32_t>& limbs) {
+    if (a.empty()) return {};
+    const auto& dp = *a[0].params;
+    detail::load_key(rlk);
+    std::vector<uint64_t> fa, fb;
+    for (size_t i = 0; i < a.size(); ++i) {
+        auto x = detail::flatten_dbfv(a[i]), y = detail::flatten_dbfv(b[i]);
+        fa.insert(fa.end(), x.begin(), x.end());
+        fb.insert(fb.end(), y.begin(), y.end());
+    }
+    const size_t per = 2 * dp.bfv_params->num_limbs() * dp.bfv_params->ring_degree;
+    std::vector<uint64_t> out(a.size() * limbs.size() * per);
+    detail::check(exacto_dbfv_mul_limbs(dp.bfv_params->ctx(), dp.num_digits, dp.base, dp.plain_modulus, fa.data(),
+                                        fb.data(), out.data(), a.size(), limbs.data(), limbs.size()));
+    std::vector<std::vector<BfvCiphertext>> res(a.size());
+    for (size_t i = 0; i < a.size(); ++i)
+        res[i] = detail::unflatten(std::vector<uint64_t>(out.begin() + (long)(i * limbs.size() * per),
+                                                         out.begin() + (long)((i + 1) * limbs.size() * per)),
+                                   limbs.size(), 2, dp.bfv_params);
+    return res;
+}
+
+// ---- RCCL over xGMI (exacto_hip.h): one communicator per GPU, keys broadcast from one root
+class RcclComm {
+  public:
+    // ncclGetUniqueId on the root; every rank passes the same 128 bytes
+    static std::vector<uint8_t> unique_id() {
+        std::vector<uint8_t> id(128);
+        detail::check(exacto_rccl_unique_id(id.data()));
+        return id;
+    }
+    RcclComm(int nranks, const std::vector<uint8_t>& id, int rank, int device) {
+        detail::check(exacto_rccl_comm_init(&h_, nranks, id.data(), rank, device));
+    }
+    ~RcclComm() { exacto_rccl_comm_destroy(h_); }
+    RcclComm(const RcclComm&) = delete;
+    RcclComm& operator=(const RcclComm&) = delete;
+    void* handle() const { return h_; }
+
+  private:
+    void* h_ = nullptr;
+};
+
+// The root's relinearisation key (loaded with load_relin_key / generated on its device) becomes the
+// resident key of every rank's context (ncclBroadcast in place): keys are made once, keygen.rs:123-162.
+inline void broadcast_relin_key(const BfvParams& prm, const RcclComm& comm, int root, size_t num_keys) {
+    detail::check(exacto_ctx_broadcast_relin_key(prm.ctx(), comm.handle(), root, num_keys));
+    prm.loaded_key = nullptr;   // resident contents now come from the root
+}
+
 }  // namespace exacto

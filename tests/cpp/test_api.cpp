@@ -108,6 +108,15 @@ static int run_case(const std::string& dir, const std::string& name) {
         }
         const auto want = read_u64(dir + "/" + name + ".out.u64");
         if (!same(limbs, want)) return 6;
+        // one GPU's share of a limb-split dbfv_mul: each limb, in reverse order, equals dbfv_mul's
+        std::vector<uint32_t> rev;
+        for (size_t k = m.d; k-- > 0;) rev.push_back((uint32_t)k);
+        auto part = dbfv_mul_limbs(A, Bc, rlk, rev);
+        for (size_t i = 0; i < B; ++i)
+            for (size_t s = 0; s < rev.size(); ++s)
+                if (part[i][s].c.size() != 2 || part[i][s].c[0].data != r[i].limbs[rev[s]].c[0].data ||
+                    part[i][s].c[1].data != r[i].limbs[rev[s]].c[1].data)
+                    return 44;
         // paper_repro.rs:203-236 chain: depth 1 is one dbfv_mul, depth 0 the input
         if (!same(dbfv_mul_chain(A[0], Bc[0], rlk, 1).limbs,
                   std::vector<uint64_t>(want.begin(), want.begin() + (long)per)))
@@ -195,6 +204,22 @@ static int keygen_case() {
     if (mixed.c.size() != 3 || decode_scalar(decrypt(mixed, sk)) != 24) return 28;
     auto mixed2 = bfv_sub(c3, c21);
     if (mixed2.c.size() != 3 || decode_scalar(decrypt(mixed2, sk)) != 257 - 18) return 29;
+    // RCCL entry points over a one-rank communicator: the resident key broadcast in place (then the
+    // product still decrypts), a device Galois-key buffer broadcast, an in-place all-gather
+    {
+        detail::load_key(rlk);
+        RcclComm comm(1, RcclComm::unique_id(), 0, 0);
+        broadcast_relin_key(*prm, comm, 0, rlk.keys.size());
+        if (decode_scalar(decrypt(bfv_mul_and_relin(c3, c7, rlk), sk)) != 21) return 40;
+        uint64_t* dev = exacto_ctx_relin_key_buffer(prm->ctx(), rlk.keys.size());
+        if (!dev) return 41;
+        detail::check(exacto_broadcast_galois_key(prm->ctx(), comm.handle(), 0, dev, rlk.keys.size()));
+        detail::check(exacto_rccl_allgather_u64(prm->ctx(), comm.handle(), dev, dev, 1024));
+        detail::check(exacto_synchronize(prm->ctx()));
+        if (exacto_ctx_broadcast_relin_key(prm->ctx(), comm.handle(), 3, rlk.keys.size()) != EXACTO_ERR_INVALID_PARAM)
+            return 42;
+        if (decode_scalar(decrypt(bfv_mul_and_relin(c3, c7, rlk), sk)) != 21) return 43;
+    }
     // eval.rs:954-976: sigma_3(1 + 2X) = 1 + 2X^3
     CoeffPoly m;
     m.coeffs.assign(prm->ring_degree, 0);

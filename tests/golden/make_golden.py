@@ -11,7 +11,12 @@
 3. digests.json — SHA-256 of the C-oracle output for full-size cfg3 (n=4096, 3x60-bit) on
    seeded inputs; the GPU tests regenerate the inputs and compare digests.
 
+   --dbfv-digests adds full-size cfg4 / cfg5 dbfv_mul and cfg5 depth-4 chain digests of the C
+   restatement of dbfv_mul (all d^2 products, sums, reduce).
+
 Run: python tests/golden/make_golden.py   (takes ~1 minute)
+     python tests/golden/make_golden.py --dbfv-digests   (~10 minutes on 8 cores)
+     python tests/golden/make_golden.py --worst-digests  (~5 minutes: tests/worstcase.py inputs at cfg5)
 """
 
 import hashlib
@@ -183,7 +188,97 @@ def sha(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint64).tobytes()).hexdigest()
 
 
+# Full-size dBFV digests (BASELINE configs[3] and [4]), from the C restatement of dbfv_mul
+# (oracle/c oracle_dbfv_mul: all d^2 products, per-limb sums, reduce): inputs regenerated from the
+# seed, item 0 of each list is the pinned item.  The chain is paper_repro's guard-bypass chain
+# (src/bin/paper_repro.rs:203-236: acc <- dbfv_mul(acc, y) with mul_depth reset, `depth` steps).
+DBFV_DIGESTS = {
+    "cfg4_full": {"config": "cfg4", "n": 4096, "items": 4, "seed": 4004, "depth": 1},
+    "cfg5_full": {"config": "cfg5", "n": 8192, "items": 1, "seed": 5005, "depth": 1},
+    "cfg5_chain4": {"config": "cfg5", "n": 8192, "items": 1, "seed": 5006, "depth": 4},
+}
+DBFV_GEN = ("numpy.random.default_rng(seed); a, b = uniform_residues((items, d, 2)); "
+            "rlk = uniform_residues((G, 2))  (tests/bridge.py)")
+
+
+def dbfv_digest_inputs(spec):
+    dp = P.cfg4_params(spec["n"]) if spec["config"] == "cfg4" else P.cfg5_params(spec["n"])
+    prm = dp.bfv_params
+    rng = np.random.default_rng(spec["seed"])
+    q, n, d = prm.ct_basis.moduli, prm.ring_degree, dp.num_digits
+    a = uniform_residues(rng, (spec["items"], d, 2), q, n)
+    b = uniform_residues(rng, (spec["items"], d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    return dp, a, b, rlk
+
+
+def dbfv_digests(threads):
+    from oracle import cref
+    out = {}
+    for name, spec in DBFV_DIGESTS.items():
+        dp, a, b, rlk = dbfv_digest_inputs(spec)
+        acc = a
+        for _ in range(spec["depth"]):
+            acc = cref.dbfv_mul(dp, acc, b, rlk, threads=threads)
+        e = dict(spec, generator=DBFV_GEN)
+        e["sha256_inputs"] = sha(np.concatenate([a.ravel(), b.ravel(), rlk.ravel()]))
+        e["sha256_out"] = sha(acc)
+        e["sha256_out_item0_limbs"] = [sha(acc[0, k]) for k in range(acc.shape[1])]
+        out[name] = e
+        print(name, e["sha256_out"], flush=True)
+    return out
+
+
+# Worst-case inputs of the two exactness bounds (tests/worstcase.py): every digit -B/2 with a
+# sign-aligned key (the key switch over 31-bit primes) and tensors at 2 n floor(Q/2)^2 (psum), at
+# cfg5 size, where the C restatement needs minutes (cfg3 / cfg4 are checked in-test).
+WORST = {
+    "worst_cfg5_digits": {"config": "cfg5", "n": 8192, "kind": "digits", "d": 8},
+    "worst_cfg5_tensor": {"config": "cfg5", "n": 8192, "kind": "tensor", "d": 8},
+}
+
+
+def worst_inputs(spec):
+    import worstcase as W
+    dp = P.cfg5_params(spec["n"]) if spec["config"] == "cfg5" else P.cfg4_params(spec["n"])
+    prm = dp.bfv_params
+    q, n, d, G = prm.ct_basis.moduli, prm.ring_degree, dp.num_digits, prm.gadget_digits
+    if spec["kind"] == "digits":
+        a, b, rlk, _ = W.digit_case_dbfv(q, prm.plain_modulus, prm.gadget_base, G, n, d)
+    else:
+        a, b, rlk = W.tensor_case_dbfv(q, n, d, G)
+    return dp, a, b, rlk
+
+
+def worst_digests(threads):
+    from oracle import cref
+    out = {}
+    for name, spec in WORST.items():
+        dp, a, b, rlk = worst_inputs(spec)
+        r = cref.dbfv_mul(dp, a, b, rlk, threads=threads)
+        e = dict(spec)
+        e["sha256_inputs"] = sha(np.concatenate([a.ravel(), b.ravel(), rlk.ravel()]))
+        e["sha256_out"] = sha(r)
+        out[name] = e
+        print(name, e["sha256_out"], flush=True)
+    return out
+
+
 def main():
+    if "--worst-digests" in sys.argv:
+        with open(os.path.join(HERE, "digests.json")) as f:
+            dg = json.load(f)
+        dg.update(worst_digests(threads=os.cpu_count() or 1))
+        with open(os.path.join(HERE, "digests.json"), "w") as f:
+            json.dump(dg, f, indent=1)
+        return
+    if "--dbfv-digests" in sys.argv:   # minutes of CPU: BigInt schoolbook tensors at n = 8192
+        with open(os.path.join(HERE, "digests.json")) as f:
+            dg = json.load(f)
+        dg.update(dbfv_digests(threads=os.cpu_count() or 1))
+        with open(os.path.join(HERE, "digests.json"), "w") as f:
+            json.dump(dg, f, indent=1)
+        return
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(kats(), f, indent=1)
     arrays, meta = {}, {}
@@ -200,8 +295,11 @@ def main():
     spec = dict(DIGEST_SPEC)
     spec["sha256_inputs"] = sha(np.concatenate([ct1.ravel(), ct2.ravel(), rlk.ravel()]))
     spec["sha256_out"] = sha(out)
-    with open(os.path.join(HERE, "digests.json"), "w") as f:
-        json.dump({"cfg3_full": spec}, f, indent=1)
+    path = os.path.join(HERE, "digests.json")
+    dg = json.load(open(path)) if os.path.exists(path) else {}
+    dg["cfg3_full"] = spec
+    with open(path, "w") as f:
+        json.dump(dg, f, indent=1)
     print("wrote kats.json, vectors.npz, vectors_meta.json, digests.json")
 
 

@@ -219,3 +219,52 @@ def test_cfg5_full_size(gpu_available):
     chain = ctx.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2)
     step2, _ = ctx.dbfv_mul(d, dp.base, dp.plain_modulus, out, b)
     assert np.array_equal(chain, step2)
+
+
+def _dbfv_digest_case(name, fill_to):
+    """The pinned items of a full-size dBFV digest, padded with other random items to the production
+    batch (psum, int8 / int16 digit sums, two-lane halves: all library defaults)."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import dbfv_digest_inputs
+    with open(os.path.join(GOLD, "digests.json")) as f:
+        spec = json.load(f)[name]
+    dp, a, b, rlk = dbfv_digest_inputs(spec)
+    sha = lambda x: hashlib.sha256(np.ascontiguousarray(x, dtype=np.uint64).tobytes()).hexdigest()
+    assert sha(np.concatenate([a.ravel(), b.ravel(), rlk.ravel()])) == spec["sha256_inputs"]
+    k = a.shape[0]
+    if fill_to > k:
+        rng = np.random.default_rng(99)
+        q, n, d = dp.bfv_params.ct_basis.moduli, spec["n"], dp.num_digits
+        a = np.concatenate([a, uniform_residues(rng, (fill_to - k, d, 2), q, n)])
+        b = np.concatenate([b, uniform_residues(rng, (fill_to - k, d, 2), q, n)])
+    ctx = HipContext.from_params(dp.bfv_params)
+    ctx.load_relin_key(rlk)
+    return spec, dp, ctx, a, b, k, sha
+
+
+def test_cfg4_full_size_dbfv_digest(gpu_available):
+    """BASELINE configs[3] at full size: 4 pinned dbfv_mul items in a batch of 64 (192 products: two
+    pipeline lanes, psum, wide-basis digit sums) against the C restatement's digest."""
+    spec, dp, ctx, a, b, k, sha = _dbfv_digest_case("cfg4_full", 64)
+    assert ctx.psum_max >= 2
+    out, _ = ctx.dbfv_mul(dp.num_digits, dp.base, dp.plain_modulus, a, b)
+    assert sha(out[:k]) == spec["sha256_out"]
+
+
+def test_cfg5_full_size_dbfv_digest(gpu_available):
+    """BASELINE configs[4] at full size (n = 8192, 4x60-bit, d = 8): one pinned dbfv_mul item in the
+    bench's batch of 8 (288 products: two lanes of 144, psum, int8 digit sums)."""
+    spec, dp, ctx, a, b, k, sha = _dbfv_digest_case("cfg5_full", 8)
+    out, _ = ctx.dbfv_mul(dp.num_digits, dp.base, dp.plain_modulus, a, b)
+    got = [sha(out[0, j]) for j in range(dp.num_digits)]
+    assert got == spec["sha256_out_item0_limbs"], [j for j in range(len(got)) if got[j] != spec["sha256_out_item0_limbs"][j]]
+    assert sha(out[:k]) == spec["sha256_out"]
+
+
+def test_cfg5_full_size_chain_digest(gpu_available):
+    """The bench's cfg5 workload itself: a depth-4 dbfv_mul chain (paper_repro.rs:203-236 guard-bypass
+    semantics) of one pinned item in a batch of 8, against the C restatement's digest."""
+    spec, dp, ctx, a, b, k, sha = _dbfv_digest_case("cfg5_chain4", 8)
+    out = ctx.dbfv_mul_chain(dp.num_digits, dp.base, dp.plain_modulus, a, b, spec["depth"])
+    assert sha(out[:k]) == spec["sha256_out"]

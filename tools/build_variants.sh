@@ -10,7 +10,7 @@ build() {  # name, flags...
   local name=$1; shift
   $H "$@" -c $R/exacto_amd/csrc/ntt.hip -o $OUT/ntt_$name.o
   $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o \
-    $R/build/obj/keygen.o $R/build/obj/plain.o $OUT/ntt_$name.o
+    $R/build/obj/keygen.o $R/build/obj/plain.o $R/build/obj/ks32.o $OUT/ntt_$name.o -ldl
 }
 for v in "$@"; do
   case $v in
