@@ -800,15 +800,23 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
         // blocks re-acquired after such a release gave wrong results at n = 16 (DESIGN.md §3,
         // "Scratch"), which keeping them mapped avoids.  Only this pool is configured; the device's
         // default pool keeps its settings for everything else in the process.
+        // EXACTO_SCRATCH_POOL=default: the device's default pool (threshold raised there), for A/B
+        const char* pe = getenv("EXACTO_SCRATCH_POOL");
+        const bool own = !(pe && std::strcmp(pe, "default") == 0);
         hipMemPoolProps props{};
         props.allocType = hipMemAllocationTypePinned;
         props.location.type = hipMemLocationTypeDevice;
         props.location.id = device;
-        if (hipMemPoolCreate(&c->pool, &props) == hipSuccess) {
-            uint64_t thr = ~0ull;
-            (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr);
+        uint64_t thr = ~0ull;
+        if (own && hipMemPoolCreate(&c->pool, &props) == hipSuccess &&
+            hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess) {
+            // this pool only
         } else {
-            c->pool = nullptr;   // Scratch falls back to the device's default pool
+            if (c->pool) (void)hipMemPoolDestroy(c->pool);
+            c->pool = nullptr;   // Scratch uses the device's default pool, kept mapped the same way
+            hipMemPool_t dp;
+            if (hipDeviceGetDefaultMemPool(&dp, device) == hipSuccess)
+                (void)hipMemPoolSetAttribute(dp, hipMemPoolAttrReleaseThreshold, &thr);
         }
     }
     if (const char* e = getenv("EXACTO_DEBUG_SCRATCH")) c->debug_scratch = atoi(e) != 0;

@@ -801,6 +801,37 @@ __device__ __forceinline__ u64 mulmod_near60(u64 a, u64 b, uint32_t d) {
     return L2 + H2 * d;
 }
 
+// Products of the tensor kernels by the generated MulNear60Asm statements (ntt_asm.inc,
+// tools/gen_ntt_asm.py MulPair): 9 slow + 6 fast instructions per product, the same result (< 2q) as
+// mulmod_near60, which hipcc compiles to ~26 (EXACTO_MUL_ASM=0 keeps the C++ for A/B builds).
+#ifndef EXACTO_MUL_ASM
+#define EXACTO_MUL_ASM 1
+#endif
+__device__ __forceinline__ void mul2_near60(u64& r0, u64 a0, u64 b0, u64& r1, u64 a1, u64 b1, uint32_t d) {
+#if EXACTO_MUL_ASM
+    MulNear60Asm<2>::run(r0, r1, a0, b0, a1, b1, d, 16 * d);
+#else
+    r0 = mulmod_near60(a0, b0, d);
+    r1 = mulmod_near60(a1, b1, d);
+#endif
+}
+
+__device__ __forceinline__ u64 mul1_near60(u64 a, u64 b, uint32_t d) {
+#if EXACTO_MUL_ASM
+    u64 r;
+    MulNear60Asm<1>::run(r, a, b, d, 16 * d);
+    return r;
+#else
+    return mulmod_near60(a, b, d);
+#endif
+}
+
+// x[k] = a[k] b[k] mod q (< 2q), k < 16
+__device__ __forceinline__ void mul16_near60(u64 (&x)[16], const u64 (&a)[16], const u64 (&b)[16], uint32_t d) {
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) mul2_near60(x[k], a[k], b[k], x[k + 1], a[k + 1], b[k + 1], d);
+}
+
 // Block b -> logical index, so that each group of G consecutive logical indices runs on one XCD
 // in consecutive dispatch slots (workgroups go to XCDs round robin, b % 8: a placement used for
 // speed only, never for correctness).  Bijective on [0, total); a tail that does not fill 8
@@ -868,21 +899,35 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     if (c != 1) {
         load(c == 0 ? A0 : A1, x);
         load(c == 0 ? B0 : B1, y);
+        if constexpr (ASM) {
+            mul16_near60(x, x, y, dq);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = mulr(x[k], y[k]);
+            for (int k = 0; k < 16; ++k) x[k] = mulr(x[k], y[k]);
+        }
     } else {
         u64 z[16];
         load(A0, x);
         load(B1, y);
+        if constexpr (ASM) {
+            mul16_near60(z, x, y, dq);
+        } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) z[k] = mulr(x[k], y[k]);
+            for (int k = 0; k < 16; ++k) z[k] = mulr(x[k], y[k]);
+        }
         load(A1, x);
         load(B0, y);
         const u64 q = P.q, q2 = P.two_q;
+        if constexpr (ASM) {
+            mul16_near60(x, x, y, dq);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const u64 v = z[k] + mulr(x[k], y[k]);
-            x[k] = ASM ? v : LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);  // ASM: < 4q
+            for (int k = 0; k < 16; ++k) x[k] += z[k];   // < 4q
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const u64 v = z[k] + mulr(x[k], y[k]);
+                x[k] = LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
+            }
         }
     }
     if constexpr (ASM) {
@@ -924,9 +969,12 @@ ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
         x[2 * k] = u.x; x[2 * k + 1] = u.y;
         y[2 * k] = v.x; y[2 * k + 1] = v.y;
     }
+    if constexpr (ASM) {
+        mul16_near60(x, x, y, dq);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-        x[k] = ASM ? mulmod_near60(x[k], y[k], dq) : LAZY ? barrett_mul_lazy(x[k], y[k], P) : mul_mod(x[k], y[k], P);
+        for (int k = 0; k < 16; ++k) x[k] = LAZY ? barrett_mul_lazy(x[k], y[k], P) : mul_mod(x[k], y[k], P);
+    }
     if constexpr (ASM) {
         const AsmK AK = make_asmk_inv(P);
         inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
@@ -1008,8 +1056,7 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     fwd_rounds_asm<LOGN, 0>(xa, lds, tid, tf, K);
     fwd_rounds_asm<LOGN, 0>(xb, lds, tid, tf, K);
     const uint32_t dq = (uint32_t)((1ull << 60) - q);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) xa[k] = mulmod_near60(xa[k], xb[k], dq);   // < 2q: the inverse's input bound
+    mul16_near60(xa, xa, xb, dq);   // < 2q: the inverse's input bound
     const AsmK AK = make_asmk_inv(P);
     inv_rounds_asm<LOGN, 0>(xa, lds, tid, tw_table(P.tw_inv), AK);
     u64* dst = out + p * N;
@@ -1253,10 +1300,16 @@ ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restric
         load(A1, a1);
         load(B1, b1);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            stash[k * T + tid] = mulmod_near60(a1[k], b1[k], dq);
-            c1[k] = mulmod_near60(a0[k], b1[k], dq) + mulmod_near60(a1[k], b0[k], dq);   // < 4q
-            c0[k] = mulmod_near60(a0[k], b0[k], dq);
+        for (int k = 0; k < 16; k += 2) {
+            u64 p0, p1, s0, s1;
+            mul2_near60(p0, a1[k], b1[k], p1, a1[k + 1], b1[k + 1], dq);
+            stash[k * T + tid] = p0;
+            stash[(k + 1) * T + tid] = p1;
+            mul2_near60(p0, a0[k], b1[k], p1, a0[k + 1], b1[k + 1], dq);
+            mul2_near60(s0, a1[k], b0[k], s1, a1[k + 1], b0[k + 1], dq);
+            c1[k] = p0 + s0;             // < 4q
+            c1[k + 1] = p1 + s1;
+            mul2_near60(c0[k], a0[k], b0[k], c0[k + 1], a0[k + 1], b0[k + 1], dq);
         }
     }
     const AsmK AK = make_asmk_inv(P);
@@ -1295,8 +1348,7 @@ ntt_inv_tensor_c2_kernel(Operands op, u64* __restrict__ Tout, int L, int K, cons
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const ulonglong2 u = s1[e], v = s2[e];
-        x[2 * e] = mulmod_near60(u.x, v.x, dq);
-        x[2 * e + 1] = mulmod_near60(u.y, v.y, dq);
+        mul2_near60(x[2 * e], u.x, v.x, x[2 * e + 1], u.y, v.y, dq);
     }
     inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
     u64* dst = Tout + ((item * 3 + 2) * (L + K) + L + a) * N;
@@ -1332,12 +1384,13 @@ dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L
         const u64* EA = op.ea + (long)op.ea_off[pr] + off_a;
         const u64* EB = op.eb + (long)op.eb_off[pr] + off_a;
         const u64 a0 = EA[0], a1 = EA[off_k], b0 = EB[0], b1 = EB[off_k];
-        u64 v = s0 + mulmod_near60(a0, b0, dq);
+        u64 p0, p1;
+        mul2_near60(p0, a0, b1, p1, a1, b0, dq);
+        u64 v = s1 + p0 + p1;                      // < 6q
+        v = v >= 4 * q ? v - 4 * q : v;
+        s1 = v >= q2 ? v - q2 : v;
+        v = s0 + mul1_near60(a0, b0, dq);
         s0 = v >= q2 ? v - q2 : v;
-        v = s1 + mulmod_near60(a0, b1, dq);
-        s1 = v >= q2 ? v - q2 : v;
-        v = s1 + mulmod_near60(a1, b0, dq);
-        s1 = v >= q2 ? v - q2 : v;
     }
     u64* o = out + (((ib * d + k) * 2) * K + a) * (long)n + j;
     o[0] = s0 >= q ? s0 - q : s0;

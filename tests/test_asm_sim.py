@@ -26,6 +26,15 @@ def test_rounds_match_exact_arithmetic():
                     asm_sim.check_inv_round(logn, r, q, rng, approx)
 
 
+def test_tensor_products_match_exact_arithmetic():
+    # MulNear60Asm: the 120-bit product folded twice through 2^60 == d, for every BASELINE prime
+    # (the fifth entry of PRIMES has d = 2^32 - 3, outside the d < 2^24 this sequence needs)
+    rng = random.Random(11)
+    for i in range(2000):
+        for w in (1, 2):
+            asm_sim.check_mulpair(w, asm_sim.PRIMES[i % 4], rng)
+
+
 def test_committed_inc_is_current(tmp_path):
     out = tmp_path / "ntt_asm.inc"
     old = gen_ntt_asm.OUT

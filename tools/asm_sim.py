@@ -115,6 +115,8 @@ class Lane:
             self.wr32(ops[0], x >> int(ops[1]))
         elif mnem == "v_and_b32":
             self.wr32(ops[0], self.rd32(ops[1]) & self.rd32(ops[2]))
+        elif mnem == "v_alignbit_b32":
+            self.wr32(ops[0], ((self.rd32(ops[1]) << 32 | self.rd32(ops[2])) >> int(ops[3])) & M32)
         else:
             raise NotImplementedError(mnem)
 
@@ -218,6 +220,30 @@ def check_inv_round(logn, r, q, rng, approx=True):
         assert got[k] < rd.bound_out * q, ("inv bound", logn, r, k, got[k] / q, rd.bound_out)
 
 
+def check_mulpair(w, q, rng):
+    """MulNear60Asm<w>: r_k == a_k b_k (mod q) and r_k < 2q for a_k, b_k < q (extremes included)."""
+    st = G.MulPair(w)
+    seq = st.gen()
+    d = (1 << 60) - q
+    vals = []
+    for k in range(w):
+        if rng.random() < 0.3:
+            a, b = q - 1 - rng.randrange(3), q - 1 - rng.randrange(3)
+        else:
+            a, b = rng.randrange(q), rng.randrange(q)
+        vals.append((a, b))
+    named = {"d": [d, 32], "e": [16 * d, 32]}
+    for k, (a, b) in enumerate(vals):
+        named.update({f"a{k}l": [a & M32, 32], f"a{k}h": [a >> 32, 32], f"b{k}l": [b & M32, 32],
+                      f"b{k}h": [b >> 32, 32], f"r{k}": [0, 64]})
+    lane = Lane(named)
+    for ins in seq:
+        lane.run(ins.text)
+    for k, (a, b) in enumerate(vals):
+        r = named[f"r{k}"][0]
+        assert r % q == a * b % q and r < 2 * q, ("mulpair", w, k, a, b, r)
+
+
 PRIMES = [1152921504606830593, 1152921504606748673, 1152921504606683137, 1152921504606601217,
           (1 << 60) - (1 << 32) + 3]  # the last: d = 2^32 - 3, the edge of the path (primality irrelevant here)
 
@@ -231,6 +257,9 @@ def main():
                 for i in range(trials):
                     check_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
                     check_inv_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+    for i in range(trials):
+        for w in (1, 2):
+            check_mulpair(w, PRIMES[i % 4], rng)
     print(f"asm_sim: all forward and inverse rounds of n=4096/8192 (approximate and exact Shoup "
           f"quotients) agree with exact arithmetic over {trials} trials each")
 
