@@ -315,7 +315,7 @@ struct exacto_ctx {
     // per-call scratch: the context's own stream-ordered pool (Scratch)
     hipMemPool_t pool = nullptr;
     bool debug_scratch = false;
-    size_t dbfv_group_bytes = (size_t)4096 << 20;   // dbfv_mul item groups (EXACTO_DBFV_GROUP_MB)
+    size_t dbfv_group_bytes = (size_t)16384 << 20;  // dbfv_mul item groups (EXACTO_DBFV_GROUP_MB)
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
@@ -1282,6 +1282,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         // scale bytes per item: the three components' L+K residues in; c0, c1 (L residues each) out
         // (psum: c2 only), and the third component's digits (int16 / int8) or its L residues
         const double dig_b = d16 ? (c->ks_defer && c->ks_defer8 ? 1.0 : 2.0) * guse : 8.0 * L * (relin ? guse : 1);
+        {   // (scoped: the events bracket the scale launch alone)
         ProfScope psc(c, PK_SCALE, (u64)cnt, (double)n * cnt *
                       ((ps.on ? 1.0 : 3.0) * 8.0 * (L + K) + (ps.on ? 0.0 : 16.0 * L) + (relin ? dig_b : 8.0 * L)));
         if (c->path == EXACTO_PATH_HPS)
@@ -1296,6 +1297,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                                guse, cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
                                c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8);
         CHECK_LAUNCH();
+        }
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
             const long item0 = s / ps.npairs;
             const double ib = (double)(cnt / ps.npairs);
@@ -1929,10 +1931,12 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
 }
 
 // Every buffer of a dbfv_mul pass grows with its item count (the products' results and digits, their
-// per-limb digit sums and 31-bit residues, the shared extensions: ~81 MB per item at cfg5, ~2.5 MB
-// at cfg4), so a batch runs in groups of whole items whose buffers stay within EXACTO_DBFV_GROUP_MB
-// (default 4096 MB; the BASELINE batches are one group).  Items are independent: the groups give the
-// same results as one pass.  out = [B][dout][2][L][n] for the output limbs `limbs` (nullptr: all d).
+// per-limb digit sums and 31-bit residues, the shared extensions: per_item below, 4.4 MB at cfg4 and
+// 113 MB at cfg5), so a batch runs in groups of whole items whose buffers stay within
+// EXACTO_DBFV_GROUP_MB (default 16 GiB of the 288 GB HBM: the BASELINE batches, 4.5 GB at cfg4 and
+// 0.9 GB at cfg5, are one group -- a 4 GiB default split cfg4's 1024 items into 932 + 92 and cost 5 %).
+// Items are independent: the groups give the same results as one pass.  out = [B][dout][2][L][n] for
+// the output limbs `limbs` (nullptr: all d).
 static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
                          const uint64_t* b, uint64_t* out, size_t B, bool b_extended,
                          const std::vector<int>* limbs = nullptr) {

@@ -804,32 +804,41 @@ __device__ __forceinline__ u64 mulmod_near60(u64 a, u64 b, uint32_t d) {
 // Products of the tensor kernels by the generated MulNear60Asm statements (ntt_asm.inc,
 // tools/gen_ntt_asm.py MulPair): 9 slow + 6 fast instructions per product, the same result (< 2q) as
 // mulmod_near60, which hipcc compiles to ~26 (EXACTO_MUL_ASM=0 keeps the C++ for A/B builds).
+// The statements clobber fixed VGPRs (v104 up), so the register allocator must keep everything
+// live across them elsewhere: in kernels that hold many operands that costs spills.  Measured
+// same-box A/B (ROUND 3): ntt_inv_tensor_kernel<12> 323 -> 305 us per launch with the asm (no
+// spills either way), but dbfv_pairsum 51 -> 95 us, ntt_inv_tensor3_kernel<13> 258 -> 277 us and
+// ntt_inv_tensor_c2_kernel<13> 130 -> 156 us (12 / 28 VGPRs spilled): those take the C++ form
+// (ASM = false at their call sites).
 #ifndef EXACTO_MUL_ASM
 #define EXACTO_MUL_ASM 1
 #endif
+template <bool ASM = (EXACTO_MUL_ASM != 0)>
 __device__ __forceinline__ void mul2_near60(u64& r0, u64 a0, u64 b0, u64& r1, u64 a1, u64 b1, uint32_t d) {
-#if EXACTO_MUL_ASM
-    MulNear60Asm<2>::run(r0, r1, a0, b0, a1, b1, d, 16 * d);
-#else
-    r0 = mulmod_near60(a0, b0, d);
-    r1 = mulmod_near60(a1, b1, d);
-#endif
+    if constexpr (ASM) {
+        MulNear60Asm<2>::run(r0, r1, a0, b0, a1, b1, d, 16 * d);
+    } else {
+        r0 = mulmod_near60(a0, b0, d);
+        r1 = mulmod_near60(a1, b1, d);
+    }
 }
 
+template <bool ASM = (EXACTO_MUL_ASM != 0)>
 __device__ __forceinline__ u64 mul1_near60(u64 a, u64 b, uint32_t d) {
-#if EXACTO_MUL_ASM
-    u64 r;
-    MulNear60Asm<1>::run(r, a, b, d, 16 * d);
-    return r;
-#else
-    return mulmod_near60(a, b, d);
-#endif
+    if constexpr (ASM) {
+        u64 r;
+        MulNear60Asm<1>::run(r, a, b, d, 16 * d);
+        return r;
+    } else {
+        return mulmod_near60(a, b, d);
+    }
 }
 
 // x[k] = a[k] b[k] mod q (< 2q), k < 16
+template <bool ASM = (EXACTO_MUL_ASM != 0)>
 __device__ __forceinline__ void mul16_near60(u64 (&x)[16], const u64 (&a)[16], const u64 (&b)[16], uint32_t d) {
 #pragma unroll
-    for (int k = 0; k < 16; k += 2) mul2_near60(x[k], a[k], b[k], x[k + 1], a[k + 1], b[k + 1], d);
+    for (int k = 0; k < 16; k += 2) mul2_near60<ASM>(x[k], a[k], b[k], x[k + 1], a[k + 1], b[k + 1], d);
 }
 
 // Block b -> logical index, so that each group of G consecutive logical indices runs on one XCD
@@ -970,7 +979,7 @@ ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
         y[2 * k] = v.x; y[2 * k + 1] = v.y;
     }
     if constexpr (ASM) {
-        mul16_near60(x, x, y, dq);
+        mul16_near60<false>(x, x, y, dq);
     } else {
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = LAZY ? barrett_mul_lazy(x[k], y[k], P) : mul_mod(x[k], y[k], P);
@@ -1302,14 +1311,14 @@ ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restric
 #pragma unroll
         for (int k = 0; k < 16; k += 2) {
             u64 p0, p1, s0, s1;
-            mul2_near60(p0, a1[k], b1[k], p1, a1[k + 1], b1[k + 1], dq);
+            mul2_near60<false>(p0, a1[k], b1[k], p1, a1[k + 1], b1[k + 1], dq);
             stash[k * T + tid] = p0;
             stash[(k + 1) * T + tid] = p1;
-            mul2_near60(p0, a0[k], b1[k], p1, a0[k + 1], b1[k + 1], dq);
-            mul2_near60(s0, a1[k], b0[k], s1, a1[k + 1], b0[k + 1], dq);
+            mul2_near60<false>(p0, a0[k], b1[k], p1, a0[k + 1], b1[k + 1], dq);
+            mul2_near60<false>(s0, a1[k], b0[k], s1, a1[k + 1], b0[k + 1], dq);
             c1[k] = p0 + s0;             // < 4q
             c1[k + 1] = p1 + s1;
-            mul2_near60(c0[k], a0[k], b0[k], c0[k + 1], a0[k + 1], b0[k + 1], dq);
+            mul2_near60<false>(c0[k], a0[k], b0[k], c0[k + 1], a0[k + 1], b0[k + 1], dq);
         }
     }
     const AsmK AK = make_asmk_inv(P);
@@ -1348,7 +1357,7 @@ ntt_inv_tensor_c2_kernel(Operands op, u64* __restrict__ Tout, int L, int K, cons
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const ulonglong2 u = s1[e], v = s2[e];
-        mul2_near60(x[2 * e], u.x, v.x, x[2 * e + 1], u.y, v.y, dq);
+        mul2_near60<false>(x[2 * e], u.x, v.x, x[2 * e + 1], u.y, v.y, dq);
     }
     inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
     u64* dst = Tout + ((item * 3 + 2) * (L + K) + L + a) * N;
@@ -1385,11 +1394,11 @@ dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L
         const u64* EB = op.eb + (long)op.eb_off[pr] + off_a;
         const u64 a0 = EA[0], a1 = EA[off_k], b0 = EB[0], b1 = EB[off_k];
         u64 p0, p1;
-        mul2_near60(p0, a0, b1, p1, a1, b0, dq);
+        mul2_near60<false>(p0, a0, b1, p1, a1, b0, dq);
         u64 v = s1 + p0 + p1;                      // < 6q
         v = v >= 4 * q ? v - 4 * q : v;
         s1 = v >= q2 ? v - q2 : v;
-        v = s0 + mul1_near60(a0, b0, dq);
+        v = s0 + mul1_near60<false>(a0, b0, dq);
         s0 = v >= q2 ? v - q2 : v;
     }
     u64* o = out + (((ib * d + k) * 2) * K + a) * (long)n + j;

@@ -101,3 +101,36 @@ def test_int8_digits_cfg5(gpu_available):
         ctx.load_relin_key(rlk)
         res.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
     assert np.array_equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("chain", [False, True])
+def test_dbfv_item_groups_match_one_pass(gpu_available, chain):
+    """A batch whose buffers exceed EXACTO_DBFV_GROUP_MB runs in groups of whole items
+    (dbfv_mul_core); 1 MB forces one item per group at cfg4 (4.4 MB per item).  Items are
+    independent, so every group size gives the one-pass result, for dbfv_mul and for a chain (whose
+    constant right operand's extensions are then recomputed per group)."""
+    dp = P.cfg4_params(4096)
+    prm = dp.bfv_params
+    q, n, d, B = prm.ct_basis.moduli, 4096, 2, 3
+    rng = np.random.default_rng(5151)
+    a = uniform_residues(rng, (B, d, 2), q, n)
+    b = uniform_residues(rng, (B, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    outs = []
+    for mb in ("1", None):
+        old = os.environ.get("EXACTO_DBFV_GROUP_MB")
+        if mb:
+            os.environ["EXACTO_DBFV_GROUP_MB"] = mb
+        try:
+            ctx = HipContext.from_params(prm, device=0)
+        finally:
+            if old is None:
+                os.environ.pop("EXACTO_DBFV_GROUP_MB", None)
+            else:
+                os.environ["EXACTO_DBFV_GROUP_MB"] = old
+        ctx.load_relin_key(rlk)
+        if chain:
+            outs.append(ctx.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2))
+        else:
+            outs.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+    assert np.array_equal(outs[0], outs[1])

@@ -28,6 +28,8 @@ for v in "$@"; do
     w5) build w5 -DEXACTO_NTT_WAVES=5 ;;
     ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
+    noaddx) build noaddx -DEXACTO_ASM_ADDX=0 ;;
+    nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
     pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
     pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;

@@ -151,13 +151,15 @@ class Statement:
     def xl(self, k): return self._in(f"x{k}l", "v", f"(uint32_t)x[{k}]")
 
 
-def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True):
-    """Instructions computing T['E'] = Shoup(Y, w) (in [0, 2q) exact, [0, 3q) approx).
-    T: temp pairs Z (Z.hi == 0, exact only), A, B, E, F; c: this stream's carry SGPR pair.
-    fixup=False leaves out the last instruction (E.hi += F.lo) for the caller to place: E.lo is
-    final before it."""
+def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True, E=None, addend="0"):
+    """Instructions computing E = addend + Shoup(Y, w) mod 2^64 (Shoup in [0, 2q) exact, [0, 3q)
+    approx).  T: temp pairs Z (Z.hi == 0, exact only), A, B, E, F; c: this stream's carry SGPR pair.
+    E: the result pair (default T['E']; must be addressable by halves); addend: a 64-bit operand
+    added for free by the first mad (the forward butterfly's X).  fixup=False leaves out the last
+    instruction (E.hi += F.lo) for the caller to place: E.lo is final before it."""
     SD = sp(SGPR_SD)
-    Z, A, B, E, F = (T.get(n) for n in "ZABEF")
+    Z, A, B, _, F = (T.get(n) for n in "ZABEF")
+    E = E or T.get("E")
     seq = []
     if approx:
         seq.append(Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s0}, 0", wr=[SD]))
@@ -166,7 +168,7 @@ def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True):
         seq.append(Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s0}, {Z}", wr=[SD]))
     seq += [
         Ins(f"v_mad_u64_u32 {B}, {c}, {yl}, {s1}, {A}", wr=[c]),
-        Ins(f"v_mad_u64_u32 {E}, {SD}, {yl}, {w0}, 0", wr=[SD]),
+        Ins(f"v_mad_u64_u32 {E}, {SD}, {yl}, {w0}, {addend}", wr=[SD]),
         Ins(f"v_mov_b32 {lo(A)}, {hi(B)}"),
         Ins(f"v_mul_lo_u32 {lo(F)}, {yl}, {w1}"),
         Ins(f"v_cndmask_b32_e64 {hi(A)}, 0, 1, {c}", rd=[c]),
@@ -226,9 +228,9 @@ def emit_statement(struct, st, seq, vmax, comment, run_args):
 class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
-    def __init__(self, logn, r, approx=True):
+    def __init__(self, logn, r, approx=True, addx=True):
         super().__init__()
-        self.logn, self.r, self.approx = logn, r, approx
+        self.logn, self.r, self.approx, self.addx = logn, r, approx, addx
         self.c = 3 if approx else 2            # Shoup output bound (units of q)
         self.lo = max(logn - 4 * (r + 1), 0)
         self.bhi = logn - 1 - 4 * r
@@ -304,6 +306,24 @@ class Round(Statement):
                         yl, yh = self.xl(k1), self.xh(k1)
                     X = vp(P[k0]) if in_p[k0] else xop[k0]
                     o0, o1 = (xop[k0], xop[k1]) if direct_out else (vp(P[k0]), vp(P[k1]))
+                    if not direct_out and self.addx:
+                        # o0 = X + T straight from the Shoup chain (X is its first mad's addend), and
+                        # o1 = (2X + cq) - o0 = X + cq - T (mod 2^64; the true value is < 16q):
+                        # one 64-bit add less per butterfly.  2X + cq goes to the E pair before
+                        # the chain overwrites X's pair (o0 is usually X's own pair).
+                        Zt = T["E"]
+                        s = [Ins(f"v_lshl_add_u64 {Zt}, {X}, 1, {self.mq(self.c)}")]
+                        s += shoup_seq(self, yl, yh, self.tw(slot, "w0"), self.tw(slot, "w1"),
+                                       self.tw(slot, "s0"), self.tw(slot, "s1"), T, c, self.approx,
+                                       fixup=False, E=o0, addend=X)
+                        s += [
+                            Ins(f"v_sub_co_u32_e64 {lo(o1)}, {c}, {lo(Zt)}, {lo(o0)}", wr=[c]),
+                            fix_seq(o0, T["F"]),
+                            Ins(f"v_subb_co_u32_e64 {hi(o1)}, {c}, {hi(Zt)}, {hi(o0)}, {c}", rd=[c], wr=[c]),
+                        ]
+                        streams.append(s)
+                        in_p[k0] = in_p[k1] = True
+                        continue
                     s = shoup_seq(self, yl, yh, self.tw(slot, "w0"), self.tw(slot, "w1"),
                                   self.tw(slot, "s0"), self.tw(slot, "s1"), T, c, self.approx, fixup=False)
                     s += [
@@ -594,6 +614,9 @@ HEADER = """// GENERATED by tools/gen_ntt_asm.py -- do not edit.
 #ifndef EXACTO_ASM_APPROX
 #define EXACTO_ASM_APPROX 1   // Shoup quotient without the low-low partial product (T < 3q)
 #endif
+#ifndef EXACTO_ASM_ADDX
+#define EXACTO_ASM_ADDX 1     // forward butterflies: X as the Shoup chain's addend (one add less)
+#endif
 
 struct AsmK {
     uint32_t n0, n1;      // 2^64 - q (n1 = 0xF0000000 for the primes of this path)
@@ -633,9 +656,12 @@ def main():
     for approx in (True, False):
         parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
         for logn in (12, 13):
-            for r in range((logn + 3) // 4):
-                parts.append(Round(logn, r, approx).emit())
-                parts.append("\n")
+            for addx in (True, False):
+                parts.append(f"#if {'' if addx else '!'}EXACTO_ASM_ADDX\n\n")
+                for r in range((logn + 3) // 4):
+                    parts.append(Round(logn, r, approx, addx).emit())
+                    parts.append("\n")
+                parts.append(f"#endif  // {'' if addx else '!'}EXACTO_ASM_ADDX\n\n")
             for rd in inv_rounds(logn, approx):
                 parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
                 parts.append("\n")
