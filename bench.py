@@ -9,7 +9,8 @@ timed region starts.
 
 A step is `reps` passes of the hot path, each over one whole batch (the input batches rotate over
 two resident copies).  `reps` is chosen after the warm-up so that the K timed steps last at least
---min-time seconds (default 2 s): the BASELINE batch (1024 products, ~2.5 ms) is far shorter than
+--min-time seconds (default 2.5 s: the batch-count estimate comes from two untimed batches, so the
+region itself lands at >= 2 s): the BASELINE batch (1024 products, ~2.5 ms) is far shorter than
 anything a wall-clock or GPU-busy sampler can see.  value = units processed / timed seconds.
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the
@@ -83,7 +84,7 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=0, help="products per pipeline chunk (0 = library default)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--split", default="batch", choices=("batch", "limbs"))
-    ap.add_argument("--min-time", type=float, default=2.0, help="lower bound of the timed region, seconds")
+    ap.add_argument("--min-time", type=float, default=2.5, help="lower bound of the timed region, seconds")
     ap.add_argument("--reps", type=int, default=0, help="batches per step (0 = from --min-time)")
     ap.add_argument("--dry", action="store_true", help="no HIP calls: CPU/gloo stand-in of the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -138,11 +139,13 @@ def _entry(rec, name, share=None):
     return e
 
 
-def roofline_block(ctx, step_one, cfg, n, L, S):
-    """One profiled batch (single lane: per-kernel events time each kernel alone), every family."""
-    ctx.prof_enable(True)
-    step_one()
+def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
+    """`batches` profiled batches after the timed region (single lane: per-kernel events time each
+    kernel alone), every family; launch averages over all of them."""
     import torch
+    ctx.prof_enable(True)
+    for _ in range(batches):
+        step_one()
     torch.cuda.synchronize()
     recs = {k: ctx.prof_read(k) for k in KINDS}
     ctx.prof_enable(False)

@@ -1,7 +1,16 @@
-"""Per-kernel VALU issue counters from a `rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE
-SQ_BUSY_CYCLES` run of bench.py -> the JSON bench.py reads as profiles/r2_<cfg>_valu_counters.json.
+"""Per-kernel issue counters from `rocprofv3 --pmc ...` runs of bench.py (one or more pass
+directories) -> the JSON bench.py reads as profiles/r3_<cfg>_valu_counters.json.
 
-usage: python3 tools/valu_report.py <pmc dir> <source description> > out.json
+Every counter found is averaged per dispatch.  Derived, where the counters are present:
+  valu_per_wave        SQ_INSTS_VALU / SQ_WAVES
+  gpu_cycles           GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs)
+  wave_cycles          SQ_WAVE_CYCLES * 4 / SQ_WAVES (SQ_* cycle counters count quad-cycles)
+  frac_active / frac_wait_any / frac_wait_inst   SQ_ACTIVE_INST_ANY, SQ_WAIT_ANY (parked:
+                       s_waitcnt / barrier), SQ_WAIT_INST_ANY (issue stall) over SQ_WAVE_CYCLES
+                       (the three are disjoint and sum to about 1)
+  frac_valu            SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
+
+usage: python3 tools/valu_report.py "<source description>" <pmc dir> [<pmc dir> ...] > out.json
 """
 import collections
 import csv
@@ -9,27 +18,51 @@ import glob
 import json
 import sys
 
-d = sys.argv[1]
+src = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
-for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        k = (f, int(r["Dispatch_Id"]))
-        vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        names[k] = r["Kernel_Name"].split("(")[0]
-agg = collections.defaultdict(list)
-for k, v in vals.items():
-    agg[names[k]].append(v)
-out = {"source": sys.argv[2] if len(sys.argv) > 2 else d,
-       "note": "per-dispatch averages; SQ_INSTS_VALU and SQ_WAVES are chip totals; "
-               "GRBM_GUI_ACTIVE summed over 8 XCDs (divided back)",
+for d in sys.argv[2:]:
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = (d, int(r["Dispatch_Id"]))
+            vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            names[k] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+# the passes are separate runs of the same program: dispatch ids line up per kernel name in order
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for k, v in sorted(vals.items()):
+    for c, x in v.items():
+        agg[names[k]][c].append(x)
+out = {"source": src,
+       "note": "per-dispatch averages; SQ_* counts are chip totals (cycle counters in quad-cycles); "
+               "GRBM_GUI_ACTIVE summed over 8 XCDs (divided back in gpu_cycles)",
        "kernels": {}}
-for name, lst in sorted(agg.items(), key=lambda kv: sum(x["GRBM_GUI_ACTIVE"] for x in kv[1])):
-    n = len(lst)
-    vi = sum(x["SQ_INSTS_VALU"] for x in lst) / n
-    w = sum(x["SQ_WAVES"] for x in lst) / n
-    out["kernels"][name] = {"dispatches": n, "valu_insts": vi, "waves": w,
-                            "gpu_cycles": sum(x["GRBM_GUI_ACTIVE"] for x in lst) / n / 8,
-                            "valu_per_wave": vi / max(w, 1)}
+
+
+def avg(c, name):
+    lst = agg[name].get(c)
+    return sum(lst) / len(lst) if lst else None
+
+
+for name in sorted(agg, key=lambda nm: -(avg("GRBM_GUI_ACTIVE", nm) or 0) * len(agg[nm].get("GRBM_GUI_ACTIVE", [1]))):
+    e = {"dispatches": max(len(x) for x in agg[name].values())}
+    for c in sorted(agg[name]):
+        e[c] = avg(c, name)
+    w = e.get("SQ_WAVES") or 0
+    if e.get("SQ_INSTS_VALU") is not None:
+        e["valu_insts"] = e["SQ_INSTS_VALU"]
+        e["valu_per_wave"] = e["SQ_INSTS_VALU"] / max(w, 1)
+    if e.get("GRBM_GUI_ACTIVE") is not None:
+        e["gpu_cycles"] = e["GRBM_GUI_ACTIVE"] / 8
+    if w:
+        e["waves"] = w
+    wc = e.get("SQ_WAVE_CYCLES")
+    if wc:
+        e["wave_cycles"] = wc * 4 / max(w, 1)
+        for c, key in (("SQ_ACTIVE_INST_ANY", "frac_active"), ("SQ_WAIT_ANY", "frac_wait_any"),
+                       ("SQ_WAIT_INST_ANY", "frac_wait_inst"), ("SQ_ACTIVE_INST_VALU", "frac_valu"),
+                       ("SQ_WAIT_INST_LDS", "frac_wait_lds")):
+            if e.get(c) is not None:
+                e[key] = e[c] / wc
+    out["kernels"][name] = e
 json.dump(out, sys.stdout, indent=1)
 print()
