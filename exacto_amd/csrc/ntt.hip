@@ -741,6 +741,48 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
     if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
 }
 
+// The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread).
+// EXACTO_ASM_TIN = 0: each thread loads its 16 consecutive words (8 x 16 B at a 128-B lane stride:
+// every wave-load touches 64 cache lines); 1: coalesced 8-B loads of element tid + k*T (every
+// wave-load 512 contiguous bytes), transposed through LDS (one store/load pass, one barrier).
+#ifndef EXACTO_ASM_TIN
+#define EXACTO_ASM_TIN 0
+#endif
+template <int N>
+__device__ __forceinline__ void load_rows16(u64 (&x)[16], const u64* __restrict__ src, int tid) {
+    if constexpr (EXACTO_ASM_TIN) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * (N / 16)];
+    } else {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 v = s2[k];
+            x[2 * k] = v.x;
+            x[2 * k + 1] = v.y;
+        }
+    }
+}
+
+// x from load_rows16 -> element 16*tid + k in x[k] (the transpose when EXACTO_ASM_TIN; the LDS
+// image is free until the first round's exchange, which starts with a barrier)
+template <int LOGN>
+__device__ __forceinline__ void rows16_to_inv_layout(u64 (&x)[16], u64* lds, int tid) {
+    if constexpr (EXACTO_ASM_TIN) {
+        int t2 = tid;
+        asm volatile("" : "+v"(t2));
+        lds_store_x<LOGN - 4>(lds, x, t2);
+        lds_barrier();
+        lds_load_x<0>(lds, x, t2);
+    }
+}
+
+template <int LOGN>
+__device__ __forceinline__ void load_inv_input(u64 (&x)[16], const u64* __restrict__ src, u64* lds, int tid) {
+    load_rows16<1 << LOGN>(x, src, tid);
+    rows16_to_inv_layout<LOGN>(x, lds, tid);
+}
+
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(EXACTO_ASM_WAVES)))
 ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
@@ -755,13 +797,7 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
                      (long)sub * N;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     u64 x[16];
-    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const ulonglong2 v = s2[k];
-        x[2 * k] = v.x;
-        x[2 * k + 1] = v.y;
-    }
+    load_inv_input<LOGN>(x, src, lds, tid);
     const AsmK K = make_asmk_inv(P);
     inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), K);
 #pragma unroll
@@ -895,13 +931,19 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     auto mulr = [&](u64 a, u64 b) {
         return ASM ? mulmod_near60(a, b, dq) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
     };
+    // (ASM + EXACTO_ASM_TIN: coalesced operand loads; the pointwise products do not care about the
+    // layout, and the one component is transposed before the rounds)
     auto load = [&](const u64* src, u64 (&v)[16]) {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+        if constexpr (ASM) {
+            load_rows16<N>(v, src, tid);
+        } else {
+            const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const ulonglong2 w = s2[k];
-            v[2 * k] = w.x;
-            v[2 * k + 1] = w.y;
+            for (int k = 0; k < 8; ++k) {
+                const ulonglong2 w = s2[k];
+                v[2 * k] = w.x;
+                v[2 * k + 1] = w.y;
+            }
         }
     };
     u64 x[16], y[16];
@@ -940,6 +982,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         }
     }
     if constexpr (ASM) {
+        rows16_to_inv_layout<LOGN>(x, lds, tid);
         const AsmK AK = make_asmk_inv(P);
         inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {

@@ -30,6 +30,7 @@ for v in "$@"; do
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
     noaddx) build noaddx -DEXACTO_ASM_ADDX=0 ;;
     nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
+    tin) build tin -DEXACTO_ASM_TIN=1 ;;
     pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
     pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;
