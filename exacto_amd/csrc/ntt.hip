@@ -424,9 +424,15 @@ __device__ __forceinline__ void sload_round0_tw(TwPair (&tw)[15], const TwPair* 
 
 // 16 coalesced 8-byte stores per thread: element tid + k*T of dst <- x[k] (byte offsets
 // off[j] = 8*tid + j*4096 with immediate 0 / 2048).  The trailing s_nop keeps hipcc from
-// reusing the data registers before the last store has read them.
+// reusing the data registers before the last store has read them.  The leading s_nop 4: the base
+// address is an SGPR pair, and when hipcc reloads a spilled SGPR right before the statement
+// (v_readlane_b32, a VALU write) a vector-memory read of it needs 5 wait states, which hipcc's
+// hazard recognizer does not insert for an instruction inside inline asm -- without it a build
+// whose spill placement differed (more SGPR spills) stored through a stale base and faulted
+// (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION, round 3).
 __device__ __forceinline__ void store_poly4096(u64* dst, const u64 (&x)[16], const uint32_t (&off)[8]) {
     asm volatile(
+        "s_nop 4\n\t"
         "global_store_dwordx2 %16, %0, %24\n\tglobal_store_dwordx2 %16, %1, %24 offset:2048\n\t"
         "global_store_dwordx2 %17, %2, %24\n\tglobal_store_dwordx2 %17, %3, %24 offset:2048\n\t"
         "global_store_dwordx2 %18, %4, %24\n\tglobal_store_dwordx2 %18, %5, %24 offset:2048\n\t"

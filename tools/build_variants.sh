@@ -12,6 +12,17 @@ build() {  # name, flags...
   $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o \
     $R/build/obj/keygen.o $R/build/obj/plain.o $R/build/obj/ks32.o $OUT/ntt_$name.o -ldl
 }
+# a variant whose generated rounds differ (gen_ntt_asm.py env switches): ntt.hip is compiled from a
+# copy next to the regenerated ntt_asm.inc (quoted includes search the file's own directory first)
+build_gen() {  # name, env assignment
+  local name=$1; shift
+  local D=$OUT/src_$name; mkdir -p $D
+  cp $R/exacto_amd/csrc/ntt.hip $D/
+  env "$@" python3 -c "import sys; sys.path.insert(0, '$R/tools'); import gen_ntt_asm as G; G.OUT = '$D/ntt_asm.inc'; G.main()" > /dev/null
+  $H -I $R/exacto_amd/csrc -c $D/ntt.hip -o $OUT/ntt_$name.o
+  $H --offload-arch=gfx950 -shared -fPIC -o $OUT/$name.so $R/build/obj/context.o $R/build/obj/kernels.o \
+    $R/build/obj/keygen.o $R/build/obj/plain.o $R/build/obj/ks32.o $OUT/ntt_$name.o -ldl
+}
 for v in "$@"; do
   case $v in
     base) build base ;;
@@ -31,6 +42,7 @@ for v in "$@"; do
     noaddx) build noaddx -DEXACTO_ASM_ADDX=0 ;;
     nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
     tin) build tin -DEXACTO_ASM_TIN=1 ;;
+    n1shift) build_gen n1shift EXACTO_ASM_N1SHIFT=1 ;;
     pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
     pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;

@@ -60,6 +60,7 @@ W = int(os.environ.get("EXACTO_ASM_STREAMS", "2"))       # butterflies interleav
 SGPR_C = [80, 82, 84, 88, 90, 92][:max(W, 2)]            # carry pair of each stream
 SGPR_SD = 86                  # sink for the carry-out of v_mad_u64_u32 where it is not used
 INV_BOUND_IN = 4              # inverse round 0 input bound (the fused tensor's c1 < 4q)
+N1SHIFT = os.environ.get("EXACTO_ASM_N1SHIFT", "0") == "1"   # qh.lo * n1 by shift + sub (A/B)
 
 
 def v(i):
@@ -175,7 +176,17 @@ def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True, E=None, adde
         Ins(f"v_mad_u64_u32 {F}, {SD}, {yh}, {w0}, {F}", wr=[SD]),
         Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s1}, {A}", wr=[SD]),
         Ins(f"v_mad_u64_u32 {E}, {SD}, {lo(A)}, {st.n0()}, {E}", wr=[SD]),
-        Ins(f"v_mad_u64_u32 {F}, {SD}, {lo(A)}, {st.n1()}, {F}", wr=[SD]),
+    ]
+    if N1SHIFT:
+        # qh.lo * n1 with n1 = 2^32 - 2^28 is -(qh.lo << 28) mod 2^32: a shift and a subtraction
+        # instead of a multiply (B is free once its high word has moved to A.lo)
+        seq += [
+            Ins(f"v_lshlrev_b32 {hi(B)}, 28, {lo(A)}"),
+            Ins(f"v_sub_u32 {lo(F)}, {lo(F)}, {hi(B)}"),
+        ]
+    else:
+        seq.append(Ins(f"v_mad_u64_u32 {F}, {SD}, {lo(A)}, {st.n1()}, {F}", wr=[SD]))
+    seq += [
         Ins(f"v_mad_u64_u32 {F}, {SD}, {hi(A)}, {st.n0()}, {F}", wr=[SD]),
     ]
     if fixup:
