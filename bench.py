@@ -9,8 +9,8 @@ timed region starts.
 
 A step is `reps` passes of the hot path, each over one whole batch (the input batches rotate over
 two resident copies).  `reps` is chosen after the warm-up so that the K timed steps last at least
---min-time seconds (default 2.5 s: the batch-count estimate comes from two untimed batches, so the
-region itself lands at >= 2 s): the BASELINE batch (1024 products, ~2.5 ms) is far shorter than
+--min-time seconds (default 3 s: the batch-count estimate comes from two untimed batches and reads
+high by up to ~35 %, so the region itself lands at >= 2 s): the BASELINE batch (1024 products, ~2.5 ms) is far shorter than
 anything a wall-clock or GPU-busy sampler can see.  value = units processed / timed seconds.
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, no WORLD_SIZE in the
@@ -84,7 +84,7 @@ def parse(argv=None):
     ap.add_argument("--chunk", type=int, default=0, help="products per pipeline chunk (0 = library default)")
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--split", default="batch", choices=("batch", "limbs"))
-    ap.add_argument("--min-time", type=float, default=2.5, help="lower bound of the timed region, seconds")
+    ap.add_argument("--min-time", type=float, default=3.0, help="lower bound of the timed region, seconds")
     ap.add_argument("--reps", type=int, default=0, help="batches per step (0 = from --min-time)")
     ap.add_argument("--dry", action="store_true", help="no HIP calls: CPU/gloo stand-in of the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
