@@ -810,6 +810,104 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
+// ---------------------------------------------------------------- pinned-home rounds
+
+// The generated statements above keep the 16 values of a round in the tied u64 operands x[k] and,
+// because inline asm cannot address the halves of a compiler-allocated 64-bit operand, copy them
+// into a second set of fixed VGPR pairs for the round (32 VGPRs twice over).  The pinned form
+// binds the values to fixed pairs for the whole kernel instead (EXACTO_PIN_DECL: register
+// variables xl_k / xh_k = v[PIN_BASE + 2k], v[PIN_BASE + 2k + 1]; hipcc keeps them there at every
+// statement, and its loads, LDS exchanges and stores use the pairs in place), and the statements
+// (EXACTO_FWD_PIN_*, EXACTO_INV_PIN_*) work on the homes directly: one set of value registers,
+// ~124 VGPRs in all, so four waves per SIMD (n = 8192: two 8-wave workgroups per CU instead of one).
+#define PIN_X16(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+#define PIN_GET(k) (((u64)xh##k << 32) | xl##k)
+#define PIN_SET(k, val)                      \
+    {                                        \
+        const u64 pv_ = (val);               \
+        xl##k = (uint32_t)pv_;               \
+        xh##k = (uint32_t)(pv_ >> 32);       \
+    }
+// LDS exchange of the pinned values: element index of value k is base(tid) ^ (k << LO) (lds_store_x)
+#define PIN_ST1(k) *reinterpret_cast<u64*>(pin_lb + (pin_b ^ (swz((k) << PIN_LO_ST) << 3))) = PIN_GET(k);
+#define PIN_LD1(k) PIN_SET(k, *reinterpret_cast<const u64*>(pin_lbc + (pin_bl ^ (swz((k) << PIN_LO_LD) << 3))))
+#define PIN_EXCHANGE(lds_, tid_, LOST, LOLD)                                           \
+    {                                                                                  \
+        constexpr int PIN_LO_ST = (LOST), PIN_LO_LD = (LOLD);                          \
+        int pin_t2 = (tid_);                                                           \
+        asm volatile("" : "+v"(pin_t2));                                               \
+        lds_barrier();                                                                 \
+        char* pin_lb = reinterpret_cast<char*>(lds_);                                  \
+        const int pin_b = lds_base_bytes<PIN_LO_ST>(pin_t2);                           \
+        PIN_X16(PIN_ST1)                                                               \
+        lds_barrier();                                                                 \
+        const char* pin_lbc = reinterpret_cast<const char*>(lds_);                     \
+        const int pin_bl = lds_base_bytes<PIN_LO_LD>(pin_t2);                          \
+        PIN_X16(PIN_LD1)                                                               \
+    }
+
+#ifndef EXACTO_NTT_PIN
+#define EXACTO_NTT_PIN 1   // 0: launch_ntt's n = 4096 / 8192 asm inverse is ntt_inv_asm_kernel (A/B builds)
+#endif
+
+// Inverse NTT, n = 4096 / 8192, pinned homes: the rounds of ntt_inv_asm_kernel (same twiddles,
+// exchanges, bounds and output layout).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    EXACTO_PIN_DECL
+    {
+        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
+        { const ulonglong2 w_ = s2[0]; PIN_SET(0, w_.x) PIN_SET(1, w_.y) }
+        { const ulonglong2 w_ = s2[1]; PIN_SET(2, w_.x) PIN_SET(3, w_.y) }
+        { const ulonglong2 w_ = s2[2]; PIN_SET(4, w_.x) PIN_SET(5, w_.y) }
+        { const ulonglong2 w_ = s2[3]; PIN_SET(6, w_.x) PIN_SET(7, w_.y) }
+        { const ulonglong2 w_ = s2[4]; PIN_SET(8, w_.x) PIN_SET(9, w_.y) }
+        { const ulonglong2 w_ = s2[5]; PIN_SET(10, w_.x) PIN_SET(11, w_.y) }
+        { const ulonglong2 w_ = s2[6]; PIN_SET(12, w_.x) PIN_SET(13, w_.y) }
+        { const ulonglong2 w_ = s2[7]; PIN_SET(14, w_.x) PIN_SET(15, w_.y) }
+    }
+    const AsmK K = make_asmk_inv(P);
+    const TwTab tab = tw_table(P.tw_inv);
+    {
+        TwPair tw[15];
+        load_round_tw_inv<LOGN, 0, 0, 3>(tw, tid, tab);
+        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_0(tw, K); else EXACTO_INV_PIN_13_0(tw, K);
+    }
+    {
+        TwPair tw[15];
+        load_round_tw_inv<LOGN, 4, 4, 7>(tw, tid, tab);   // in flight across the exchange
+        PIN_EXCHANGE(lds, tid, 0, 4)
+        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_1(tw, K); else EXACTO_INV_PIN_13_1(tw, K);
+    }
+    {
+        TwPair tw[15];
+        load_round_tw_inv<LOGN, 8, 8, (LOGN == 12 ? 11 : 11)>(tw, tid, tab);
+        PIN_EXCHANGE(lds, tid, 4, 8)
+        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_2(tw, K); else EXACTO_INV_PIN_13_2(tw, K);
+    }
+    if constexpr (LOGN == 13) {
+        TwPair tw[15];
+        load_round_tw_inv<13, 9, 12, 12>(tw, tid, tab);
+        PIN_EXCHANGE(lds, tid, 8, 9)
+        EXACTO_INV_PIN_13_3(tw, K);
+    }
+#define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
+    PIN_X16(PIN_OUT)
+#undef PIN_OUT
+}
+
 // ---------------------------------------------------------------- tensor product + inverse
 
 // Degree-2 tensor of two degree-1 ciphertexts fused into the inverse transform of its
@@ -1564,11 +1662,13 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         return;
     }
     if (asm_inv && inverse && logn == 12) {
-        hipLaunchKernelGGL((ntt_inv_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        if (EXACTO_NTT_PIN) hipLaunchKernelGGL((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_inv_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
         return;
     }
     if (asm_inv && inverse && logn == 13) {
-        hipLaunchKernelGGL((ntt_inv_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        if (EXACTO_NTT_PIN) hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_inv_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     if (asm_fwd && !inverse && logn == 13) {

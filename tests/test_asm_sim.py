@@ -24,6 +24,8 @@ def test_rounds_match_exact_arithmetic():
                     q = asm_sim.PRIMES[i % len(asm_sim.PRIMES)]
                     asm_sim.check_round(logn, r, q, rng, approx)
                     asm_sim.check_inv_round(logn, r, q, rng, approx)
+                    asm_sim.check_round_pinned(logn, r, q, rng, approx)
+                    asm_sim.check_inv_round_pinned(logn, r, q, rng, approx)
 
 
 def test_tensor_products_match_exact_arithmetic():

@@ -220,6 +220,55 @@ def check_inv_round(logn, r, q, rng, approx=True):
         assert got[k] < rd.bound_out * q, ("inv bound", logn, r, k, got[k] / q, rd.bound_out)
 
 
+def _run_pinned(rd, x, tw, q, logn):
+    """Run a pinned statement: the values start and end in the home pairs G.PIN_BASE + 2k."""
+    seq = rd.gen()
+    named, n_inv, last_w = _named(rd, [0] * 16, tw, q, logn)
+    lane = Lane(named)
+    for k in range(16):
+        lane.v[G.PIN_BASE + 2 * k] = x[k] & M32
+        lane.v[G.PIN_BASE + 2 * k + 1] = x[k] >> 32
+    for ins in seq:
+        lane.run(ins.text)
+    got = [lane.v[G.PIN_BASE + 2 * k] | (lane.v[G.PIN_BASE + 2 * k + 1] << 32) for k in range(16)]
+    return got, n_inv, last_w
+
+
+def check_round_pinned(logn, r, q, rng, approx=True):
+    rd = G.Round(logn, r, approx, True, pinned=True)
+    bound_in = q if r == 0 else 16 * q
+    x = _inputs(rng, bound_in)
+    tw = [rng.randrange(q) for _ in range(15)]
+    got, _, _ = _run_pinned(rd, x, tw, q, logn)
+    want = [v % q for v in x]
+    for lb, bfs in rd.stages():
+        for k0, k1, slot in bfs:
+            t = want[k1] * tw[slot] % q
+            want[k0], want[k1] = (want[k0] + t) % q, (want[k0] - t) % q
+    for k in range(16):
+        assert got[k] % q == want[k], ("pinned fwd", logn, r, k)
+        assert got[k] < (q if rd.last else rd.bound_out * q), ("pinned fwd bound", logn, r, k, got[k] / q)
+
+
+def check_inv_round_pinned(logn, r, q, rng, approx=True):
+    b = G.inv_rounds_pinned(logn, approx)[r].bound_in
+    rd = G.InvRoundPinned(logn, r, b, approx)
+    x = _inputs(rng, b * q)
+    tw = [rng.randrange(q) for _ in range(15)]
+    got, n_inv, last_w = _run_pinned(rd, x, tw, q, logn)
+    want = [v % q for v in x]
+    for final, bfs in rd.stages():
+        for k0, k1, slot in bfs:
+            u, w_ = want[k0], want[k1]
+            if final:
+                want[k0], want[k1] = (u + w_) * n_inv % q, (u - w_) * last_w % q
+            else:
+                want[k0], want[k1] = (u + w_) % q, (u - w_) * tw[slot] % q
+    for k in range(16):
+        assert got[k] % q == want[k], ("pinned inv", logn, r, k)
+        assert got[k] < rd.bound_out * q, ("pinned inv bound", logn, r, k, got[k] / q)
+
+
 def check_mulpair(w, q, rng):
     """MulNear60Asm<w>: r_k == a_k b_k (mod q) and r_k < 2q for a_k, b_k < q (extremes included)."""
     st = G.MulPair(w)
@@ -257,6 +306,8 @@ def main():
                 for i in range(trials):
                     check_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
                     check_inv_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+                    check_round_pinned(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+                    check_inv_round_pinned(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
     for i in range(trials):
         for w in (1, 2):
             check_mulpair(w, PRIMES[i % 4], rng)

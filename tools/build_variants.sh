@@ -43,6 +43,7 @@ for v in "$@"; do
     nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
     tin) build tin -DEXACTO_ASM_TIN=1 ;;
     n1shift) build_gen n1shift EXACTO_ASM_N1SHIFT=1 ;;
+    nopin) build nopin -DEXACTO_NTT_PIN=0 ;;
     pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
     pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;

@@ -236,12 +236,43 @@ def emit_statement(struct, st, seq, vmax, comment, run_args):
             f"            : {', '.join(clob)});\n    }}\n}};\n")
 
 
+PIN_BASE = int(os.environ.get("EXACTO_PIN_BASE", "72"))   # first home VGPR of the pinned rounds
+
+
+def pin_homes_decl():
+    """The register variables the pinned statements keep their values in (x[k] = xh_k:xl_k)."""
+    decl = ", ".join(f"xl{k} asm(\"v{PIN_BASE + 2 * k}\"), xh{k} asm(\"v{PIN_BASE + 2 * k + 1}\")"
+                     for k in range(16))
+    return f"#define EXACTO_PIN_DECL register uint32_t {decl};\n"
+
+
+def emit_pinned(name, st, seq, vmax, comment):
+    """A pinned round as a macro over the enclosing kernel's register variables xl0..xh15 (bound to
+    the home pairs by EXACTO_PIN_DECL): they are "+v" operands, so hipcc keeps each in its register
+    at the statement, and the body addresses them by their physical names; only the temps are
+    clobbered.  Macro arguments: tw (const TwPair[15]) and K (AsmK)."""
+    seq = pad_hazards(seq)
+    body = "\\n\\t".join(i.text for i in seq)
+    base = PIN_BASE + 32
+    clob = [f'"v{i}"' for i in range(base, vmax)]
+    clob += [f'"s{i}"' for p in SGPR_C + [SGPR_SD] for i in (p, p + 1)]
+    clob.append('"memory"')
+    outs = ", ".join(f'"+v"(xl{k}), "+v"(xh{k})' for k in range(16))
+    ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in st.ins)
+    nops = sum(1 for i in seq if i.text.startswith("s_nop"))
+    valu = sum(1 for i in seq if i.valu)
+    return (f"// {comment}, {valu} VALU, {nops} s_nop\n"
+            f"#define {name}(tw, K) \\\n"
+            f"    asm volatile(\"{body}\" \\\n        : {outs} \\\n        : {ins} \\\n"
+            f"        : {', '.join(clob)})\n")
+
+
 class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
-    def __init__(self, logn, r, approx=True, addx=True):
+    def __init__(self, logn, r, approx=True, addx=True, pinned=False):
         super().__init__()
-        self.logn, self.r, self.approx, self.addx = logn, r, approx, addx
+        self.logn, self.r, self.approx, self.addx, self.pinned = logn, r, approx, addx, pinned
         self.c = 3 if approx else 2            # Shoup output bound (units of q)
         self.lo = max(logn - 4 * (r + 1), 0)
         self.bhi = logn - 1 - 4 * r
@@ -273,8 +304,9 @@ class Round(Statement):
         return res
 
     def gen(self):
-        P = [VBASE + 2 * k for k in range(16)]
-        TB = VBASE + 32
+        base = PIN_BASE if self.pinned else VBASE
+        P = [base + 2 * k for k in range(16)]
+        TB = base + 32
         # 10 VGPRs per stream: Z (Z.hi stays 0), A (= D = qh), B (then cq - T), E (T), F (cross chain)
         temps = [dict(Z=TB + 10 * j, A=TB + 10 * j + 2, B=TB + 10 * j + 4, E=TB + 10 * j + 6,
                       F=TB + 10 * j + 8) for j in range(max(W, 2))]
@@ -290,8 +322,10 @@ class Round(Statement):
         if nstage < 2 and not self.last:
             raise SystemExit("single-stage non-final round not supported")
         first_lb = st[0][0]
-        xop = {k: f"%[x{k}]" for k in range(16)}
-        in_p = {k: False for k in range(16)}
+        # pinned: the values live in their home pairs P for the whole kernel (register variables
+        # bound to them), so every stage reads and writes the homes and nothing goes to tied operands
+        xop = {k: (vp(P[k]) if self.pinned else f"%[x{k}]") for k in range(16)}
+        in_p = {k: self.pinned for k in range(16)}
 
         if self.r > 0:   # round-start reduction of the first stage's X values into P
             red = [k for k in range(16) if not (k >> first_lb) & 1]
@@ -299,12 +333,13 @@ class Round(Statement):
             for i, k in enumerate(red):
                 j = i % len(temps)
                 t = temps[j]
-                streams[j] += reduce_seq(self, vp(P[k]), xop[k], self.xh(k), v(t["B"]), v(t["B"] + 1))
+                src_hi = v(P[k] + 1) if self.pinned else self.xh(k)
+                streams[j] += reduce_seq(self, vp(P[k]), xop[k], src_hi, v(t["B"]), v(t["B"] + 1))
                 in_p[k] = True
             seq += interleave(streams)
 
         for si, (lb, bfs) in enumerate(st):
-            direct_out = si == nstage - 1 and not self.last
+            direct_out = si == nstage - 1 and not self.last and not self.pinned
             for pi in range(0, len(bfs), W):
                 streams = []
                 for j, (k0, k1, slot) in enumerate(bfs[pi:pi + W]):
@@ -366,6 +401,10 @@ class Round(Statement):
 
     def emit(self):
         seq = self.gen()
+        if self.pinned:
+            return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
+                               f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes: "
+                               f"stage bits {self.bhi}..{self.lo}")
         return emit_statement(f"FwdRoundAsm<{self.logn}, {self.r}>", self, seq, self.vmax,
                               f"round {self.r} of the {1 << self.logn}-point forward NTT: stage bits "
                               f"{self.bhi}..{self.lo}",
@@ -538,6 +577,84 @@ class InvRound(Statement):
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
 
 
+class InvRoundPinned(InvRound):
+    """An inverse round whose 16 values stay in fixed home pairs (PIN_BASE + 2k): the sum U + V
+    overwrites U's home, the Shoup product of the difference is written straight into V's home (V
+    is consumed by then), reductions are in place.  No renaming, so no value-home pool: the
+    temps are A, B, F, D, E (and Z exact) per stream after the homes."""
+
+    def gen(self):
+        H = [PIN_BASE + 2 * k for k in range(16)]
+        names = "ABFDE" if self.approx else "ZABFDE"
+        TB = PIN_BASE + 32
+        temps = [{n: vp(TB + 2 * (len(names) * j + i)) for i, n in enumerate(names)} for j in range(max(W, 2))]
+        self.vmax = TB + 2 * len(names) * max(W, 2)
+        seq = [Ins("s_nop 1", valu=False)]
+        if not self.approx:
+            for t in temps:
+                seq.append(Ins(f"v_mov_b32 {hi(t['Z'])}, 0"))
+        bnd = {k: self.bound_in for k in range(16)}
+        C = SGPR_C
+        for final, bfs in self.stages():
+            for pi in range(0, len(bfs), W):
+                streams = []
+                for j, (k0, k1, slot) in enumerate(bfs[pi:pi + W]):
+                    t = temps[j]
+                    c = sp(C[j])
+                    s = []
+                    for _ in range(2):
+                        if bnd[k0] + bnd[k1] <= 16:
+                            break
+                        kr = k0 if bnd[k0] >= bnd[k1] else k1
+                        s += reduce_seq(self, vp(H[kr]), vp(H[kr]), v(H[kr] + 1), lo(t["B"]), hi(t["B"]))
+                        bnd[kr] = 2
+                    m = bnd[k1]
+                    U, V, D = vp(H[k0]), vp(H[k1]), t["D"]
+                    s += [
+                        Ins(f"v_lshl_add_u64 {D}, {U}, 0, {self.mq(m)}"),
+                        Ins(f"v_sub_co_u32_e64 {lo(D)}, {c}, {lo(D)}, {lo(V)}", wr=[c]),
+                        Ins(f"v_lshl_add_u64 {U}, {U}, 0, {V}"),
+                        Ins(f"v_subb_co_u32_e64 {hi(D)}, {c}, {hi(D)}, {hi(V)}, {c}", rd=[c], wr=[c]),
+                    ]
+                    if not final:
+                        s += shoup_seq(self, lo(D), hi(D), self.tw(slot, "w0"), self.tw(slot, "w1"),
+                                       self.tw(slot, "s0"), self.tw(slot, "s1"), t, c, self.approx, E=V)
+                        bnd[k0] = bnd[k0] + bnd[k1]
+                        bnd[k1] = self.tb
+                    else:
+                        ex = dict(t)
+                        if self.approx:   # exact Shoup here: B doubles as Z (B.hi = 0 first)
+                            ex["Z"] = t["B"]
+                        for dst, y, w in ((V, D, "l"), (U, U, "n")):
+                            if self.approx:
+                                s.append(Ins(f"v_mov_b32 {hi(t['B'])}, 0"))
+                            wn, sn = ("lw", "ls") if w == "l" else ("ni", "ns")
+                            s += shoup_seq(self, lo(y), hi(y), self.kc(wn + "l"), self.kc(wn + "h"),
+                                           self.kc(sn + "l"), self.kc(sn + "h"), ex, c, False)
+                            s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
+                        bnd[k0] = bnd[k1] = 1
+                    streams.append(s)
+                seq += interleave(streams)
+        self.bound_out = max(bnd.values())
+        return seq
+
+    def emit(self):
+        seq = self.gen()
+        return emit_pinned(f"EXACTO_INV_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
+                           f"round {self.r} of the {1 << self.logn}-point inverse NTT, pinned homes: stage "
+                           f"bits {self.blo}..{self.bhi}, inputs < {self.bound_in}q, outputs < {self.bound_out}q")
+
+
+def inv_rounds_pinned(logn, approx=True):
+    out, b = [], INV_BOUND_IN
+    for r in range((logn + 3) // 4):
+        rd = InvRoundPinned(logn, r, b, approx)
+        rd.gen()
+        out.append(rd)
+        b = rd.bound_out
+    return out
+
+
 def inv_rounds(logn, approx=True):
     """The inverse rounds of one transform, each starting at the previous round's output bound."""
     out, b = [], INV_BOUND_IN
@@ -663,7 +780,7 @@ template <int W> struct MulNear60Asm;
 
 
 def main():
-    parts = [HEADER, MulPair(2).emit(), "\n", MulPair(1).emit(), "\n"]
+    parts = [HEADER, pin_homes_decl(), "\n", MulPair(2).emit(), "\n", MulPair(1).emit(), "\n"]
     for approx in (True, False):
         parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
         for logn in (12, 13):
@@ -675,6 +792,12 @@ def main():
                 parts.append(f"#endif  // {'' if addx else '!'}EXACTO_ASM_ADDX\n\n")
             for rd in inv_rounds(logn, approx):
                 parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
+                parts.append("\n")
+            for r in range((logn + 3) // 4):
+                parts.append(Round(logn, r, approx, True, pinned=True).emit())
+                parts.append("\n")
+            for rd in inv_rounds_pinned(logn, approx):
+                parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
                 parts.append("\n")
         parts.append(f"#endif  // {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
     with open(OUT, "w") as f:
