@@ -118,10 +118,15 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     on = lambda k: env.get(k, "1") != "0"
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
     fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and on("EXACTO_NTT_PIPE")
+           else f"ntt_fwd_pin_kernel<{logn}>" if asm and on("EXACTO_FWD_PIN")
            else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>")
-    inv = f"ntt_inv_asm_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}, true>"
+    # the asm inverse is the pinned-home kernel (ntt.hip EXACTO_NTT_PIN, a build-time switch)
+    inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}, true>"
+    tp = env.get("EXACTO_TENSOR_PIN", "")
+    pin = asm and on("EXACTO_NTT_ASM_INV") and (tp != "0" if tp else logn == 13)
     t3 = env.get("EXACTO_TENSOR3", "1" if logn == 13 else "0") == "1"
-    tensor = f"ntt_inv_tensor3_kernel<{logn}>" if t3 else f"ntt_inv_tensor_kernel<{logn}, true, true>"
+    tensor = (f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor3_kernel<{logn}>" if t3
+              else f"ntt_inv_tensor_kernel<{logn}, true, true>")
     return {0: fwd, 1: inv, 2: tensor, 3: f"ntt_polymul_kernel<{logn}>", 4: f"exact_lift_sp_kernel<{L}>",
             5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
             8: f"ks32_crt_kernel<{logn}, {S}>", 9: "dbfv_pairsum_kernel", 10: f"exact_psum_sp_kernel<{L}>",

@@ -846,6 +846,70 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         PIN_X16(PIN_LD1)                                                               \
     }
 
+// The inverse rounds over the pinned homes (inputs < 4q; output element LAST_LO-layout, canonical):
+// ntt_inv_asm_kernel's twiddles and exchanges.  A macro because the homes are the enclosing
+// kernel's register variables.
+#define PIN_INV_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
+    {                                                                                            \
+        const AsmK pin_K = (K_);                                                                 \
+        const TwTab pin_tab = (tab_);                                                            \
+        {                                                                                        \
+            TwPair tw[15];                                                                       \
+            load_round_tw_inv<LOGN_, 0, 0, 3>(tw, tid_, pin_tab);                                \
+            if constexpr (LOGN_ == 12) EXACTO_INV_PIN_12_0(tw, pin_K); else EXACTO_INV_PIN_13_0(tw, pin_K); \
+        }                                                                                        \
+        {                                                                                        \
+            TwPair tw[15];                                                                       \
+            load_round_tw_inv<LOGN_, 4, 4, 7>(tw, tid_, pin_tab); /* in flight across the exchange */ \
+            PIN_EXCHANGE(lds_, tid_, 0, 4)                                                       \
+            if constexpr (LOGN_ == 12) EXACTO_INV_PIN_12_1(tw, pin_K); else EXACTO_INV_PIN_13_1(tw, pin_K); \
+        }                                                                                        \
+        {                                                                                        \
+            TwPair tw[15];                                                                       \
+            load_round_tw_inv<LOGN_, 8, 8, 11>(tw, tid_, pin_tab);                               \
+            PIN_EXCHANGE(lds_, tid_, 4, 8)                                                       \
+            if constexpr (LOGN_ == 12) EXACTO_INV_PIN_12_2(tw, pin_K); else EXACTO_INV_PIN_13_2(tw, pin_K); \
+        }                                                                                        \
+        if constexpr (LOGN_ == 13) {                                                             \
+            TwPair tw[15];                                                                       \
+            load_round_tw_inv<13, 9, 12, 12>(tw, tid_, pin_tab);                                 \
+            PIN_EXCHANGE(lds_, tid_, 8, 9)                                                       \
+            EXACTO_INV_PIN_13_3(tw, pin_K);                                                      \
+        }                                                                                        \
+    }
+
+// The forward rounds over the pinned homes (canonical inputs, element tid + k T; canonical outputs,
+// element 16 tid + k): ntt_fwd_asm_kernel's twiddles and exchanges.
+#define PIN_FWD_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
+    {                                                                                            \
+        const AsmK pin_K = (K_);                                                                 \
+        const TwTab pin_tab = (tab_);                                                            \
+        {                                                                                        \
+            TwPair tw[15];                                                                       \
+            load_round_tw<LOGN_, LOGN_ - 4, LOGN_ - 1, LOGN_ - 4>(tw, tid_, pin_tab);            \
+            if constexpr (LOGN_ == 12) EXACTO_FWD_PIN_12_0(tw, pin_K); else EXACTO_FWD_PIN_13_0(tw, pin_K); \
+        }                                                                                        \
+        {                                                                                        \
+            TwPair tw[15];                                                                       \
+            load_round_tw<LOGN_, LOGN_ - 8, LOGN_ - 5, LOGN_ - 8>(tw, tid_, pin_tab);            \
+            PIN_EXCHANGE(lds_, tid_, LOGN_ - 4, LOGN_ - 8)                                       \
+            if constexpr (LOGN_ == 12) EXACTO_FWD_PIN_12_1(tw, pin_K); else EXACTO_FWD_PIN_13_1(tw, pin_K); \
+        }                                                                                        \
+        {                                                                                        \
+            constexpr int pin_lo = LOGN_ == 12 ? 0 : 1;                                          \
+            TwPair tw[15];                                                                       \
+            load_round_tw<LOGN_, pin_lo, LOGN_ - 9, pin_lo>(tw, tid_, pin_tab);                  \
+            PIN_EXCHANGE(lds_, tid_, LOGN_ - 8, pin_lo)                                          \
+            if constexpr (LOGN_ == 12) EXACTO_FWD_PIN_12_2(tw, pin_K); else EXACTO_FWD_PIN_13_2(tw, pin_K); \
+        }                                                                                        \
+        if constexpr (LOGN_ == 13) {                                                             \
+            TwPair tw[15];                                                                       \
+            load_round_tw<13, 0, 0, 0>(tw, tid_, pin_tab);                                       \
+            PIN_EXCHANGE(lds_, tid_, 1, 0)                                                       \
+            EXACTO_FWD_PIN_13_3(tw, pin_K);                                                      \
+        }                                                                                        \
+    }
+
 #ifndef EXACTO_NTT_PIN
 #define EXACTO_NTT_PIN 1   // 0: launch_ntt's n = 4096 / 8192 asm inverse is ntt_inv_asm_kernel (A/B builds)
 #endif
@@ -878,32 +942,44 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         { const ulonglong2 w_ = s2[6]; PIN_SET(12, w_.x) PIN_SET(13, w_.y) }
         { const ulonglong2 w_ = s2[7]; PIN_SET(14, w_.x) PIN_SET(15, w_.y) }
     }
-    const AsmK K = make_asmk_inv(P);
-    const TwTab tab = tw_table(P.tw_inv);
-    {
-        TwPair tw[15];
-        load_round_tw_inv<LOGN, 0, 0, 3>(tw, tid, tab);
-        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_0(tw, K); else EXACTO_INV_PIN_13_0(tw, K);
-    }
-    {
-        TwPair tw[15];
-        load_round_tw_inv<LOGN, 4, 4, 7>(tw, tid, tab);   // in flight across the exchange
-        PIN_EXCHANGE(lds, tid, 0, 4)
-        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_1(tw, K); else EXACTO_INV_PIN_13_1(tw, K);
-    }
-    {
-        TwPair tw[15];
-        load_round_tw_inv<LOGN, 8, 8, (LOGN == 12 ? 11 : 11)>(tw, tid, tab);
-        PIN_EXCHANGE(lds, tid, 4, 8)
-        if constexpr (LOGN == 12) EXACTO_INV_PIN_12_2(tw, K); else EXACTO_INV_PIN_13_2(tw, K);
-    }
-    if constexpr (LOGN == 13) {
-        TwPair tw[15];
-        load_round_tw_inv<13, 9, 12, 12>(tw, tid, tab);
-        PIN_EXCHANGE(lds, tid, 8, 9)
-        EXACTO_INV_PIN_13_3(tw, K);
-    }
+    PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
 #define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
+    PIN_X16(PIN_OUT)
+#undef PIN_OUT
+}
+
+// Forward NTT, n = 4096 / 8192, pinned homes: ntt_fwd_asm_kernel's rounds, exchanges and
+// coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64 q = P.q;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    EXACTO_PIN_DECL
+    if (nb.src16) {
+        const int16_t* s16 = nb.src16 + (long)item * nb.src16_item_stride + (long)(sub / nb.period) * N + tid;
+#define PIN_IN16(k) { const i64 d_ = s16[(k) * T]; PIN_SET(k, d_ < 0 ? q + (u64)d_ : (u64)d_) }
+        PIN_X16(PIN_IN16)
+#undef PIN_IN16
+    } else {
+        const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                         (long)sub * N + tid;
+#define PIN_IN64(k) PIN_SET(k, src[(k) * T])
+        PIN_X16(PIN_IN64)
+#undef PIN_IN64
+    }
+    PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q))
+    // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
+    PIN_EXCHANGE(lds, tid, 0, LOGN - 4)
+#define PIN_OUT(k) dst[tid + (k) * T] = PIN_GET(k);
     PIN_X16(PIN_OUT)
 #undef PIN_OUT
 }
@@ -1095,6 +1171,83 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
+// The tensor kernel over pinned homes (n = 4096 / 8192, special primes): the products
+// (MulNear60PinAsm: temps v44-v71, below the homes; < 2q, c1 < 4q) go straight into the homes, and the inverse rounds are
+// PIN_INV_ROUNDS -- one set of value registers, four waves per SIMD (n = 8192: two 8-wave
+// workgroups per CU).  Same blocks, remap and p2only as ntt_inv_tensor_kernel.
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
+                          const PrimeConst* __restrict__ primes, int remap, int p2only) {
+    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int NP = L + K;
+    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
+    const int per = p2only ? 3 * L + K : 3 * NP;
+    const long item = p / per;
+    const int rem = (int)(p - item * per);
+    const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);
+    const int c = (!p2only || rem < 3 * L) ? rem - t * 3 : 2;
+    const PrimeConst& P = primes[t];
+    const u64 *A0, *A1, *B0, *B1;
+    if (t < L) {
+        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
+        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
+        A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
+        B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
+    } else if (op.ea) {
+        const u64* EA = op.ea + (long)op.ea_off[item] + (long)(t - L) * N;
+        const u64* EB = op.eb + (long)op.eb_off[item] + (long)(t - L) * N;
+        A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
+    } else {
+        const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
+        A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
+    }
+    const uint32_t dq = (uint32_t)((1ull << 60) - P.q), e16 = 16 * dq;
+    EXACTO_PIN_DECL
+    if (c != 1) {
+        const ulonglong2* sa = reinterpret_cast<const ulonglong2*>((c == 0 ? A0 : A1) + 16 * tid);
+        const ulonglong2* sb = reinterpret_cast<const ulonglong2*>((c == 0 ? B0 : B1) + 16 * tid);
+#define PIN_T1(e, k0, k1)                                                \
+        {                                                          \
+            const ulonglong2 u_ = sa[e], v_ = sb[e];               \
+            u64 r0_, r1_;                                          \
+            MulNear60PinAsm<2>::run(r0_, r1_, u_.x, v_.x, u_.y, v_.y, dq, e16);   \
+            PIN_SET(k0, r0_) PIN_SET(k1, r1_)                      \
+        }
+        PIN_T1(0, 0, 1) PIN_T1(1, 2, 3) PIN_T1(2, 4, 5) PIN_T1(3, 6, 7)
+        PIN_T1(4, 8, 9) PIN_T1(5, 10, 11) PIN_T1(6, 12, 13) PIN_T1(7, 14, 15)
+#undef PIN_T1
+    } else {
+        const ulonglong2* sa0 = reinterpret_cast<const ulonglong2*>(A0 + 16 * tid);
+        const ulonglong2* sa1 = reinterpret_cast<const ulonglong2*>(A1 + 16 * tid);
+        const ulonglong2* sb0 = reinterpret_cast<const ulonglong2*>(B0 + 16 * tid);
+        const ulonglong2* sb1 = reinterpret_cast<const ulonglong2*>(B1 + 16 * tid);
+#define PIN_T2(e, k0, k1)                                                \
+        {                                                          \
+            const ulonglong2 u0_ = sa0[e], v1_ = sb1[e];           \
+            const ulonglong2 u1_ = sa1[e], v0_ = sb0[e];           \
+            u64 r0_, r1_, s0_, s1_;                                \
+            MulNear60PinAsm<2>::run(r0_, r1_, u0_.x, v1_.x, u0_.y, v1_.y, dq, e16); \
+            MulNear60PinAsm<2>::run(s0_, s1_, u1_.x, v0_.x, u1_.y, v0_.y, dq, e16); \
+            PIN_SET(k0, r0_ + s0_) PIN_SET(k1, r1_ + s1_)          \
+        }
+        // two halves of 16 loads each: hoisting all 32 (128 VGPRs) past the products would spill
+        PIN_T2(0, 0, 1) PIN_T2(1, 2, 3) PIN_T2(2, 4, 5) PIN_T2(3, 6, 7)
+        __builtin_amdgcn_sched_barrier(0);
+        PIN_T2(4, 8, 9) PIN_T2(5, 10, 11) PIN_T2(6, 12, 13) PIN_T2(7, 14, 15)
+#undef PIN_T2
+    }
+    PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
+    u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
+#define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
+    PIN_X16(PIN_OUT)
+#undef PIN_OUT
 }
 
 // ---------------------------------------------------------------- fused product + inverse
@@ -1568,7 +1721,27 @@ static bool tensor3_at(int logn) {
     return t3env >= 0 ? t3env == 1 : logn == 13;
 }
 
-bool inverse_tensor_split(int logn) { return (logn == 12 || logn == 13) && tensor3_at(logn); }
+// pinned-home kernels (runtime A/B switches, read once).  Tensor: ntt_inv_tensor_pin_kernel at
+// n = 8192 replaces tensor3 + tensor_c2 (cfg5 1996 -> 2175 chains/s, same box); at n = 4096 the
+// 3-wave ntt_inv_tensor_kernel stays (pinned 297-302 vs 295-296 us per cfg3 launch).
+// EXACTO_TENSOR_PIN=0: never, =1: at both sizes.  EXACTO_FWD_PIN=0: the forward
+// ntt_fwd_asm_kernel instead of ntt_fwd_pin_kernel (n = 8192: 41 -> 33 us per cfg5 launch).
+static int env_switch(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && e[0] ? (e[0] != '0') : dflt;
+}
+static bool tensor_pin_at(int logn) {
+    static const int on = env_switch("EXACTO_TENSOR_PIN", -1);
+    return on < 0 ? logn == 13 : on && (logn == 12 || logn == 13);
+}
+static bool fwd_pin() {
+    static const int on = env_switch("EXACTO_FWD_PIN", 1);
+    return on;
+}
+
+bool inverse_tensor_split(int logn) {
+    return (logn == 12 || logn == 13) && !tensor_pin_at(logn) && tensor3_at(logn);
+}
 
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
@@ -1578,6 +1751,12 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
     const bool t3 = tensor3_at(LOGN);
     if constexpr (LOGN == 12 || LOGN == 13) {
+        if (asm_inv && tensor_pin_at(LOGN)) {
+            const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
+            hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L, K,
+                               primes, remap, p2only);
+            return;
+        }
         if (asm_inv && t3) {
             // blocks = items * 3 (L + K); psum: the ciphertext primes here, the auxiliary c2 apart
             const long items = blocks / (3 * (L + K));
@@ -1658,7 +1837,8 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         return;
     }
     if (asm_fwd && !inverse && logn == 12) {
-        hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        if (fwd_pin()) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
         return;
     }
     if (asm_inv && inverse && logn == 12) {
@@ -1672,7 +1852,8 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         return;
     }
     if (asm_fwd && !inverse && logn == 13) {
-        hipLaunchKernelGGL((ntt_fwd_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        if (fwd_pin()) hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_fwd_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     switch (logn) {

@@ -677,9 +677,14 @@ class MulPair(Statement):
     9 slow (8 mads, alignbit) + 6 fast instructions per product instead of the ~26 hipcc emits for
     the same C++ (mulmod_near60)."""
 
-    def __init__(self, w=2):
+    def __init__(self, w=2, base=None, struct="MulNear60Asm", volatile=True):
         super().__init__()
         self.w = w
+        # non-volatile: a pure function of its operands, so the scheduler may move loads across it
+        # (an asm volatile statement is a scheduling barrier for every memory access)
+        self.volatile = volatile
+        self.base = VBASE if base is None else base
+        self.struct = struct
 
     def a(self, k, h): return self._in(f"a{k}{h}", "v", f"(uint32_t)(a{k} >> {32 if h == 'h' else 0})")
     def b(self, k, h): return self._in(f"b{k}{h}", "v", f"(uint32_t)(b{k} >> {32 if h == 'h' else 0})")
@@ -691,7 +696,7 @@ class MulPair(Statement):
         streams = []
         seq = [Ins("s_nop 1", valu=False)]
         for k in range(self.w):
-            base = VBASE + 14 * k
+            base = self.base + 14 * k
             T, Z, M, H, S, Wp = (vp(base + 2 * i) for i in range(6))
             U = v(base + 12)
             R = f"%[r{k}]"
@@ -714,13 +719,13 @@ class MulPair(Statement):
                 Ins(f"v_and_b32 {hi(S)}, 0x0fffffff, {lo(Wp)}"),
                 Ins(f"v_mad_u64_u32 {R}, {SD}, {U}, {self.d()}, {S}", wr=[SD]),
             ])
-        self.vmax = VBASE + 14 * self.w
+        self.vmax = self.base + 14 * self.w
         return seq + interleave(streams)
 
     def emit(self):
         seq = pad_hazards(self.gen())
         body = "\\n\\t".join(i.text for i in seq)
-        clob = [f'"v{i}"' for i in range(VBASE, self.vmax)] + [f'"s{SGPR_SD}"', f'"s{SGPR_SD + 1}"']
+        clob = [f'"v{i}"' for i in range(self.base, self.vmax)] + [f'"s{SGPR_SD}"', f'"s{SGPR_SD + 1}"']
         outs = ", ".join(f'[r{k}] "=&v"(r{k})' for k in range(self.w))
         ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in self.ins)
         args = ", ".join([f"u64& r{k}" for k in range(self.w)] + [f"u64 a{k}, u64 b{k}" for k in range(self.w)] +
@@ -728,9 +733,9 @@ class MulPair(Statement):
         valu = sum(1 for i in seq if i.valu)
         nops = sum(1 for i in seq if i.text.startswith("s_nop"))
         return (f"// {self.w} products mod 2^60 - d (< 2q), {valu} VALU, {nops} s_nop\n"
-                f"template <> struct MulNear60Asm<{self.w}> {{\n"
+                f"template <> struct {self.struct}<{self.w}> {{\n"
                 f"    static __device__ __forceinline__ void run({args}) {{\n"
-                f"        asm volatile(\"{body}\"\n            : {outs}\n            : {ins}\n"
+                f"        asm{' volatile' if self.volatile else ''}(\"{body}\"\n            : {outs}\n            : {ins}\n"
                 f"            : {', '.join(clob)});\n    }}\n}};\n")
 
 
@@ -775,12 +780,14 @@ __device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
 template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
 template <int W> struct MulNear60Asm;
+template <int W> struct MulNear60PinAsm;   // temps below the pinned homes (kernels with EXACTO_PIN_DECL)
 
 """
 
 
 def main():
-    parts = [HEADER, pin_homes_decl(), "\n", MulPair(2).emit(), "\n", MulPair(1).emit(), "\n"]
+    parts = [HEADER, pin_homes_decl(), "\n", MulPair(2).emit(), "\n", MulPair(1).emit(), "\n",
+             MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinAsm", volatile=False).emit(), "\n"]
     for approx in (True, False):
         parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
         for logn in (12, 13):
