@@ -117,7 +117,7 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     logn = n.bit_length() - 1
     on = lambda k: env.get(k, "1") != "0"
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and on("EXACTO_NTT_PIPE")
+    fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and env.get("EXACTO_NTT_PIPE", "0") != "0"
            else f"ntt_fwd_pin_kernel<{logn}>" if asm and on("EXACTO_FWD_PIN")
            else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>")
     # the asm inverse is the pinned-home kernel (ntt.hip EXACTO_NTT_PIN, a build-time switch)

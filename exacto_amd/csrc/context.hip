@@ -213,7 +213,10 @@ struct exacto_ctx {
     bool rlk_s_valid = false;
     bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
-    bool ntt_pipe = true;   // EXACTO_NTT_PIPE=0: one workgroup per polynomial instead of the persistent LDS-DMA kernel
+    // EXACTO_NTT_PIPE=1: the persistent LDS-DMA forward kernel at n = 4096 instead of the pinned-home
+    // one-workgroup-per-polynomial kernel (same box: 117-118 vs 108-109 us per cfg3 launch, the step
+    // within 0.3 %)
+    bool ntt_pipe = false;
     bool ntt_asm_inv = true;  // EXACTO_NTT_ASM_INV=0: compiler-scheduled inverse NTT (A/B)
     // relinearisation MAC in an auxiliary basis of S 31-bit primes (ks32.hip; EXACTO_KS32=0: the
     // limb-wise 60-bit digit NTTs + relin_mac)

@@ -1,5 +1,5 @@
-"""The persistent LDS-DMA forward NTT (ntt_fwd_pipe_kernel, n = 4096) against the oracle and
-against the one-workgroup-per-polynomial kernel it replaces (EXACTO_NTT_PIPE=0), on batches
+"""The persistent LDS-DMA forward NTT (ntt_fwd_pipe_kernel, n = 4096, EXACTO_NTT_PIPE=1) against the
+oracle and against the default one-workgroup-per-polynomial kernel (ntt_fwd_pin_kernel), on batches
 large enough that every resident workgroup streams several polynomials through its LDS
 halves, with mixed primes, and on the int16 gadget-digit source of bfv_mul_and_relin.
 

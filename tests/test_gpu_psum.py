@@ -134,3 +134,33 @@ def test_dbfv_item_groups_match_one_pass(gpu_available, chain):
         else:
             outs.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_psum_cfg5_two_halves_vs_limbwise(gpu_available):
+    """The cfg5 bench path as it runs by default -- psum, int8 digit sums, the ks32 digit-sum key
+    switch, and a batch that fits one chunk split into two halves on both pipeline lanes (B = 4:
+    144 products, 2 x 72) -- against the other key-switch formulation: 60-bit limb-wise MAC
+    (EXACTO_KS32=0) and per-product scaling summed by dbfv_combine (EXACTO_PSUM=0)."""
+    dp = P.cfg5_params(8192)
+    prm = dp.bfv_params
+    q, n, d, B = prm.ct_basis.moduli, 8192, dp.num_digits, 4
+    rng = np.random.default_rng(5252)
+    a = uniform_residues(rng, (B, d, 2), q, n)
+    b = uniform_residues(rng, (B, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    outs = []
+    for envs in ({}, {"EXACTO_KS32": "0", "EXACTO_PSUM": "0"}):
+        old = {k: os.environ.get(k) for k in envs}
+        os.environ.update(envs)
+        try:
+            ctx = HipContext.from_params(prm, device=0)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
+        assert (ctx.psum_max >= 8) if not envs else ctx.psum_max == 0
+        ctx.load_relin_key(rlk)
+        outs.append(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+    assert np.array_equal(outs[0], outs[1])
