@@ -127,7 +127,9 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     t3 = env.get("EXACTO_TENSOR3", "1" if logn == 13 else "0") == "1"
     tensor = (f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor3_kernel<{logn}>" if t3
               else f"ntt_inv_tensor_kernel<{logn}, true, true>")
-    return {0: fwd, 1: inv, 2: tensor, 3: f"ntt_polymul_kernel<{logn}>", 4: f"exact_lift_sp_kernel<{L}>",
+    polymul = (f"ntt_polymul_pin_kernel<{logn}>" if env.get("EXACTO_POLYMUL_PIN", "0") == "1"
+               else f"ntt_polymul_kernel<{logn}>")
+    return {0: fwd, 1: inv, 2: tensor, 3: polymul, 4: f"exact_lift_sp_kernel<{L}>",
             5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
             8: f"ks32_crt_kernel<{logn}, {S}>", 9: "dbfv_pairsum_kernel", 10: f"exact_psum_sp_kernel<{L}>",
             11: f"ntt_inv_tensor_c2_kernel<{logn}>", 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel"}

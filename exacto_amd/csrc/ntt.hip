@@ -1373,6 +1373,96 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = xa[k];
 }
 
+// Buffer-resource row access for the pinned kernels: one block-uniform descriptor (SGPRs) per
+// polynomial, one shared lane offset (VGPR) and a per-row SGPR/constant offset, so that the 16 rows
+// of a thread cost no per-lane 64-bit pointers (which do not fit beside the homes).
+typedef __amdgpu_buffer_rsrc_t BufRes;
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ BufRes poly_res(const u64* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64*>(p), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x2v bld64(BufRes r, int voff, int soff) {
+    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+}
+__device__ __forceinline__ void bst64(uint32_t lo, uint32_t hi, BufRes r, int voff, int soff) {
+    u32x2v v;
+    v.x = lo;
+    v.y = hi;
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
+}
+
+// ntt_polymul_kernel over pinned homes, four waves per SIMD: a is transformed in the homes and its
+// evaluations parked in the block's own output rows (coalesced; this thread's words only, read back
+// by the same thread, so no barrier: the L2 usually still holds them), then b is transformed, a's
+// evaluations are read back, the product formed into the homes (MulNear60PinAsm, < 2q) and
+// inverse-transformed over the parked words.  One set of values in registers instead of two (the
+// register-resident form holds 32 more VGPRs and spills at three waves per SIMD).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ntt_polymul_pin_kernel(const u64* A, const u64* B, u64* out, int period, const PrimeConst* __restrict__ primes) {
+    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const long p = blockIdx.x;
+    const PrimeConst& P = primes[(int)(blockIdx.x % (unsigned)period)];
+    const u64 q = P.q;
+    const BufRes ra = poly_res(A + p * N, N * 8), rb = poly_res(B + p * N, N * 8), ro = poly_res(out + p * N, N * 8);
+    const int vrow = 8 * tid;                                  // element tid + k T: soffset 8 k T
+    EXACTO_PIN_DECL
+#define PIN_INA(k) { const u32x2v v_ = bld64(ra, vrow, 8 * (k) * T); xl##k = v_.x; xh##k = v_.y; }
+    PIN_X16(PIN_INA)
+#undef PIN_INA
+    const AsmK K = make_asmk(q);
+    const TwTab tf = tw_table(P.tw_fwd);
+    PIN_FWD_ROUNDS(LOGN, lds, tid, tf, K)
+#define PIN_PARK(k) bst64(xl##k, xh##k, ro, vrow, 8 * (k) * T);
+    PIN_X16(PIN_PARK)
+#undef PIN_PARK
+#define PIN_INB(k) { const u32x2v v_ = bld64(rb, vrow, 8 * (k) * T); xl##k = v_.x; xh##k = v_.y; }
+    PIN_X16(PIN_INB)
+#undef PIN_INB
+    // a fresh copy of tid for b's rounds: otherwise hipcc keeps a's twiddle addresses live (spilled)
+    int tid2 = tid;
+    asm volatile("" : "+v"(tid2));
+    PIN_FWD_ROUNDS(LOGN, lds, tid2, tf, K)
+    const uint32_t dq = (uint32_t)((1ull << 60) - q), e16 = 16 * dq;
+    // products in two halves: 8 parked words loaded together, then four ordered (volatile) product
+    // pairs into the homes; the statements also fence the inverse's twiddle loads below them
+#define PIN_LDP(k) const u32x2v u##k##_ = bld64(ro, vrow, 8 * (k) * T);
+#define PIN_MUL(k0, k1)                                                                              \
+    {                                                                                                \
+        u64 r0_, r1_;                                                                                \
+        MulNear60PinVAsm<2>::run(r0_, r1_, ((u64)u##k0##_.y << 32) | u##k0##_.x, PIN_GET(k0),        \
+                                 ((u64)u##k1##_.y << 32) | u##k1##_.x, PIN_GET(k1), dq, e16);        \
+        PIN_SET(k0, r0_) PIN_SET(k1, r1_)                                                            \
+    }
+    {
+        PIN_LDP(0) PIN_LDP(1) PIN_LDP(2) PIN_LDP(3) PIN_LDP(4) PIN_LDP(5) PIN_LDP(6) PIN_LDP(7)
+        PIN_MUL(0, 1) PIN_MUL(2, 3) PIN_MUL(4, 5) PIN_MUL(6, 7)
+    }
+    {
+        PIN_LDP(8) PIN_LDP(9) PIN_LDP(10) PIN_LDP(11) PIN_LDP(12) PIN_LDP(13) PIN_LDP(14) PIN_LDP(15)
+        PIN_MUL(8, 9) PIN_MUL(10, 11) PIN_MUL(12, 13) PIN_MUL(14, 15)
+    }
+#undef PIN_MUL
+#undef PIN_LDP
+    int tid3 = tid;
+    asm volatile("" : "+v"(tid3));
+    // the twiddle table is read-only memory, whose loads move freely; an opaque copy of the pointer
+    // defined here keeps them below the products
+    const TwPair* ti = P.tw_inv;
+    asm volatile("" : "+s"(ti));
+    PIN_INV_ROUNDS(LOGN, lds, tid3, tw_table(ti), make_asmk_inv(P))
+    // element elem_index<LAST_LO>(tid, k) = base(tid) | k << LAST_LO
+    const int vout = 8 * elem_index<LAST_LO>(tid3, 0);
+#define PIN_OUT(k) bst64(xl##k, xh##k, ro, vout, 8 * ((k) << LAST_LO));
+    PIN_X16(PIN_OUT)
+#undef PIN_OUT
+}
+
 // The key switch's lift (ks32_crt_values: S inverse 32-bit transforms, centred Garner lift, + the
 // scaled component) and the forward 60-bit transform of the result in one workgroup per (item, c,
 // l): the coefficient-domain relinearised component never goes to HBM and back (bfv_mul_and_relin's
@@ -1426,7 +1516,16 @@ bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, in
 
 bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,
                     hipStream_t s) {
-    if (logn == 12)
+    // EXACTO_POLYMUL_PIN=1: the pinned form (4 waves per SIMD, a parked in out's rows) instead of
+    // ntt_polymul_kernel (2 waves): measured slower, 866-876 vs 806 us per cfg2 launch (same box), so
+    // off.  It parks a's evaluations before it reads b: never when out is b (in place on b).
+    static const bool pin_env = [] { const char* e = std::getenv("EXACTO_POLYMUL_PIN"); return e && e[0] == '1'; }();
+    const bool pin = pin_env && out != B;
+    if (pin && logn == 12)
+        hipLaunchKernelGGL(ntt_polymul_pin_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
+    else if (pin && logn == 13)
+        hipLaunchKernelGGL(ntt_polymul_pin_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
+    else if (logn == 12)
         hipLaunchKernelGGL(ntt_polymul_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
     else if (logn == 13)
         hipLaunchKernelGGL(ntt_polymul_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);

@@ -274,7 +274,32 @@ static int bootstrap_case() {
     return 0;
 }
 
+// diagnostic: the bootstrap of trivial ciphertexts repeated in one process; counts wrong decodes and
+// outputs that differ from the first repetition (the computation is deterministic)
+static int boot_repro(int reps) {
+    auto orig = BfvParamsBuilder().ring_degree(16).plain_modulus(5).ct_moduli({65537ull}).sigma(3.2).build();
+    auto boot = BfvParamsBuilder().ring_degree(16).plain_modulus(29).ct_moduli({1125899906842817ull}).sigma(3.2)
+                    .gadget_base(8).build();
+    ChaChaRng rng(42);
+    auto sko = gen_secret_key_with_rng(orig, rng);
+    auto bsk = gen_bootstrap_key(sko, boot, 25, 5, rng);
+    std::vector<std::vector<uint64_t>> first(5);
+    int wrong = 0, differ = 0;
+    for (int r = 0; r < reps; ++r)
+        for (uint64_t v = 0; v < 5; ++v) {
+            auto out = bfv_bootstrap(trivial_encrypt(v, orig), bsk);
+            std::vector<uint64_t> flat;
+            for (auto& p : out.c) flat.insert(flat.end(), p.data.begin(), p.data.end());
+            if (r == 0) first[v] = flat;
+            else if (flat != first[v]) ++differ;
+            if (decode_scalar(decrypt(out, bsk.boot_sk)) % 5 != v) ++wrong;
+        }
+    std::printf("boot_repro reps=%d wrong=%d differ=%d\n", reps, wrong, differ);
+    return wrong || differ;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 3 && std::string(argv[1]) == "--boot-reps") return boot_repro(std::atoi(argv[2]));
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <fixture-dir> <case>...\n", argv[0]);
         return 2;

@@ -781,13 +781,15 @@ template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
 template <int W> struct MulNear60Asm;
 template <int W> struct MulNear60PinAsm;   // temps below the pinned homes (kernels with EXACTO_PIN_DECL)
+template <int W> struct MulNear60PinVAsm;  // ... as asm volatile (ordered with fences and other statements)
 
 """
 
 
 def main():
     parts = [HEADER, pin_homes_decl(), "\n", MulPair(2).emit(), "\n", MulPair(1).emit(), "\n",
-             MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinAsm", volatile=False).emit(), "\n"]
+             MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinAsm", volatile=False).emit(), "\n",
+             MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinVAsm").emit(), "\n"]
     for approx in (True, False):
         parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
         for logn in (12, 13):
