@@ -354,12 +354,26 @@ struct Scratch {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Every device allocation of the library.  EXACTO_DEBUG_FILL=1 (read once): new blocks are filled
+// with 0xA5 bytes, so that a kernel reading memory nothing wrote sees garbage at once instead of the
+// zeros of fresh pages (a read of that kind passed in a fresh process and failed after other work
+// had freed and re-used the memory).
+static hipError_t dev_alloc(void** p, size_t bytes) {
+    static const bool fill = [] { const char* e = getenv("EXACTO_DEBUG_FILL"); return e && e[0] == '1'; }();
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess && fill && bytes) {
+        e = hipMemset(*p, 0xA5, bytes);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+    }
+    return e;
+}
+
 static int grow(u64** buf, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
     free_dev(*buf);
     *buf = nullptr;
     *cap = 0;
-    HIP_TRY(hipMalloc((void**)buf, bytes));
+    HIP_TRY(dev_alloc((void**)buf, bytes));
     *cap = bytes;
     return 0;
 }
@@ -472,13 +486,13 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
         const u64 m63 = (1ull << 63) % p;
         Q.k63 = (uint32_t)(m63 == 0 ? 0 : p - m63);
     }
-    HIP_TRY(hipMalloc((void**)&b->d_tw32, tw.size() * sizeof(uint2)));
+    HIP_TRY(dev_alloc((void**)&b->d_tw32, tw.size() * sizeof(uint2)));
     if (int e_ = upload(c, b->d_tw32, tw.data(), tw.size() * sizeof(uint2))) return e_;
     for (int s = 0; s < S; ++s) {
         pc[s].tw_fwd = b->d_tw32 + (size_t)s * 2 * n;
         pc[s].tw_inv = b->d_tw32 + (size_t)s * 2 * n + n;
     }
-    HIP_TRY(hipMalloc((void**)&b->d_p32, S * sizeof(Prime32)));
+    HIP_TRY(dev_alloc((void**)&b->d_p32, S * sizeof(Prime32)));
     if (int e_ = upload(c, b->d_p32, pc.data(), S * sizeof(Prime32))) return e_;
     Ks32Tables T;
     std::memset(&T, 0, sizeof(T));
@@ -507,7 +521,7 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
         const u64 pm = P.mod(q);
         T.negP[l] = pm == 0 ? 0 : q - pm;
     }
-    HIP_TRY(hipMalloc((void**)&b->d_kst, sizeof(Ks32Tables)));
+    HIP_TRY(dev_alloc((void**)&b->d_kst, sizeof(Ks32Tables)));
     if (int e_ = upload(c, b->d_kst, &T, sizeof(Ks32Tables))) return e_;
     b->S = S;
     return 0;
@@ -583,13 +597,13 @@ static int build_tables(exacto_ctx* c) {
     for (int t = 0; t < NP; ++t)
         pc[t] = make_prime_const(c->primes[t], c->n, c->logn, &tw[(size_t)t * 2 * c->n],
                                  &tw[(size_t)t * 2 * c->n + c->n]);
-    HIP_TRY(hipMalloc((void**)&c->d_tw, tw.size() * sizeof(TwPair)));
+    HIP_TRY(dev_alloc((void**)&c->d_tw, tw.size() * sizeof(TwPair)));
     if (int e_ = upload(c, c->d_tw, tw.data(), tw.size() * sizeof(TwPair))) return e_;
     for (int t = 0; t < NP; ++t) {
         pc[t].tw_fwd = c->d_tw + (size_t)t * 2 * c->n;
         pc[t].tw_inv = c->d_tw + (size_t)t * 2 * c->n + c->n;
     }
-    HIP_TRY(hipMalloc((void**)&c->d_primes, NP * sizeof(PrimeConst)));
+    HIP_TRY(dev_alloc((void**)&c->d_primes, NP * sizeof(PrimeConst)));
     if (int e_ = upload(c, c->d_primes, pc.data(), NP * sizeof(PrimeConst))) return e_;
 
     // ---- CRT tables
@@ -669,8 +683,8 @@ static int build_tables(exacto_ctx* c) {
         C.special = C.fast && mn > (1ull << 60) - (1ull << 24);
         C.digit_small = c->gbase <= *std::min_element(qv.begin(), qv.end());
     }
-    HIP_TRY(hipMalloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
-    HIP_TRY(hipMalloc((void**)&c->d_crt, sizeof(CrtTables)));
+    HIP_TRY(dev_alloc((void**)&c->d_scal, EXACTO_MAX_L * sizeof(u64)));
+    HIP_TRY(dev_alloc((void**)&c->d_crt, sizeof(CrtTables)));
     if (int e_ = upload(c, c->d_crt, &C, sizeof(CrtTables))) return e_;
     return 0;
 }
@@ -1039,17 +1053,17 @@ static int ensure_workspace(exacto_ctx* c, size_t items) {
     c->ws_items = 0;
     const size_t pb = poly_bytes(c);
     const int NP = c->L + c->K;
-    HIP_TRY(hipMalloc((void**)&c->ws_coefQ, items * 4 * c->L * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws_extP, items * 4 * std::max(c->K, 1) * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws_T, items * 3 * NP * pb));
-    HIP_TRY(hipMalloc((void**)&c->ws_D, items * std::max(c->G, 1) * c->L * pb));
+    HIP_TRY(dev_alloc((void**)&c->ws_coefQ, items * 4 * c->L * pb));
+    HIP_TRY(dev_alloc((void**)&c->ws_extP, items * 4 * std::max(c->K, 1) * pb));
+    HIP_TRY(dev_alloc((void**)&c->ws_T, items * 3 * NP * pb));
+    HIP_TRY(dev_alloc((void**)&c->ws_D, items * std::max(c->G, 1) * c->L * pb));
     if (c->ws_D16) (void)hipFree(c->ws_D16);
-    HIP_TRY(hipMalloc((void**)&c->ws_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
+    HIP_TRY(dev_alloc((void**)&c->ws_D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
     free_dev(c->ws_DS); free_dev(c->ws_U);
     c->ws_DS = c->ws_U = nullptr;
     if (c->S32) {  // ks32: digit residues [item][G][S][n] and accumulators [item][2L][S][n]
-        HIP_TRY(hipMalloc((void**)&c->ws_DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc((void**)&c->ws_U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(dev_alloc((void**)&c->ws_DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(dev_alloc((void**)&c->ws_U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
     }
     c->ws_items = items;
     return 0;
@@ -1070,14 +1084,14 @@ static int ensure_lane(exacto_ctx* c, int idx, size_t items) {
     l.items = 0;
     const size_t pb = poly_bytes(c);
     const int NP = c->L + c->K;
-    HIP_TRY(hipMalloc((void**)&l.coefQ, items * 4 * c->L * pb));
-    HIP_TRY(hipMalloc((void**)&l.extP, items * 4 * std::max(c->K, 1) * pb));
-    HIP_TRY(hipMalloc((void**)&l.T, items * 3 * NP * pb));
-    HIP_TRY(hipMalloc((void**)&l.D, items * std::max(c->G, 1) * c->L * pb));
-    HIP_TRY(hipMalloc((void**)&l.D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
+    HIP_TRY(dev_alloc((void**)&l.coefQ, items * 4 * c->L * pb));
+    HIP_TRY(dev_alloc((void**)&l.extP, items * 4 * std::max(c->K, 1) * pb));
+    HIP_TRY(dev_alloc((void**)&l.T, items * 3 * NP * pb));
+    HIP_TRY(dev_alloc((void**)&l.D, items * std::max(c->G, 1) * c->L * pb));
+    HIP_TRY(dev_alloc((void**)&l.D16, items * std::max(c->G, 1) * c->n * sizeof(int16_t)));
     if (c->S32) {
-        HIP_TRY(hipMalloc((void**)&l.DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc((void**)&l.U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(dev_alloc((void**)&l.DS, items * std::max(c->G, 1) * c->S32 * c->n * sizeof(uint32_t)));
+        HIP_TRY(dev_alloc((void**)&l.U, items * 2 * c->L * c->S32 * c->n * sizeof(uint32_t)));
     }
     l.items = items;
     return 0;
@@ -1755,9 +1769,9 @@ static int dbfv_plan(exacto_ctx* c, size_t B, size_t d, u64 base, u64 plain, con
     if (int e_ = upload(c, c->d_off, off.data(), off.size() * sizeof(u64))) return e_;
     free_dev(c->d_term_start);
     free_dev(c->d_terms);
-    HIP_TRY(hipMalloc((void**)&c->d_term_start, start.size() * sizeof(int)));
+    HIP_TRY(dev_alloc((void**)&c->d_term_start, start.size() * sizeof(int)));
     if (int e_ = upload(c, c->d_term_start, start.data(), start.size() * sizeof(int))) return e_;
-    HIP_TRY(hipMalloc((void**)&c->d_terms, std::max<size_t>(terms.size(), 1) * sizeof(CombineTerm)));
+    HIP_TRY(dev_alloc((void**)&c->d_terms, std::max<size_t>(terms.size(), 1) * sizeof(CombineTerm)));
     if (!terms.empty())
         if (int e_ = upload(c, c->d_terms, terms.data(), terms.size() * sizeof(CombineTerm))) return e_;
     c->cached_B = B; c->cached_d = d; c->cached_base = base; c->cached_p = plain;
@@ -2303,7 +2317,7 @@ static int delta_residues(exacto_ctx* c) {
         for (size_t w = D.size(); w-- > 0;) r = ((r << 64) | D[w]) % c->primes[i];
         dr[i] = (u64)r;
     }
-    if (!c->d_delta) HIP_TRY(hipMalloc((void**)&c->d_delta, EXACTO_MAX_L * sizeof(u64)));
+    if (!c->d_delta) HIP_TRY(dev_alloc((void**)&c->d_delta, EXACTO_MAX_L * sizeof(u64)));
     if (int e_ = upload(c, c->d_delta, dr.data(), dr.size() * sizeof(u64))) return e_;
     c->delta_ok = true;
     return 0;
@@ -3069,7 +3083,7 @@ extern "C" int exacto_bootstrap_key_material(exacto_ctx* o, exacto_ctx* b, const
     if (int e = boot_pair_check(o, b)) return e;
     const size_t n = o->n;
     u64* d = nullptr;
-    HIP_TRY(hipMalloc((void**)&d, (n + b->L * n + n) * sizeof(u64)));
+    HIP_TRY(dev_alloc((void**)&d, (n + b->L * n + n) * sizeof(u64)));
     int rc = upload(o, d, sk, n * sizeof(u64));
     if (rc == 0) rc = exacto_bootstrap_key_material_dev(o, b, d, d + n, d + n + b->L * n);
     if (rc == 0 && (hipMemcpyAsync(boot_sk, d + n, b->L * n * sizeof(u64), hipMemcpyDeviceToHost, o->stream) != hipSuccess ||

@@ -300,6 +300,18 @@ static int boot_repro(int reps) {
 
 int main(int argc, char** argv) {
     if (argc == 3 && std::string(argv[1]) == "--boot-reps") return boot_repro(std::atoi(argv[2]));
+    if (argc == 3 && std::string(argv[1]) == "--boot-case-reps") {   // the whole bootstrap case, repeated
+        int fails = 0, first = 0;
+        for (int r = 0; r < std::atoi(argv[2]); ++r) {
+            const int rc = bootstrap_case();
+            if (rc) {
+                ++fails;
+                if (!first) first = rc;
+            }
+        }
+        std::printf("boot_case reps=%s fails=%d first_code=%d\n", argv[2], fails, first);
+        return fails != 0;
+    }
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s <fixture-dir> <case>...\n", argv[0]);
         return 2;
