@@ -2947,6 +2947,26 @@ static int boot_pair_check(exacto_ctx* o, exacto_ctx* b) {
     return 0;
 }
 
+// The bootstrap functions work on two contexts.  They run every step of both on ONE stream (the
+// boot context's): o's stream is rebound to b's for the call.  With a stream per context, data went
+// from one stream to the other with only host-side synchronisation in between (the inputs uploaded
+// on b's stream and copied on o's, the modulus-switched rows written on o's and read on b's), and
+// the C++ test saw a bootstrap return the previous call's result bit for bit (its input buffer sits
+// at the same address every call): a read that did not see the upload.  On one stream every such
+// dependency is ordered by the runtime itself.
+struct StreamRebind {
+    exacto_ctx* c;
+    hipStream_t saved;
+    StreamRebind(exacto_ctx* c_, hipStream_t s) : c(c_), saved(c_->stream) {
+        if (saved != s) (void)hipStreamSynchronize(saved);
+        c->stream = s;
+    }
+    ~StreamRebind() {
+        if (c->stream != saved) (void)hipStreamSynchronize(c->stream);
+        c->stream = saved;
+    }
+};
+
 // gen_bootstrap_key's key material (bfv_host.rs:57-100, 289-330): the boot scheme's secret key
 // boot_sk [Lb][n] (NTT domain, create_boot_sk) and the plaintext s_pt [n] that bsk encrypts.
 extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, const uint64_t* sk, uint64_t* boot_sk,
@@ -2954,6 +2974,7 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
     if (int e = boot_pair_check(o, b)) return e;
     if (!sk || !boot_sk || !s_pt) return invalid_param("null argument");
     const int n = o->n;
+    StreamRebind one(o, b->stream);   // before the scratch: its block is freed on b's stream
     Scratch ts;
     HIP_TRY(ts.alloc(2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch));
     u64* tmp = ts.as<u64>();
@@ -2991,6 +3012,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (B == 0) return 0;
     const int n = o->n;
     const long Lbn = (long)b->L * n;
+    StreamRebind one(o, b->stream);   // declared first: destroyed after the scratch blocks are freed
     // Scratch of the whole call.  A block of o's stream is also read on b's stream (small), so
     // both streams drain before any block goes back to its pool: `drain` is declared after the
     // blocks, so its destructor runs first on every return path; the normal path calls finish()

@@ -268,8 +268,16 @@ static int bootstrap_case() {
                     .gadget_base(8).build();
     auto sko = gen_secret_key_with_rng(orig, rng);
     auto bsk = gen_bootstrap_key(sko, boot, 25, 5, rng);
-    for (uint64_t v = 0; v < 5; ++v)
-        if (decode_scalar(decrypt(bfv_bootstrap(trivial_encrypt(v, orig), bsk), bsk.boot_sk)) % 5 != v) return 37;
+    for (uint64_t v = 0; v < 5; ++v) {
+        const auto out = bfv_bootstrap(trivial_encrypt(v, orig), bsk);
+        const uint64_t dec = decode_scalar(decrypt(out, bsk.boot_sk));
+        uint64_t h = 1469598103934665603ull;   // FNV-1a of the output words: identical run to run
+        for (auto& p : out.c)
+            for (uint64_t w : p.data) h = (h ^ w) * 1099511628211ull;
+        std::printf("boot v=%llu dec=%llu out=%016llx\n", (unsigned long long)v, (unsigned long long)dec,
+                    (unsigned long long)h);
+        if (dec % 5 != v) return 37;
+    }
     if (lagrange_interpolate({0, 1, 4, 2}, 7) != std::vector<uint64_t>{0, 0, 1, 0}) return 38;
     return 0;
 }
@@ -300,6 +308,16 @@ static int boot_repro(int reps) {
 
 int main(int argc, char** argv) {
     if (argc == 3 && std::string(argv[1]) == "--boot-reps") return boot_repro(std::atoi(argv[2]));
+    if (argc >= 3 && std::string(argv[1]) == "--seq") {   // diagnostic: named cases in the given order
+        int bad = 0;
+        for (int i = 2; i < argc; ++i) {
+            const std::string c = argv[i];
+            const int rc = c == "error" ? error_cases() : c == "keygen" ? keygen_case() : c == "boot" ? bootstrap_case() : 98;
+            std::printf("%s %s (%d)\n", rc ? "FAIL" : "PASS", argv[i], rc);
+            bad |= rc != 0;
+        }
+        return bad;
+    }
     if (argc == 3 && std::string(argv[1]) == "--boot-case-reps") {   // the whole bootstrap case, repeated
         int fails = 0, first = 0;
         for (int r = 0; r < std::atoi(argv[2]); ++r) {
