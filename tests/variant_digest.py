@@ -1,0 +1,73 @@
+"""Digests of the hot path's outputs under the kernel-selection switches of this process's
+environment (run as a child process by tests/test_gpu_variants.py: each switch is read once per
+process).  Prints one JSON object {case: sha256}.
+
+Cases: cfg3 bfv_mul_and_relin (n = 4096, 3 limbs: forward, inverse, tensor, key switch), cfg5
+dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels), and the fused
+NTT product at n = 4096 / 8192, out of place and in place on b.
+"""
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+from bridge import uniform_residues  # noqa: E402
+from oracle import params as P  # noqa: E402
+from exacto_amd._ffi import HipContext  # noqa: E402
+
+
+def sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint64).tobytes()).hexdigest()
+
+
+def main():
+    import torch
+    out = {}
+    prm = P.cfg3_params(4096)
+    q, n = prm.ct_basis.moduli, 4096
+    rng = np.random.default_rng(7001)
+    ct1 = uniform_residues(rng, (8, 2), q, n)
+    ct2 = uniform_residues(rng, (8, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    ctx = HipContext.from_params(prm)
+    ctx.load_relin_key(rlk)
+    out["cfg3_mul_relin"] = sha(ctx.bfv_mul_and_relin(ct1, ct2))
+
+    dp = P.cfg5_params(8192)
+    prm5 = dp.bfv_params
+    q5, d = prm5.ct_basis.moduli, dp.num_digits
+    rng = np.random.default_rng(7002)
+    a = uniform_residues(rng, (1, d, 2), q5, 8192)
+    b = uniform_residues(rng, (1, d, 2), q5, 8192)
+    rlk5 = uniform_residues(rng, (prm5.gadget_digits, 2), q5, 8192)
+    ctx5 = HipContext.from_params(prm5)
+    ctx5.load_relin_key(rlk5)
+    out["cfg5_dbfv_mul"] = sha(ctx5.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+    out["cfg5_chain2"] = sha(ctx5.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2))
+
+    for nn, qs in ((4096, [1152921504606830593]), (8192, [1152921504606830593, 1152921504606748673])):
+        rng = np.random.default_rng(7003 + nn)
+        c = HipContext(nn, qs, plain_modulus=257)
+        qa = np.array(qs, dtype=np.uint64)[None, :, None]
+        x = (rng.integers(0, 1 << 63, size=(4, len(qs), nn), dtype=np.uint64) % qa).astype(np.uint64)
+        y = (rng.integers(0, 1 << 63, size=(4, len(qs), nn), dtype=np.uint64) % qa).astype(np.uint64)
+        dx = torch.from_numpy(x.view(np.int64)).cuda()
+        dy = torch.from_numpy(y.view(np.int64)).cuda()
+        o = torch.empty_like(dx)
+        c.rns_polymul_dev(dx, dy, o, 4)
+        c.rns_polymul_dev(dx, dy, dy, 4)   # in place on b
+        c.synchronize()
+        out[f"polymul_{nn}"] = sha(o.cpu().numpy().view(np.uint64))
+        out[f"polymul_{nn}_inplace"] = sha(dy.cpu().numpy().view(np.uint64))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
