@@ -228,8 +228,9 @@ struct exacto_ctx {
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
-    // EXACTO_CRT_FWD=2/3: the key switch's lift and the forward NTT of bfv_mul_and_relin's outputs in
-    // one kernel (ks32_crt_fwd_kernel, 2 / 3 waves per SIMD).  Off by default: cfg3 398.3k -> 391.3k/s
+    // EXACTO_CRT_FWD=2/3/4: the key switch's lift and the forward NTT of bfv_mul_and_relin's outputs in
+    // one kernel (ks32_crt_fwd_kernel, 2 / 3 waves per SIMD; 4: ks32_crt_fwd_pin_kernel, pinned rounds,
+    // 13-22 VGPRs spilled in the lift: cfg3 413k vs 429k/s same box, round 3).  Off by default: cfg3 398.3k -> 391.3k/s
     // (3 waves, a few spills) and 386.5k/s (2 waves): the lift's 126-VGPR phase and the transform do
     // not share a register budget well, and the separate forward is the persistent LDS-DMA kernel
     int crt_fwd = 0;

@@ -1496,13 +1496,48 @@ ks32_crt_fwd_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_
     for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
 }
 
+// ks32_crt_fwd_kernel with the forward rounds over pinned homes (waves = 4 at launch_ks32_crt_fwd):
+// the lift's values go into the homes, PIN_FWD_ROUNDS, one LDS transpose, coalesced stores.
+template <int LOGN, int S>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
+ks32_crt_fwd_pin_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
+                        const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
+                        const PrimeConst* __restrict__ qprimes) {
+    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
+    constexpr int N = 1 << LOGN, T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const uint32_t b = blockIdx.x;             // (item, cl)
+    EXACTO_PIN_DECL
+    {
+        u64 x[16];
+        ks32_crt_values<LOGN, S>(x, U, R, r_stride, L, b, reinterpret_cast<uint32_t*>(lds), tid, KT, primes, qprimes);
+#define PIN_FROM_X(k) PIN_SET(k, x[k])
+        PIN_X16(PIN_FROM_X)
+#undef PIN_FROM_X
+    }
+    const uint32_t CL = 2 * L;
+    const long item = b / CL;
+    const int cl = (int)(b - (uint32_t)item * CL);
+    const PrimeConst& P = qprimes[cl % L];
+    lds_barrier();   // the lift's last LDS reads are done before the forward rounds reuse lds
+    PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q))
+    PIN_EXCHANGE(lds, tid, 0, LOGN - 4)
+    u64* dst = R + item * r_stride + (long)cl * N + tid;
+#define PIN_OUT(k) dst[(k) * T] = PIN_GET(k);
+    PIN_X16(PIN_OUT)
+#undef PIN_OUT
+}
+
 bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn,
                          const Ks32Tables* KT, const Prime32* primes, const PrimeConst* qprimes, hipStream_t s,
                          int waves) {
     const dim3 grid((unsigned)((long)items * 2 * L));
 #define CF_(LG, S_, W_) hipLaunchKernelGGL((ks32_crt_fwd_kernel<LG, S_, W_>), grid, dim3((1 << LG) / 16), 0, s, U, R, \
                                            r_stride, L, KT, primes, qprimes)
-#define CFW_(LG, S_) do { if (waves == 2) CF_(LG, S_, 2); else CF_(LG, S_, 3); } while (0)
+#define CFP_(LG, S_) hipLaunchKernelGGL((ks32_crt_fwd_pin_kernel<LG, S_>), grid, dim3((1 << LG) / 16), 0, s, U, R, \
+                                         r_stride, L, KT, primes, qprimes)
+#define CFW_(LG, S_) do { if (waves == 4) CFP_(LG, S_); else if (waves == 2) CF_(LG, S_, 2); else CF_(LG, S_, 3); } while (0)
     if (items <= 0) return true;
     if (logn == 12 && S == 3) CFW_(12, 3);
     else if (logn == 13 && S == 3) CFW_(13, 3);
@@ -1510,6 +1545,7 @@ bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, in
     else if (logn == 13 && S == 2) CFW_(13, 2);
     else return false;
 #undef CFW_
+#undef CFP_
 #undef CF_
     return true;
 }

@@ -1,6 +1,7 @@
 """The kernel-selection switches give bit-identical results: every A/B alternative that ships in
 the library (the pinned-home forward / tensor / polymul kernels against the asm, pipe, tensor3 +
-tensor_c2 and register-resident forms) computes the same outputs as the default selection.
+tensor_c2 and register-resident forms; the fused ks32 lift + forward kernels against the separate
+ones) computes the same outputs as the default selection.
 
 Each switch is read once per process, so each variant runs tests/variant_digest.py in a child
 process (sequentially, one GPU process at a time) and the digests are compared with the default's.
@@ -23,12 +24,15 @@ VARIANTS = {
     "tensor_pin_none": {"EXACTO_TENSOR_PIN": "0"},
     "asm_fwd_and_pipe": {"EXACTO_FWD_PIN": "0", "EXACTO_NTT_PIPE": "1"},
     "polymul_pin": {"EXACTO_POLYMUL_PIN": "1"},
+    "crt_fwd_pin": {"EXACTO_CRT_FWD": "4"},
+    "crt_fwd_3waves": {"EXACTO_CRT_FWD": "3"},
 }
 
 
 def _digests(extra_env):
     env = dict(os.environ)
-    for k in ("EXACTO_TENSOR_PIN", "EXACTO_FWD_PIN", "EXACTO_NTT_PIPE", "EXACTO_POLYMUL_PIN", "EXACTO_TENSOR3"):
+    for k in ("EXACTO_TENSOR_PIN", "EXACTO_FWD_PIN", "EXACTO_NTT_PIPE", "EXACTO_POLYMUL_PIN", "EXACTO_TENSOR3",
+              "EXACTO_CRT_FWD"):
         env.pop(k, None)
     env.update(extra_env)
     r = subprocess.run([sys.executable, os.path.join(HERE, "variant_digest.py")], env=env, capture_output=True,
