@@ -2949,12 +2949,11 @@ static int boot_pair_check(exacto_ctx* o, exacto_ctx* b) {
 }
 
 // The bootstrap functions work on two contexts.  They run every step of both on ONE stream (the
-// boot context's): o's stream is rebound to b's for the call.  With a stream per context, data went
-// from one stream to the other with only host-side synchronisation in between (the inputs uploaded
-// on b's stream and copied on o's, the modulus-switched rows written on o's and read on b's), and
-// the C++ test saw a bootstrap return the previous call's result bit for bit (its input buffer sits
-// at the same address every call): a read that did not see the upload.  On one stream every such
-// dependency is ordered by the runtime itself.
+// boot context's): o's stream is rebound to b's for the call, so that every hand-off between the
+// contexts (the inputs uploaded on b's stream and copied on o's, the modulus-switched rows written on
+// o's and read on b's) is ordered by the runtime instead of by host-side synchronisation alone.
+// (Made while chasing an intermittent failure of the C++ test's bootstrap case, which it did not
+// remove: DESIGN.md §6, "Open".)
 struct StreamRebind {
     exacto_ctx* c;
     hipStream_t saved;

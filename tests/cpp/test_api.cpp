@@ -269,7 +269,12 @@ static int bootstrap_case() {
     auto sko = gen_secret_key_with_rng(orig, rng);
     auto bsk = gen_bootstrap_key(sko, boot, 25, 5, rng);
     for (uint64_t v = 0; v < 5; ++v) {
-        const auto out = bfv_bootstrap(trivial_encrypt(v, orig), bsk);
+        const auto tin = trivial_encrypt(v, orig);
+        uint64_t hin = 1469598103934665603ull;
+        for (auto& p : tin.c)
+            for (uint64_t w : p.data) hin = (hin ^ w) * 1099511628211ull;
+        std::printf("boot v=%llu in=%016llx\n", (unsigned long long)v, (unsigned long long)hin);
+        const auto out = bfv_bootstrap(tin, bsk);
         const uint64_t dec = decode_scalar(decrypt(out, bsk.boot_sk));
         uint64_t h = 1469598103934665603ull;   // FNV-1a of the output words: identical run to run
         for (auto& p : out.c)
