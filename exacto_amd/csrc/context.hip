@@ -369,6 +369,16 @@ static hipError_t dev_alloc(void** p, size_t bytes) {
     return e;
 }
 
+// Device -> device copies of the library, as a kernel (every size here is whole u64 words).  The
+// bootstrap copied its input into a re-used pool block with an asynchronous runtime copy, and the
+// next kernel sometimes read the block's previous contents (the C++ test's bootstrap of 1 came back
+// as the bootstrap of 0, DESIGN.md §6 "Fixed"); a kernel's writes reach the next kernel on the
+// stream like any kernel output.  Device fills likewise (launch_fill_u32).
+static hipError_t dev_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    launch_copy_u64(static_cast<u64*>(dst), static_cast<const u64*>(src), (long)(bytes / 8), s);
+    return hipGetLastError();
+}
+
 static int grow(u64** buf, size_t* cap, size_t bytes) {
     if (*cap >= bytes) return 0;
     free_dev(*buf);
@@ -943,7 +953,7 @@ extern "C" int exacto_ctx_load_relin_key_dev(exacto_ctx* c, const uint64_t* rlk,
     u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
     if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
     if (num_keys)
-        HIP_TRY(hipMemcpyAsync(dst, rlk, num_keys * 2 * c->L * poly_bytes(c), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(dev_copy(dst, rlk, num_keys * 2 * c->L * poly_bytes(c), c->stream));
     return 0;
 }
 
@@ -1577,7 +1587,7 @@ extern "C" int exacto_relinearize_dev(exacto_ctx* c, const uint64_t* ct, size_t 
     const long Ln = (long)c->L * c->n;
     if (polys < 3) {  // keyswitch.rs:63-65: already degree-1, cloned: out = [B][polys][L][n]
         if (B * polys)
-            HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+            HIP_TRY(dev_copy(out, ct, B * polys * Ln * sizeof(u64), c->stream));
         return 0;
     }
     if (polys > 3) return invalid_param("relinearization only supports degree-2 ciphertexts");
@@ -2124,7 +2134,7 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     if (int e = check_ctx(c)) return e;
     const size_t bytes = B * d * 2 * c->L * poly_bytes(c);
     if (depth == 0) {
-        if (B && out != x) HIP_TRY(hipMemcpyAsync(out, x, bytes, hipMemcpyDeviceToDevice, c->stream));
+        if (B && out != x) HIP_TRY(dev_copy(out, x, bytes, c->stream));
         return 0;
     }
     if (depth > 1 && B) {
@@ -2392,7 +2402,7 @@ extern "C" int exacto_gen_galois_key_dev(exacto_ctx* c, const uint64_t* sk, uint
     if (grow(&c->enc_buf, &cap, (size_t)(2 * n + Ln) * sizeof(u64))) return EXACTO_ERR_HIP;
     c->enc_cap = cap;
     u64 *t0 = c->enc_buf, *t1 = t0 + n, *s_auto = t1 + n;
-    HIP_TRY(hipMemcpyAsync(t0, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(dev_copy(t0, sk, n * sizeof(u64), c->stream));
     if (int e = run_ntt(c, contiguous(t0, 1, 1, 0, 1, n), 1, true)) return e;
     launch_automorph(t0, n, t1, n, 1, 1, n, 1, element, c->d_primes, 0, c->stream);
     launch_lift_q0(t1, s_auto, 1, n, L, c->d_primes, c->stream);
@@ -2601,7 +2611,7 @@ extern "C" int exacto_bfv_monomial_mul_dev(exacto_ctx* c, const uint64_t* ct, si
     j %= 2 * (u64)c->n;
     if (j == 0) {  // eval.rs:619-621: a clone
         if (out != ct)
-            HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+            HIP_TRY(dev_copy(out, ct, B * polys * Ln * sizeof(u64), c->stream));
         return 0;
     }
     if (int e = pl_scratch(c, (size_t)Ln)) return e;
@@ -2644,7 +2654,7 @@ extern "C" int exacto_bfv_trace_dev(exacto_ctx* c, const uint64_t* ct, size_t po
     if (!ct || !out || (E && (!elements || !gks))) return invalid_param("null argument");
     if (B == 0) return 0;
     const long Ln = (long)c->L * c->n;
-    if (out != ct) HIP_TRY(hipMemcpyAsync(out, ct, B * polys * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream));
+    if (out != ct) HIP_TRY(dev_copy(out, ct, B * polys * Ln * sizeof(u64), c->stream));
     if (E == 0) return 0;
     if (polys != 2) return invalid_param("automorphism requires degree-1 ciphertext");
     std::vector<u64> ks(elements, elements + E);
@@ -2701,7 +2711,7 @@ extern "C" int exacto_extract_coefficients_dev(exacto_ctx* c, const uint64_t* ct
     launch_plain_apply(PLAIN_MUL, ct, 0, shifted, (long)J, 2, c->pl_buf, Ln, n, c->L, c->d_primes, c->stream);
     int rc = hipGetLastError() == hipSuccess ? 0 : fail(EXACTO_ERR_HIP, "HIP error: monomial launch");
     if (rc == 0 && naive)
-        rc = hipMemcpyAsync(out, shifted, J * 2 * Ln * sizeof(u64), hipMemcpyDeviceToDevice, c->stream) == hipSuccess
+        rc = dev_copy(out, shifted, J * 2 * Ln * sizeof(u64), c->stream) == hipSuccess
                  ? 0 : fail(EXACTO_ERR_HIP, "HIP error: copy");
     if (rc == 0) rc = trace_core(c, naive ? shifted : nullptr, out, ks, kidx, gks, num_keys, J);
     if (rc) return rc;
@@ -2908,7 +2918,8 @@ extern "C" int exacto_eval_poly_dev(exacto_ctx* c, const uint64_t* ct, const uin
     }
     // group g_i into `dst`: trivial(0) + sum_j (a mod t) x^j
     auto group = [&](size_t gi, u64* dst) -> int {
-        HIP_TRY(hipMemsetAsync(dst, 0, words * sizeof(u64), c->stream));
+        launch_fill_u32(reinterpret_cast<uint32_t*>(dst), 0, (long)(2 * words), c->stream);   // (see dev_copy)
+        HIP_TRY(hipGetLastError());
         for (size_t j = 0; j < k; ++j) {
             const size_t idx = gi * k + j;
             if (idx >= m) break;
@@ -2953,7 +2964,7 @@ static int boot_pair_check(exacto_ctx* o, exacto_ctx* b) {
 // contexts (the inputs uploaded on b's stream and copied on o's, the modulus-switched rows written on
 // o's and read on b's) is ordered by the runtime instead of by host-side synchronisation alone.
 // (Made while chasing an intermittent failure of the C++ test's bootstrap case, which it did not
-// remove: DESIGN.md §6, "Open".)
+// remove; the cause was the runtime copy into a re-used block, see dev_copy and DESIGN.md §6.)
 struct StreamRebind {
     exacto_ctx* c;
     hipStream_t saved;
@@ -2978,7 +2989,7 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
     Scratch ts;
     HIP_TRY(ts.alloc(2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch));
     u64* tmp = ts.as<u64>();
-    HIP_TRY(hipMemcpyAsync(tmp, sk, n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream));
+    HIP_TRY(dev_copy(tmp, sk, n * sizeof(u64), o->stream));
     int rc = run_ntt(o, contiguous(tmp, 1, 1, 0, 1, n), 1, true);  // sk.poly.components[0].to_coeff_poly()
     if (rc == 0) {
         launch_boot_key_map(tmp, tmp + n, s_pt, n, o->primes[0], b->primes[0], b->plain, o->stream);
@@ -3042,8 +3053,9 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64* coef = coef_s.as<u64>();
     int* flags = flags_s.as<int>();
     u64* small = coef + B * 2 * n;
-    ok(hipMemcpyAsync(coef, ct, B * 2 * n * sizeof(u64), hipMemcpyDeviceToDevice, o->stream), "copy");
-    ok(hipMemsetAsync(flags, 0, B * sizeof(int), o->stream), "memset");
+    ok(dev_copy(coef, ct, B * 2 * n * sizeof(u64), o->stream), "copy");
+    launch_fill_u32(reinterpret_cast<uint32_t*>(flags), 0, (long)B, o->stream);   // (see dev_copy)
+    ok(hipGetLastError(), "flags fill");
     if (rc == 0) rc = exacto_rns_inv_dev(o, coef, B * 2);
     if (rc == 0) {
         launch_modswitch(coef, small, flags, (long)B, n, o->primes[0], q_prime, b->plain, o->stream);
@@ -3080,7 +3092,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64 *slots = nullptr, *rounded = nullptr;
     for (size_t i = 0; i < B && rc == 0; ++i) {
         u64* oi = out + i * ctw;
-        ok(hipMemcpyAsync(phase, oi, ctw * sizeof(u64), hipMemcpyDeviceToDevice, b->stream), "copy");
+        ok(dev_copy(phase, oi, ctw * sizeof(u64), b->stream), "copy");
         if (rc) break;
         if (!hflags[i]) {  // bfv_host.rs:180-186
             rc = exacto_eval_poly_dev(b, phase, rpoly, m, oi, 1);

@@ -1232,4 +1232,35 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                        terms, out, d, n, L, primes);
 }
 
+
+// ---------------------------------------------------------------- device-to-device copy
+
+// dst <- src, u64 words, as a kernel (context.hip dev_copy: the library's device copies)
+__global__ void __launch_bounds__(256)
+copy_u64_kernel(u64* __restrict__ dst, const u64* __restrict__ src, long words) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) dst[i] = src[i];
+}
+
+void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s) {
+    if (words <= 0) return;
+    long blocks = (words + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words);
+}
+
+
+__global__ void __launch_bounds__(256)
+fill_u32_kernel(uint32_t* __restrict__ dst, uint32_t v, long words) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) dst[i] = v;
+}
+
+void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s) {
+    if (words <= 0) return;
+    long blocks = (words + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words);
+}
+
 }  // namespace exacto
