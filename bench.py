@@ -59,6 +59,9 @@ HBM_PEAK_GBS = 8000.0
 
 # name: (n, moduli, aux, BFV plain modulus, gadget base, dBFV (d, base, p) or None, chain depth)
 CONFIGS = {
+    # BASELINE configs[0] = compact_bfv (presets.rs:24-35): the literal HPS multiplier with one aux
+    # prime, G = 3; the configuration of the reference's published ~390 us (README.md:153)
+    "cfg1": (1024, [1099509805057], [562949953443841], 257, 1 << 16, None, 0),
     "cfg2": (4096, [1152921504606830593], [], 65537, 1 << 16, None, 0),   # NTT fwd + mul + inv
     "cfg3": (4096, Q3, [], 65537, 1 << 16, None, 0),                      # bfv_mul_and_relin
     "cfg4": (4096, Q3, [], 260111, 1 << 16, (2, 256, 65536), 1),          # dbfv_mul
@@ -66,13 +69,26 @@ CONFIGS = {
     # SURVEY 8(f) rank 4 (widened row, not a BASELINE config): Galois key switching
     # bfv_apply_automorphism (eval.rs:512-561) on cfg3's parameters, element 5
     "galois": (4096, Q3, [], 65537, 1 << 16, None, 0),
+    # u64_dbfv (presets.rs:61-75), the profile of the reference's published dbfv_mul 31.395 ms
+    # (reports/paper_reproduction.md:9, src/bin/paper_repro.rs:84-95): n = 4096, one 60-bit q, two
+    # HPS aux primes, t = 1040407, gadget 256 (G = 8), d = 8, b = 256, p = 2^64
+    "u64dbfv": (4096, [1152921504606830593], [18014398509998081, 36028797018972161], 1040407, 256,
+                (8, 256, 0), 1),
 }
-DEFAULT_BATCH = {"cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8, "galois": 1024}
+DEFAULT_BATCH = {"cfg1": 8192, "cfg2": 16384, "cfg3": 1024, "cfg4": 1024, "cfg5": 8, "galois": 1024,
+                 "u64dbfv": 64}
+# the reference's own published numbers for a configuration (CPU, hardware unstated): one call's latency
+PUBLISHED = {
+    "cfg1": {"op": "bfv_mul_and_relin", "latency_us": 390.0, "source": "README.md:153 (compact_bfv)"},
+    "u64dbfv": {"op": "dbfv_mul", "latency_us": 31395.0,
+                "source": "reports/paper_reproduction.md:9 (d=8, b=2^8, u64_dbfv)"},
+}
 
 # profiled kernel families (exacto_hip.h exacto_prof_read kinds, context.hip ProfKind)
 KINDS = {0: "fwd_ntt", 1: "inv_ntt", 2: "tensor_inv", 3: "polymul", 4: "exact_lift", 5: "exact_scale",
          6: "ks32_digit_ntt", 7: "ks32_mac", 8: "ks32_crt", 9: "dbfv_pairsum", 10: "psum_scale",
-         11: "tensor_c2_inv", 12: "ks32_digit_sum", 13: "dbfv_combine"}
+         11: "tensor_c2_inv", 12: "ks32_digit_sum", 13: "dbfv_combine", 14: "hps_extend", 15: "relin_mac",
+         16: "hps_scale"}
 
 
 def parse(argv=None):
@@ -111,11 +127,25 @@ def relaunch(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _near60(q, bits=32):
+    return (1 << 60) - (1 << bits) < q < (1 << 60)
+
+
 def kernel_names(n, L, S, cfg, env=os.environ):
     """Kernel (template instance) behind each profiled family for this configuration, as rocprofv3
     names it (context.hip / ntt.hip launch choices)."""
     logn = n.bit_length() - 1
     on = lambda k: env.get(k, "1") != "0"
+    _, moduli, aux, *_ = CONFIGS[cfg]
+    if aux:   # HPS: generic kernels for the primes outside (2^60 - 2^32, 2^60)
+        primes = list(moduli) + list(aux)
+        gfwd, ginv = f"ntt_fwd_kernel<{logn}, true>", f"ntt_inv_kernel<{logn}, true>"
+        near_q = logn in (12, 13) and _near60(moduli[0]) and on("EXACTO_NTT_ASM")
+        fwd = f"ntt_fwd_pin_kernel<{logn}> + {gfwd}" if near_q else gfwd
+        inv = f"ntt_inv_pin_kernel<{logn}> + {ginv}" if near_q else ginv
+        tensor = f"ntt_inv_tensor_kernel<{logn}, {'true' if max(primes) < (1 << 60) else 'false'}, false>"
+        return {0: fwd, 1: inv, 2: tensor, 5: "hps_scale_kernel", 13: "dbfv_combine_kernel", 14: "hps_extend_kernel",
+                15: "relin_mac_lds_kernel", 16: "hps_scale_kernel"}
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
     fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and env.get("EXACTO_NTT_PIPE", "0") != "0"
            else f"ntt_fwd_pin_kernel<{logn}>" if asm and on("EXACTO_FWD_PIN")
@@ -146,6 +176,15 @@ def _entry(rec, name, share=None):
     return e
 
 
+def _latest_profile(suffix):
+    """profiles/rN_<suffix> of the latest round that has one (the committed PMC passes), or None."""
+    for r in range(9, 0, -1):
+        f = os.path.join(ROOT, "profiles", f"r{r}_{suffix}")
+        if os.path.exists(f):
+            return f
+    return None
+
+
 def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     """`batches` profiled batches after the timed region (single lane: per-kernel events time each
     kernel alone), every family; launch averages over all of them."""
@@ -158,19 +197,20 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     ctx.prof_enable(False)
     names = kernel_names(n, L, S, cfg)
     total = sum(r["ms"] for r in recs.values())
-    table = {KINDS[k]: _entry(r, names[k], r["ms"] / total if total else 0.0) for k, r in recs.items() if r["launches"]}
+    table = {KINDS[k]: _entry(r, names.get(k, KINDS[k]), r["ms"] / total if total else 0.0)
+             for k, r in recs.items() if r["launches"]}
     top = max(recs, key=lambda k: recs[k]["ms"])
     roof = {"bound": "hbm"}
-    roof.update(_entry(recs[top], names[top], recs[top]["ms"] / total if total else 0.0))
+    roof.update(_entry(recs[top], names.get(top, KINDS[top]), recs[top]["ms"] / total if total else 0.0))
     roof["family"] = KINDS[top]
     roof["traffic"] = None
     # HBM bytes per launch from the committed PMC passes over this bench configuration
     # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch with the gfx950 corrections)
-    tfile = os.path.join(ROOT, "profiles", f"r3_{cfg}_traffic.json")
-    if os.path.exists(tfile):
+    tfile = _latest_profile(f"{cfg}_traffic.json")
+    if tfile:
         with open(tfile) as f:
             tr = json.load(f).get("kernels", {})
-        hit = [v for k, v in tr.items() if names[top].split("<")[0] in k]
+        hit = [v for k, v in tr.items() if roof["kernel"].split("<")[0] in k]
         if hit:
             roof["traffic"] = round(hit[0]["traffic_bytes_avg"], 1)
             roof["traffic_over_algorithmic"] = round(hit[0]["traffic_bytes_avg"] / roof["bytes_per_launch"], 4)
@@ -178,11 +218,11 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     # the compute-side ceiling (integer modular arithmetic: VALU issue, not MFMA) from the committed
     # PMC pass: VALU wave-instructions and GPU cycles per dispatch, ~4.4 cycles per integer
     # multiply-class wave-instruction per SIMD (tools/op_rate.hip), 1024 SIMDs
-    vfile = os.path.join(ROOT, "profiles", f"r3_{cfg}_valu_counters.json")
-    if os.path.exists(vfile):
+    vfile = _latest_profile(f"{cfg}_valu_counters.json")
+    if vfile:
         with open(vfile) as f:
             vc = json.load(f).get("kernels", {})
-        hit = [v for k, v in vc.items() if names[top].split("<")[0] in k]
+        hit = [v for k, v in vc.items() if roof["kernel"].split("<")[0] in k]
         if hit:
             v = hit[0]
             need = v["valu_insts"] * 4.4 / 1024.0
@@ -193,11 +233,28 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     return roof, ntt, table
 
 
-def cpu_baseline(cfg, n, moduli, plain, gbase, dbfv, depth, sample):
+def _rate(run, threads, target_s, cap):
+    """units/s of run(k, threads): one unit per thread first, then (when that took well under the
+    target) a sample sized to about target_s seconds.  Returns (rate, units, seconds)."""
+    k = threads
+    t0 = time.perf_counter()
+    run(k, threads)
+    dt = time.perf_counter() - t0
+    if dt < 0.25 * target_s and k < cap:
+        k = min(cap, max(k, int(k * target_s / max(dt, 1e-6)) // threads * threads))
+        t0 = time.perf_counter()
+        run(k, threads)
+        dt = time.perf_counter() - t0
+    return k / dt, k, dt
+
+
+def cpu_baseline(cfg, n, moduli, aux, plain, gbase, dbfv, depth, sample):
     """The C restatement of the reference algorithm (oracle/c) on a bounded sample of the workload,
-    OpenMP over the products (the reference fans dbfv_mul's d^2 products out over rayon the same
-    way), on the host cores this job may use (16 on the GPU box, whose os.cpu_count() reports the
-    whole machine)."""
+    timed on the host cores this job may use (16 on the GPU box, whose os.cpu_count() reports the
+    whole machine) and on one thread.  OpenMP over the products mirrors the reference's rayon fan-out
+    of dbfv_mul's d^2 products (dbfv/eval.rs:117-122).  Each unit is the whole reference operation:
+    a bfv_mul_and_relin (HPS for cfg1 / u64dbfv, the exact BigInt schoolbook tensor otherwise,
+    eval.rs:89-413), a dbfv_mul item with all d^2 products, or cfg2's NTT product (ntt.rs:181-195)."""
     import numpy as np
     from oracle import params as P, cref
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -205,46 +262,97 @@ def cpu_baseline(cfg, n, moduli, plain, gbase, dbfv, depth, sample):
     if not cref.available():
         return {"value": None, "error": "oracle/c/liboracle.so not built"}
     threads = min(16, os.cpu_count() or 1)
-    prm = P.BfvParamsBuilder().ring_degree(n).plain_modulus(plain).ct_moduli(moduli).gadget_base(gbase).build()
     rng = np.random.default_rng(7)
-    rlk = uniform_residues(rng, (prm.gadget_digits, 2), moduli, n)
-    impl = "oracle/c (C restatement, exact multiword schoolbook tensor)"
-    if dbfv is None:
-        sample = sample or 8 * threads
-        ct1 = uniform_residues(rng, (sample, 2), moduli, n)
-        ct2 = uniform_residues(rng, (sample, 2), moduli, n)
+    impl = "oracle/c (C restatement of the reference algorithm)"
+    target_m, target_1 = 8.0, 4.0
+    if cfg == "cfg2":
+        q = moduli[0]
+        pool = 4096
+        a = rng.integers(0, q, size=(pool, n), dtype=np.uint64)
+        b = rng.integers(0, q, size=(pool, n), dtype=np.uint64)
+
+        def run(k, th):
+            for s0 in range(0, k, pool):
+                m = min(pool, k - s0)
+                cref.polymul(n, q, a[:m], b[:m], threads=th)
+        unit, what = "poly_mul/s", f"negacyclic NTT products (fwd x2 + pointwise + inv, n={n}, 1x60-bit)"
+        cap = 1 << 22
+    else:
+        bld = P.BfvParamsBuilder().ring_degree(n).plain_modulus(plain).ct_moduli(moduli).gadget_base(gbase)
+        if aux:
+            bld = bld.aux_moduli(aux)
+        prm = bld.build()
+        rlk = uniform_residues(rng, (prm.gadget_digits, 2), moduli, n)
+        pool = 64
+        if dbfv is None or (depth > 1 and cfg == "cfg5"):
+            ct1 = uniform_residues(rng, (pool, 2), moduli, n)
+            ct2 = uniform_residues(rng, (pool, 2), moduli, n)
+
+            def run_products(k, th):
+                for s0 in range(0, k, pool):
+                    m = min(pool, k - s0)
+                    cref.bfv_mul_and_relin(prm, ct1[:m], ct2[:m], rlk, threads=th)
+        if dbfv is None:
+            run = run_products
+            unit = "bfv_mul_and_relin/s"
+            what = (f"bfv_mul_and_relin (n={n}, L={len(moduli)}, "
+                    + ("literal HPS, eval.rs:157-413" if aux else "exact BigInt schoolbook tensor, eval.rs:113-147")
+                    + f", G={prm.gadget_digits})")
+            cap = 1 << 20
+        else:
+            d, base, dplain = dbfv
+            dp = P.DbfvParams(prm, base, d, dplain)
+            items = 1 if cfg == "cfg5" else 16
+            xa = uniform_residues(rng, (items, d, 2), moduli, n)
+            xb = uniform_residues(rng, (items, d, 2), moduli, n)
+
+            def run(k, th):
+                for s0 in range(0, k, items):
+                    m = min(items, k - s0)
+                    cref.dbfv_mul(dp, xa[:m], xb[:m], rlk, threads=th)
+            unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
+            what = f"dbfv_mul items (d={d}, all {d * d} products each, n={n}, L={len(moduli)}" + \
+                   (", HPS products" if aux else "") + ")"
+            cap = 1 << 16
+            if cfg == "cfg5":
+                # one measured dbfv_mul item (64 products, minutes on one thread at n = 8192), the chain
+                # being `depth` identical dbfv_mul steps; one thread: single products x d^2
+                t0 = time.perf_counter()
+                run(1, threads)
+                dt = time.perf_counter() - t0
+                r1, k1, t1 = _rate(run_products, 1, target_1, 1 << 10)
+                return {"value": 1.0 / dt / depth, "unit": unit, "cores": threads, "kind": "port",
+                        "sample": f"one dbfv_mul item (d={d}: all {d * d} products, n={n}, L={len(moduli)}) in "
+                                  f"{dt:.2f} s on {threads} threads, divided by the chain's {depth} steps; {impl}",
+                        "single_thread": {"value": r1 / (d * d * depth), "cores": 1,
+                                          "sample": f"{k1} bfv_mul_and_relin of the chain's parameters in {t1:.2f} s, "
+                                                    f"/ {d * d * depth} products per chain"}}
+    rm, km, tm = _rate(run, threads, target_m, cap)
+    r1, k1, t1 = _rate(run, 1, target_1, cap)
+    if depth > 1:
+        rm, r1 = rm / depth, r1 / depth
+    return {"value": rm, "unit": unit, "cores": threads, "kind": "port",
+            "sample": f"{km} {what} in {tm:.2f} s on {threads} threads; {impl}",
+            "single_thread": {"value": r1, "cores": 1, "sample": f"{k1} in {t1:.2f} s on 1 thread",
+                              "us_per_unit": round(1e6 / r1, 1)}}
+
+
+def latency_block(one_single, sync, reps=30):
+    """One call of the path on one unit (batch 1: a single bfv_mul_and_relin / dbfv_mul / chain),
+    synchronised, median over `reps` calls: the quantity the reference publishes (one call's latency
+    on its CPU, README.md:153, reports/paper_reproduction.md:9)."""
+    ts = []
+    for _ in range(3):
+        one_single()
+    sync()
+    for _ in range(reps):
         t0 = time.perf_counter()
-        cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=threads)
-        dt = time.perf_counter() - t0
-        return {"value": sample / dt, "unit": "bfv_mul_and_relin/s", "cores": threads, "kind": "port",
-                "sample": f"{sample} bfv_mul_and_relin of the same workload (n={n}, L={len(moduli)}), "
-                          f"{threads} threads, {impl}; {dt:.2f} s"}
-    d, base, dplain = dbfv
-    dp = P.DbfvParams(prm, base, d, dplain)
-    if depth == 1:
-        # whole dbfv_mul items (all d^2 products, sums, reduce)
-        sample = sample or max(1, (4 * threads) // (d * d))
-        a = uniform_residues(rng, (sample, d, 2), moduli, n)
-        b = uniform_residues(rng, (sample, d, 2), moduli, n)
-        t0 = time.perf_counter()
-        cref.dbfv_mul(dp, a, b, rlk, threads=threads)
-        dt = time.perf_counter() - t0
-        return {"value": sample / dt, "unit": "dbfv_mul/s", "cores": threads, "kind": "port",
-                "sample": f"{sample} dbfv_mul (d={d}, all {d * d} products each, n={n}, L={len(moduli)}), "
-                          f"{threads} threads, {impl}; {dt:.2f} s"}
-    # chains: one product per thread timed, scaled to the chain (depth dbfv_mul of d^2 products each):
-    # a whole chain item is minutes of CPU work at n = 8192
-    sample = sample or threads
-    ct1 = uniform_residues(rng, (sample, 2), moduli, n)
-    ct2 = uniform_residues(rng, (sample, 2), moduli, n)
-    t0 = time.perf_counter()
-    cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=threads)
-    dt = time.perf_counter() - t0
-    per_chain = depth * d * d
-    return {"value": sample / dt / per_chain, "unit": f"dbfv_mul_chain(depth {depth})/s", "cores": threads,
-            "kind": "port", "sample": f"{sample} bfv_mul_and_relin products of the chain's parameters (n={n}, "
-                                      f"L={len(moduli)}, base {gbase}) in {dt:.2f} s with {threads} threads, {impl}; "
-                                      f"scaled by {per_chain} products per chain (depth {depth} x d^2 = {d * d})"}
+        one_single()
+        sync()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return {"median_us": round(1e6 * ts[len(ts) // 2], 1), "min_us": round(1e6 * ts[0], 1), "calls": reps,
+            "batch": 1}
 
 
 def main():
@@ -268,7 +376,7 @@ def main():
     L = len(moduli)
     B = args.batch or DEFAULT_BATCH[args.config]
     if args.split == "limbs" and dbfv is None:
-        print("bench.py: --split limbs needs a dBFV config (cfg4, cfg5)", file=sys.stderr)
+        print("bench.py: --split limbs needs a dBFV config (cfg4, cfg5, u64dbfv)", file=sys.stderr)
         sys.exit(2)
     distributed = world > 1
     if args.dry:
@@ -337,6 +445,7 @@ def main():
     # ---- the step: one pass over one batch (`one(i)`, i = input copy), timed `reps` times per step
     nbuf = 2
     parts = None
+    one_single = None   # one call on one unit (latency_block)
     if args.config == "cfg2":
         a = [uniform((B,)) for _ in range(nbuf)]
         b = [uniform((B,)) for _ in range(nbuf)]
@@ -381,6 +490,9 @@ def main():
                 torch.add(ct1[i], ct2[i], out=outs[i])
             else:
                 ctx.bfv_mul_and_relin_dev(ct1[i], ct2[i], outs[i], B)
+
+        def one_single():
+            ctx.bfv_mul_and_relin_dev(ct1[0], ct2[0], outs[0], 1)
         unit = "bfv_mul_and_relin/s"
         metric = "ciphertext muls/sec (bfv_mul_and_relin)"
     else:
@@ -389,7 +501,8 @@ def main():
         y = [uniform((B, d, 2)) for _ in range(nbuf)]
         outs = [torch.empty_like(x[0]) for _ in range(nbuf)]
         if args.split == "limbs":
-            parts = xdist.limb_partition(d, world) if distributed else [list(range(d))]
+            parts = (xdist.limb_partition(d, world, xdist.limb_products(d, base, dplain)) if distributed
+                     else [list(range(d))])
             mine = parts[rank]
             compact = torch.zeros((B, max(len(mine), 1), 2, L, n), dtype=torch.int64, device=device)
             acc = [torch.empty_like(x[0]), torch.empty_like(x[0])]
@@ -423,6 +536,12 @@ def main():
                     ctx.dbfv_mul_dev(d, base, dplain, x[i], y[i], outs[i], B)
                 else:
                     ctx.dbfv_mul_chain_dev(d, base, dplain, x[i], y[i], outs[i], B, depth)
+
+            def one_single():
+                if depth == 1:
+                    ctx.dbfv_mul_dev(d, base, dplain, x[0], y[0], outs[0], 1)
+                else:
+                    ctx.dbfv_mul_chain_dev(d, base, dplain, x[0], y[0], outs[0], 1, depth)
         unit = "dbfv_mul/s" if depth == 1 else f"dbfv_mul_chain(depth {depth})/s"
         metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else f"dbfv_mul chains/sec (depth {depth})"
     sync()
@@ -471,16 +590,28 @@ def main():
     if not args.dry:
         roofline, ntt, kernels = roofline_block(ctx, lambda: one(0), args.config, n, L, S)
 
+    latency = None
+    if one_single is not None and not args.dry and world == 1:
+        latency = latency_block(one_single, sync)
+        if args.config in PUBLISHED:
+            pub = PUBLISHED[args.config]
+            latency["reference_published_us"] = pub["latency_us"]
+            latency["reference_source"] = pub["source"] + "; reference Rust CPU, hardware unstated"
+
     cpu = None
     if (rank == 0 and world == 1 and not args.dry and not args.no_cpu_baseline
-            and args.config in ("cfg3", "cfg4", "cfg5")):
+            and args.config != "galois"):
         try:   # informative; never fail the bench on it
-            cpu = cpu_baseline(args.config, n, moduli, plain, gbase, dbfv, depth, args.cpu_sample)
+            cpu = cpu_baseline(args.config, n, moduli, aux, plain, gbase, dbfv, depth, args.cpu_sample)
         except Exception as e:
             cpu = {"value": None, "error": repr(e)}
 
     if rank == 0:
-        workload = {"cfg2": "batched fwd NTT + pointwise mul + inv NTT, BASELINE configs[1]",
+        workload = {"cfg1": "bfv_mul_and_relin on compact_bfv (n=1024, 40-bit q, 1 HPS aux prime, G=3), "
+                            "BASELINE configs[0]",
+                    "u64dbfv": "dbfv_mul on u64_dbfv (n=4096, 60-bit q + 2 HPS aux primes, d=8 b=256 p=2^64, "
+                               "gadget 256), the reference's published paper_repro profile",
+                    "cfg2": "batched fwd NTT + pointwise mul + inv NTT, BASELINE configs[1]",
                     "cfg3": "bfv_mul_and_relin, BASELINE configs[2]",
                     "cfg4": "dbfv_mul d=2 b=256 p=2^16, BASELINE configs[3]",
                     "cfg5": "dbfv_mul chain depth 4, d=8 b=256 p=2^64, BASELINE configs[4]",
@@ -500,7 +631,9 @@ def main():
             "dtype": "u64",
             "data": "synthetic (uniform canonical residues per limb, seeded; two resident input copies "
                     "rotated; rlk made on rank 0 and broadcast)" + ("; DRY RUN: no GPU work" if args.dry else ""),
-            "config": {"workload": workload, "ring_degree": n, "ct_limbs": L, "limb_bits": 60,
+            "config": {"workload": workload, "ring_degree": n, "ct_limbs": L,
+                       "limb_bits": max(q.bit_length() for q in moduli),
+                       "aux_moduli": aux or None,
                        "plain_modulus": plain, "gadget_base": gbase, "gadget_digits": G,
                        "batch_per_gpu": B, "global_batch": B * (world if args.split == "batch" else 1),
                        "batches_per_step": reps, "units_per_step": units_per_step,
@@ -514,6 +647,7 @@ def main():
             "ntt": ntt,
             "kernels": kernels,
             "cpu_baseline": cpu,
+            "latency": latency,
         }
         if dbfv is not None:
             line["config"].update({"dbfv_digits": dbfv[0], "dbfv_base": dbfv[1],

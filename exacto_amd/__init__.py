@@ -9,4 +9,4 @@ broadcast) and ``bootstrap`` the host-side composition of bfv_host.rs.  The C++ 
 Rust API is include/exacto.hpp.
 """
 
-__version__ = "0.3.0"
+__version__ = "0.4.0"

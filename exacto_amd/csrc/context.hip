@@ -239,6 +239,12 @@ struct exacto_ctx {
     // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
     bool psum_env = true;
     int psum_max = 0;
+    // HPS: the division-free scale (q > 2^32, p < min(q, 2^32); EXACTO_HPS_LITERAL=1: the literal i128
+    // form, kept for the equivalence test) and, in dbfv_mul, the products' c0 / c1 and signed gadget
+    // digits summed per output limb before ONE forward NTT + relinearisation MAC per limb
+    // (EXACTO_HPS_SUM=0: per product)
+    bool hps_fast = false;
+    bool hps_sum_env = true;
     struct PsumPlan {
         bool on = false;
         int d = 0, npairs = 0;
@@ -246,6 +252,8 @@ struct exacto_ctx {
         const CombineTerm* terms = nullptr;
         u64* out = nullptr;       // [B][d][2][L][n], coefficient domain
     } psum;
+    u64* d_hdig = nullptr;       // dBFV over HPS: the summed digits' NTT residues [B][d][G][L][n]
+    size_t hdig_cap = 0;
     int16_t* d_dall = nullptr;   // dBFV: per-product digits
     void* d_dk = nullptr;        // ... and their per-limb sums (int16, or int32 when m B/2 > 2^15 - 1)
     uint32_t *d_dsk = nullptr, *d_uk = nullptr;   // their residues and key-switch sums in the 31-bit basis
@@ -861,6 +869,10 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_CRT_FWD")) c->crt_fwd = atoi(e);
+    if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
+    c->hps_fast = c->path == EXACTO_PATH_HPS && c->ctq[0] > (1ull << 32) && c->plain < c->ctq[0] &&
+                  c->plain < (1ull << 32);
+    if (const char* e = getenv("EXACTO_HPS_LITERAL")) c->hps_fast &= atoi(e) == 0;
     if (int rc = build_tables(c)) { exacto_ctx_destroy(c); return rc; }
     if (int rc = setup_ks32(c)) { exacto_ctx_destroy(c); return rc; }
     *out = c;
@@ -881,7 +893,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
         if (l.D16) (void)hipFree(l.D16);
     }
     free_dev(c->ext_a); free_dev(c->ext_b);
-    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_dall); free_dev(c->d_dk); free_dev(c->d_dsk); free_dev(c->d_uk); free_dev(c->pl_buf);
+    free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_dall); free_dev(c->d_hdig); free_dev(c->d_dk); free_dev(c->d_dsk); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
     free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
     free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst); free_dev(c->kw.d_rs);
@@ -974,7 +986,7 @@ extern "C" int exacto_ctx_load_relin_key(exacto_ctx* c, const uint64_t* rlk, siz
 enum ProfKind : int {
     PK_FWD = 0, PK_INV = 1, PK_TENSOR = 2, PK_POLYMUL = 3, PK_LIFT = 4, PK_SCALE = 5, PK_KS_DIGITS = 6,
     PK_KS_MAC = 7, PK_KS_CRT = 8, PK_PAIRSUM = 9, PK_PSUM_SCALE = 10, PK_TENSOR_C2 = 11, PK_DIGIT_SUM = 12,
-    PK_COMBINE = 13, PK_COUNT = 14
+    PK_COMBINE = 13, PK_HPS_EXT = 14, PK_RELIN_MAC = 15, PK_HPS_SCALE = 16, PK_COUNT = 17
 };
 
 struct ProfScope {
@@ -1243,7 +1255,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                      c->gbase <= 65536;
     // ... and then the key switch runs over the integers in the 31-bit basis (ks32.hip)
     const bool k32 = d16 && c->ks32 && c->S32 > 0;
-    const bool skip_fwd = coef && k32;
+    // HPS in dbfv_mul (dbfv_mul_group): the scale writes each product's signed digits to ks_defer,
+    // c0 / c1 stay in the coefficient domain; the caller sums both per output limb, then transforms
+    // and relinearises once per limb
+    const bool hps_defer = c->path == EXACTO_PATH_HPS && relin && guse > 0 && c->ks_defer && coef;
+    const bool skip_fwd = coef && (k32 || hps_defer);
     if (skip_fwd) *coef = true;
     if (relin && guse > 0) {
         // both before the second lane forks: its kernels read these too
@@ -1273,9 +1289,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             nb.dst = c->ws_coefQ + 2 * Ln;
             if (int e = run_ntt(c, nb, (long)cnt * 2 * L, true)) return e;
             // 2. extension to the auxiliary primes
-            if (c->path == EXACTO_PATH_HPS)
+            if (c->path == EXACTO_PATH_HPS) {
+                // per input poly: the q residues in, K auxiliary residues out
+                ProfScope pl(c, PK_HPS_EXT, 4ull * cnt, 8.0 * (1 + K) * n * 4.0 * cnt);
                 launch_hps_extend(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_primes, K, c->stream);
-            else {
+            } else {
                 ProfScope pl(c, PK_LIFT, 4ull * cnt, 8.0 * (L + K) * n * 4.0 * cnt);
                 launch_exact_lift(c->ws_coefQ, c->ws_extP, 4L * cnt, n, c->d_crt, c->d_primes, L, K,
                                   crt_mode(c), c->stream);
@@ -1309,13 +1327,19 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         u64* D = relin ? c->ws_D : nullptr;
         // scale bytes per item: the three components' L+K residues in; c0, c1 (L residues each) out
         // (psum: c2 only), and the third component's digits (int16 / int8) or its L residues
-        const double dig_b = d16 ? (c->ks_defer && c->ks_defer8 ? 1.0 : 2.0) * guse : 8.0 * L * (relin ? guse : 1);
+        const double dig_b = (d16 || hps_defer) ? (c->ks_defer && c->ks_defer8 ? 1.0 : 2.0) * guse
+                                                : 8.0 * L * (relin ? guse : 1);
         {   // (scoped: the events bracket the scale launch alone)
-        ProfScope psc(c, PK_SCALE, (u64)cnt, (double)n * cnt *
+        ProfScope psc(c, c->path == EXACTO_PATH_HPS ? PK_HPS_SCALE : PK_SCALE, (u64)cnt, (double)n * cnt *
                       ((ps.on ? 1.0 : 3.0) * 8.0 * (L + K) + (ps.on ? 0.0 : 16.0 * L) + (relin ? dig_b : 8.0 * L)));
-        if (c->path == EXACTO_PATH_HPS)
-            launch_hps_scale(c->ws_T, R, out_stride, ncomp, D, guse, cnt, n, c->d_crt, c->d_primes, K, c->stream);
-        else
+        if (c->path == EXACTO_PATH_HPS) {
+            void* d16p = hps_defer ? (c->ks_defer8 ? (void*)((int8_t*)c->ks_defer + s * (long)guse * n)
+                                                   : (void*)(c->ks_defer + s * (long)guse * n))
+                                   : nullptr;
+            launch_hps_scale(c->ws_T, R, out_stride, ncomp, hps_defer ? nullptr : D, d16p,
+                             hps_defer && c->ks_defer8, guse, cnt, n, c->d_crt, c->d_primes, K, c->hps_fast,
+                             c->stream);
+        } else
             launch_exact_scale(c->ws_T, R, out_stride, ncomp, d16 ? nullptr : D,
                                d16 ? (c->ks_defer ? (c->ks_defer8
                                                          ? (int16_t*)((int8_t*)c->ks_defer + s * (long)guse * n)
@@ -1384,7 +1408,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                 if (fused) continue;   // R is relinearised and in the NTT domain
             }
         }
-        if (skip_fwd) continue;
+        if (skip_fwd) continue;   // (hps_defer: digits and c0 / c1 are the caller's now)
         if (int e = run_ntt(c, rb, (long)cnt * ncomp * L, false)) return e;
         if (relin && guse > 0 && !k32) {
             NttBatch db = contiguous(c->ws_D, cnt, (long)guse * L, 0, L, n);
@@ -1395,8 +1419,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             if (int e = run_ntt(c, db, (long)cnt * guse * L, false)) return e;
             // 8. relinearisation MAC, in place on the output
             if (int e = ensure_rlk_companions(c)) return e;
-            launch_relin_mac(R, out_stride, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n, L,
-                             c->d_primes, c->stream);
+            {   // per item: c0, c1 and the G digit residues in, c0, c1 out (the key from LDS)
+                ProfScope pm(c, PK_RELIN_MAC, (u64)cnt, 8.0 * n * L * cnt * (4.0 + guse));
+                launch_relin_mac(R, out_stride, c->ws_D, c->d_rlk, c->d_rlk_s, guse, R, out_stride, cnt, n, L,
+                                 c->d_primes, c->stream);
+            }
             CHECK_LAUNCH();
         }
     }
@@ -1538,8 +1565,12 @@ static int bfv_addsub(exacto_ctx* c, bool sub, const u64* x, size_t p1, const u6
     const size_t pm = std::max(p1, p2);
     if (!B || !pm) return 0;
     if ((p1 && !x) || (p2 && !y) || !o) return invalid_param("null ciphertext pointer");
-    // in place only over an operand laid out like the output
-    if ((o == x && p1 != pm) || (o == y && p2 != pm))
+    // in place only over an operand laid out like the output; any other overlap is rejected
+    const size_t pw = (size_t)c->L * c->n;
+    auto overlaps = [&](const u64* in, size_t polys) {
+        return in && polys && in < o + B * pm * pw && o < in + B * polys * pw;
+    };
+    if ((overlaps(x, p1) && (o != x || p1 != pm)) || (overlaps(y, p2) && (o != y || p2 != pm)))
         return invalid_param("output may alias an input only when it has as many components as the output");
     launch_bfv_addsub(sub, x, (int)p1, y, (int)p2, o, (long)B, c->n, c->L, c->d_primes, c->stream);
     CHECK_LAUNCH();
@@ -1824,11 +1855,14 @@ static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
         nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
         if (int e = run_ntt(c, nb, cnt * 2 * L, true)) return e;
         u64* eo = ext + g0 * Kn2;
-        if (c->path == EXACTO_PATH_HPS)
+        if (c->path == EXACTO_PATH_HPS) {
+            ProfScope pl(c, PK_HPS_EXT, 2ull * cnt, 8.0 * (1 + K) * n * 2.0 * cnt);
             launch_hps_extend(c->ws_coefQ, eo, 2 * cnt, n, c->d_primes, K, c->stream);
-        else
+        } else {
+            ProfScope pl(c, PK_LIFT, 2ull * cnt, 8.0 * (L + K) * n * 2.0 * cnt);
             launch_exact_lift(c->ws_coefQ, eo, 2 * cnt, n, c->d_crt, c->d_primes, L, K,
                               crt_mode(c), c->stream);
+        }
         CHECK_LAUNCH();
         if (int e = run_ntt(c, contiguous(eo, cnt, 2L * K, L, K, n), cnt * 2 * K, false)) return e;
     }
@@ -1884,6 +1918,24 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     const bool long_runs = use_wide ? c->kw.long_runs : c->ks32_long_runs;
     const bool wide = (u64)m * (c->gbase / 2) > 32767;   // digit sums beyond int16
     const size_t Bd = B * dout, Sn = (size_t)S * c->n;
+    // HPS (u64_dbfv): with the products' c0 / c1 kept in the coefficient domain, relinearize is linear
+    // mod q in the gadget digits and so are the per-limb sums and the NTT: limb k = NTT(sum c0) +
+    // sum_g NTT(sum_p d_pg) (.) rlk_g.  The scale writes every product's signed digits (int8 when the
+    // base is at most 2^8), ks32_digit_sum adds them per output limb as int16 (|sum| <= m B / 2), and
+    // the forward NTTs and the MAC run once per output limb instead of once per product (u64_dbfv:
+    // 8 instead of 36 products' worth of 10 forward NTTs and one MAC per dbfv_mul).
+    const bool hps_sum = c->path == EXACTO_PATH_HPS && c->hps_sum_env && m > 0 && c->gbase <= 65536 &&
+                         (u64)m * (c->gbase / 2) <= 32767 && c->rlk_loaded && gu > 0 && c->n >= 1024 &&
+                         !c->deferred_code && !c->fused_ks;
+    if (hps_sum) {
+        if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
+            grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * 2, 8)) ||
+            grow(&c->d_hdig, &c->hdig_cap, std::max<size_t>(Bd * gu * c->L * c->n * sizeof(u64), 8)))
+            return EXACTO_ERR_HIP;
+        if (int e = ensure_rlk_companions(c)) return e;
+        c->ks_defer = c->d_dall;
+        c->ks_defer8 = c->digit8_env && c->gbase <= 256;
+    }
     if (sum_ks) {
         if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
             grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * (wide ? 4 : 2), 8)) ||
@@ -1922,7 +1974,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     c->ks_defer8 = false;
     c->psum.on = false;
     if (rc) return rc;
-    if (sum_ks && !coef) return fail(EXACTO_ERR_HIP, "internal: ks32 sums without the ks32 key switch");
+    if ((sum_ks || hps_sum) && !coef) return fail(EXACTO_ERR_HIP, "internal: digit sums without a deferred key switch");
     if (!psum) {
         ProfScope pk(c, PK_COMBINE, (u64)B * dout, 8.0 * c->n * B * 2 * c->L * (double)(npairs + dout));
         launch_dbfv_combine(c->prod, npairs, c->d_term_start, c->d_terms, out, (int)B, (int)dout, c->n, c->L,
@@ -1952,9 +2004,28 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         }
         CHECK_LAUNCH();
     }
+    if (hps_sum) {
+        const double nn = c->n;
+        {   // every product's digits in (1 or 2 B), one int16 sum per (limb, digit) out
+            ProfScope pd(c, PK_DIGIT_SUM, (u64)Bd, nn * gu * ((double)B * npairs * (in8 ? 1.0 : 2.0) + 2.0 * Bd));
+            ks32_digit_sum(c->d_dall, in8, npairs, c->d_term_start, c->d_terms, c->d_dk, false, (int)B, (int)dout,
+                           (int)gu, c->n, c->stream);
+        }
+        CHECK_LAUNCH();
+        NttBatch db = contiguous(c->d_hdig, (long)Bd, (long)gu * c->L, 0, c->L, c->n);
+        db.src16 = (const int16_t*)c->d_dk;
+        db.src16_item_stride = (long)gu * c->n;
+        if (int e = run_ntt(c, db, (long)Bd * gu * c->L, false)) return e;
+    }
     if (coef)
         if (int e = run_ntt(c, contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n), (long)B * dout * 2 * c->L, false))
             return e;
+    if (hps_sum) {
+        ProfScope pm(c, PK_RELIN_MAC, (u64)Bd, 8.0 * c->n * c->L * Bd * (4.0 + gu));
+        launch_relin_mac(out, 2L * c->L * c->n, c->d_hdig, c->d_rlk, c->d_rlk_s, (int)gu, out, 2L * c->L * c->n,
+                         (int)Bd, c->n, c->L, c->d_primes, c->stream);
+        CHECK_LAUNCH();
+    }
     return 0;
 }
 
@@ -3277,6 +3348,7 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
     ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
@@ -3297,6 +3369,7 @@ const Rccl& rccl() {
         sym(x.comm_init_rank, "ncclCommInitRank");
         sym(x.comm_destroy, "ncclCommDestroy");
         sym(x.comm_count, "ncclCommCount");
+        sym(x.comm_user_rank, "ncclCommUserRank");
         sym(x.broadcast, "ncclBroadcast");
         sym(x.all_gather, "ncclAllGather");
         sym(x.error_string, "ncclGetErrorString");
@@ -3350,23 +3423,51 @@ extern "C" int exacto_rccl_comm_destroy(void* comm) {
 }
 
 // In-place broadcast of `words` u64 at buf from root's buffer, enqueued on the context stream.
-static int rccl_bcast(exacto_ctx* c, void* comm, int root, u64* buf, size_t words) {
+// Checks the communicator and the root first; *my_rank (optional) receives this rank.
+static int rccl_check(void* comm, int root, int* my_rank) {
     if (!comm) return invalid_param("null communicator");
     if (int e = rccl_ready()) return e;
     int nr = 0;
     RCCL_TRY(rccl().comm_count((ncclComm_t)comm, &nr));
     if (root < 0 || root >= nr) return invalid_param("root out of range");
+    if (my_rank) RCCL_TRY(rccl().comm_user_rank((ncclComm_t)comm, my_rank));
+    return 0;
+}
+
+static int rccl_bcast(exacto_ctx* c, void* comm, int root, u64* buf, size_t words) {
+    if (int e = rccl_check(comm, root, nullptr)) return e;
     if (!words) return 0;
     RCCL_TRY(rccl().broadcast(buf, buf, words, ncclUint64, root, (ncclComm_t)comm, c->stream));
     return 0;
 }
 
+// Every check runs before the resident key is touched: a failed call (bad root, no RCCL, a root
+// without a loaded key of that size) leaves the context's key exactly as it was.  The root
+// broadcasts its resident key as loaded (never resized); a receiving rank's buffer is (re)sized and
+// marked loaded only once the broadcast into it has been enqueued.
 extern "C" int exacto_ctx_broadcast_relin_key(exacto_ctx* c, void* comm, int root, size_t num_keys) {
     if (int e = check_ctx(c)) return e;
-    // the root's resident key stays as loaded; every other rank's buffer is (re)sized first
+    int me = -1;
+    if (int e = rccl_check(comm, root, &me)) return e;
+    const size_t words = num_keys * 2 * c->L * (size_t)c->n;
+    if (me == root) {
+        if (!c->rlk_loaded || c->rlk_keys != num_keys)
+            return invalid_param("broadcast root has no resident relinearization key of " + std::to_string(num_keys) +
+                                 " rows");
+        if (!words) return 0;
+        RCCL_TRY(rccl().broadcast(c->d_rlk, c->d_rlk, words, ncclUint64, root, (ncclComm_t)comm, c->stream));
+        return 0;
+    }
     u64* dst = exacto_ctx_relin_key_buffer(c, num_keys);
     if (!dst) return fail(EXACTO_ERR_HIP, "HIP error: relinearization key allocation failed");
-    return rccl_bcast(c, comm, root, dst, num_keys * 2 * c->L * (size_t)c->n);
+    if (words) {
+        const ncclResult_t r = rccl().broadcast(dst, dst, words, ncclUint64, root, (ncclComm_t)comm, c->stream);
+        if (r != ncclSuccess) {
+            c->rlk_loaded = false;   // the buffer's contents are undefined now
+            return fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(r) + " (ncclBroadcast)");
+        }
+    }
+    return 0;
 }
 
 extern "C" int exacto_broadcast_galois_key(exacto_ctx* c, void* comm, int root, uint64_t* gk, size_t num_keys) {
@@ -3385,4 +3486,4 @@ extern "C" int exacto_rccl_allgather_u64(exacto_ctx* c, void* comm, const uint64
     return 0;
 }
 
-extern "C" const char* exacto_version(void) { return "exacto-hip 0.1.0 (gfx950)"; }
+extern "C" const char* exacto_version(void) { return "exacto-hip 0.4.0 (gfx950)"; }

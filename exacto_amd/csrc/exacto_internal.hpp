@@ -187,8 +187,10 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false,
                         bool digits8 = false);
-void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
-                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
+// D: digits as residues mod q [item][g][n]; D16 (instead): signed int16 (d8: int8) digits [item][g][n].
+// fast: q > 2^32 and p < min(q, 2^32): the division-free form (bit-identical to the literal one)
+void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, void* D16, bool d8, int guse,
+                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K, bool fast,
                       hipStream_t s);
 // D16 != nullptr (gadget base <= 2^16): signed int16 digits [item][g][n] instead of residues
 void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items, int n,

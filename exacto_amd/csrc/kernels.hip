@@ -120,11 +120,11 @@ __device__ __forceinline__ u64 mr_eval_fast(const u64 (&v)[MAXN], int cnt, bool 
 // Writes digit g, limb i at D[g * L * n + i * n] (D already offset by the coefficient j), or, with
 // D16 (gadget base <= 2^16: every balanced digit lies in [-2^15, 2^15)), the signed digit once
 // at D16[g * n] for all limbs: 2 bytes per digit instead of 8 L.
-template <bool NEAR, int LT = 0>
+template <bool NEAR, int LT = 0, typename DT = int16_t>
 __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], int L_arg,
                                               const CrtTables* __restrict__ C,
                                               const PrimeConst* __restrict__ primes, u64* D, int n, int guse,
-                                              int16_t* D16 = nullptr) {
+                                              DT* D16 = nullptr) {
     const int L = LT ? LT : L_arg;  // LT > 0: limb count known at compile time
     u64 z[EXACTO_MAX_L];
     garner_q<NEAR>(z, res, L, C, primes);
@@ -214,8 +214,8 @@ __device__ __forceinline__ void gadget_digits(const u64 (&res)[EXACTO_MAX_L], in
                 }
             }
         }
-        if (D16) {
-            D16[(long)g * n] = (int16_t)(dneg ? -(i64)mag : (i64)mag);
+        if (D16) {   // int16 (base <= 2^16) or int8 (base <= 2^8) signed digit
+            D16[(long)g * n] = (DT)(dneg ? -(i64)mag : (i64)mag);
             continue;
         }
         // digit residue (rem mod Q) mod q_i == rem mod q_i; |rem| < B <= q_i when digit_small
@@ -887,7 +887,36 @@ void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d,
                        out, items, n, d, base, plain, t, scalar ? 1 : 0);
 }
 
-// ---------------------------------------------------------------- literal HPS scale
+// ---------------------------------------------------------------- HPS scale (eval.rs:257-413)
+
+// HPS round(p a_c / q) + p m (mod q) without i128 division (FAST: q > 2^32 and p < min(q, 2^32)).
+// Every step is exact integer arithmetic, so the result equals the literal form below bit for bit:
+//   * the rounding quotient x / q, x = p |a_c| + floor(q/2) < 2^95, is at most p/2 + 1 < 2^31: a
+//     double estimate is off by at most one and is corrected against the exact 128-bit remainder;
+//   * the m-recovery products are canonical residues, so the Barrett mul_mod equals ref_mod_mul's
+//     exact u128 % (and its Barrett branch for moduli <= 2^32, exact below m^2);
+//   * (a + b) mod q for the integer sum round + p m is formed from each part mod q (a ring map):
+//     m mod q with |m| < 2^111 splits as hi 2^64 + lo, both reduced.
+__device__ __forceinline__ u64 hps_round_mod(u64 a, u64 q, u64 p, const PrimeConst& Pq) {
+    const bool neg = a > q / 2;
+    const u64 mag = neg ? q - a : a;                      // |a_c|
+    const u128 x = (u128)p * mag + (q / 2);
+    u64 est = (u64)((double)x / (double)q);
+    i128 r = (i128)x - (i128)((u128)est * q);
+    while (r < 0) { --est; r += q; }
+    while (r >= (i128)q) { ++est; r -= q; }
+    // round_pa_q = +/- est; mod q (est < 2^31 < q)
+    return (neg && est) ? q - est : est;
+}
+
+__device__ __forceinline__ u64 hps_ext_fast(u64 a, u64 q, const PrimeConst& P) {
+    // eval.rs:307-313 with reduce64 instead of the % of a runtime divisor
+    if (a > q / 2) {
+        const u64 rem = reduce64(q - a, P.q, P.mu64);
+        return rem == 0 ? 0 : P.q - rem;
+    }
+    return reduce64(a, P.q, P.mu64);
+}
 
 __device__ __forceinline__ u64 hps_ext(u64 a, u64 q, u64 pj) {
     // eval.rs:307-313
@@ -898,70 +927,119 @@ __device__ __forceinline__ u64 hps_ext(u64 a, u64 q, u64 pj) {
     return a % pj;
 }
 
+// Scaled component c of one item, coefficient j (eval.rs:257-413).  The third component's balanced
+// gadget digits go to D as residues mod q ([item][g][n]) or, with DT = int16_t / int8_t, to D16 as
+// signed digits (gadget base <= 2^16 / 2^8; dBFV sums them per output limb before one key switch).
+template <bool FAST, typename DT>
 __global__ void __launch_bounds__(TPB)
 hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                 u64* __restrict__ D, int guse, int n, int K, const CrtTables* __restrict__ C,
-                 const PrimeConst* __restrict__ primes) {
+                 u64* __restrict__ D, DT* __restrict__ D16, int guse, int n, int K,
+                 const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
     const long item = row / 3;
     const int comp = (int)(row - item * 3);
+    if (comp >= ncomp_r && (comp != 2 || (D == nullptr && D16 == nullptr))) return;
     const u64* Tin = T + row * (1 + K) * n + j;
     const u64 q = primes[0].q;
     const u64 p = C->plain;
-    const i128 q128 = (i128)q;
     const u64 a = Tin[0];
-    const u64 half_q = q / 2;
-    const i128 a_centered = a > half_q ? (i128)a - q128 : (i128)a;
-    const i128 pa = (i128)p * a_centered;
-    const i128 round_pa_q = pa >= 0 ? (pa + q128 / 2) / q128 : -((-pa + q128 / 2) / q128);
     u64 result;
-    if (K == 1) {
-        // eval.rs:301-332
-        const u64 big_p = primes[1].q;
-        const u64 b = Tin[n];
-        const u64 a_ext = hps_ext(a, q, big_p);
-        const u64 diff = b >= a_ext ? b - a_ext : big_p - a_ext + b;
-        const u64 m_raw = ref_mod_mul(diff, C->hps_qinv[0], big_p);
-        const i128 m_centered = m_raw > big_p / 2 ? (i128)m_raw - (i128)big_p : (i128)m_raw;
-        const i128 scaled = round_pa_q + (i128)p * m_centered;
-        result = (u64)(((scaled % q128) + q128) % q128);
+    if (FAST) {
+        const PrimeConst& Pq = primes[0];
+        const u64 rq = hps_round_mod(a, q, p, Pq);
+        u64 mq;   // m mod q, Euclidean
+        if (K == 1) {
+            // eval.rs:301-332
+            const PrimeConst& P1 = primes[1];
+            const u64 bp = P1.q;
+            const u64 diff = sub_mod(Tin[n], hps_ext_fast(a, q, P1), bp);
+            const u64 m_raw = mul_mod(diff, C->hps_qinv[0], P1);
+            const bool mneg = m_raw > bp / 2;
+            const u64 mag = mneg ? bp - m_raw : m_raw;
+            const u64 r = reduce64(mag, q, Pq.mu64);
+            mq = (mneg && r) ? q - r : r;
+        } else {
+            // eval.rs:349-404: m from its residues mod p0, p1 by CRT, centred mod P = p0 p1
+            const PrimeConst& P0 = primes[1];
+            const PrimeConst& P1 = primes[2];
+            const u64 p0 = P0.q, p1 = P1.q;
+            const u64 m0 = mul_mod(sub_mod(Tin[n], hps_ext_fast(a, q, P0), p0), C->hps_qinv[0], P0);
+            const u64 m1 = mul_mod(sub_mod(Tin[2L * n], hps_ext_fast(a, q, P1), p1), C->hps_qinv[1], P1);
+            const u64 t0 = mul_mod(m0, C->hps_p1_inv_p0, P0);
+            const u64 t1 = mul_mod(m1, C->hps_p0_inv_p1, P1);
+            const u128 bigp = (u128)p0 * p1;
+            u128 mc = (u128)t0 * p1 + (u128)t1 * p0;           // < 2 P
+            if (mc >= bigp) mc -= bigp;
+            const bool mneg = mc > bigp / 2;
+            const u128 mag = mneg ? bigp - mc : mc;
+            // mag mod q = (hi (2^64 mod q) + lo) mod q
+            const u64 c64 = reduce64((u64)0 - q, q, Pq.mu64);
+            const u64 hi = reduce64((u64)(mag >> 64), q, Pq.mu64);
+            const u64 r = add_mod(mul_mod(hi, c64, Pq), reduce64((u64)mag, q, Pq.mu64), q);
+            mq = (mneg && r) ? q - r : r;
+        }
+        result = add_mod(rq, mul_mod(p, mq, Pq), q);
     } else {
-        // eval.rs:349-404
-        const u64 p0 = primes[1].q, p1 = primes[2].q;
-        const u64 b0 = Tin[n], b1 = Tin[2L * n];
-        const u64 a_ext0 = hps_ext(a, q, p0);
-        const u64 diff0 = b0 >= a_ext0 ? b0 - a_ext0 : p0 - a_ext0 + b0;
-        const u64 m0 = ref_mod_mul(diff0, C->hps_qinv[0], p0);
-        const u64 a_ext1 = hps_ext(a, q, p1);
-        const u64 diff1 = b1 >= a_ext1 ? b1 - a_ext1 : p1 - a_ext1 + b1;
-        const u64 m1 = ref_mod_mul(diff1, C->hps_qinv[1], p1);
-        const i128 t0 = (i128)ref_mod_mul(m0, C->hps_p1_inv_p0, p0);
-        const i128 t1 = (i128)ref_mod_mul(m1, C->hps_p0_inv_p1, p1);
-        const i128 big_p = (i128)p0 * (i128)p1;
-        const i128 half_big_p = big_p / 2;
-        const i128 crt_sum = t0 * (i128)p1 + t1 * (i128)p0;
-        const i128 m_crt = crt_sum % big_p;
-        const i128 m_centered = m_crt > half_big_p ? m_crt - big_p : m_crt;
-        const i128 m_mod_q = ((m_centered % q128) + q128) % q128;
-        const u64 round_mod_q = (u64)(((round_pa_q % q128) + q128) % q128);
-        const u64 pm_mod_q = ref_mod_mul(p, (u64)m_mod_q, q);
-        result = (u64)(((u128)round_mod_q + pm_mod_q) % q);
+        const i128 q128 = (i128)q;
+        const u64 half_q = q / 2;
+        const i128 a_centered = a > half_q ? (i128)a - q128 : (i128)a;
+        const i128 pa = (i128)p * a_centered;
+        const i128 round_pa_q = pa >= 0 ? (pa + q128 / 2) / q128 : -((-pa + q128 / 2) / q128);
+        if (K == 1) {
+            // eval.rs:301-332
+            const u64 big_p = primes[1].q;
+            const u64 b = Tin[n];
+            const u64 a_ext = hps_ext(a, q, big_p);
+            const u64 diff = b >= a_ext ? b - a_ext : big_p - a_ext + b;
+            const u64 m_raw = ref_mod_mul(diff, C->hps_qinv[0], big_p);
+            const i128 m_centered = m_raw > big_p / 2 ? (i128)m_raw - (i128)big_p : (i128)m_raw;
+            const i128 scaled = round_pa_q + (i128)p * m_centered;
+            result = (u64)(((scaled % q128) + q128) % q128);
+        } else {
+            // eval.rs:349-404
+            const u64 p0 = primes[1].q, p1 = primes[2].q;
+            const u64 b0 = Tin[n], b1 = Tin[2L * n];
+            const u64 a_ext0 = hps_ext(a, q, p0);
+            const u64 diff0 = b0 >= a_ext0 ? b0 - a_ext0 : p0 - a_ext0 + b0;
+            const u64 m0 = ref_mod_mul(diff0, C->hps_qinv[0], p0);
+            const u64 a_ext1 = hps_ext(a, q, p1);
+            const u64 diff1 = b1 >= a_ext1 ? b1 - a_ext1 : p1 - a_ext1 + b1;
+            const u64 m1 = ref_mod_mul(diff1, C->hps_qinv[1], p1);
+            const i128 t0 = (i128)ref_mod_mul(m0, C->hps_p1_inv_p0, p0);
+            const i128 t1 = (i128)ref_mod_mul(m1, C->hps_p0_inv_p1, p1);
+            const i128 big_p = (i128)p0 * (i128)p1;
+            const i128 half_big_p = big_p / 2;
+            const i128 crt_sum = t0 * (i128)p1 + t1 * (i128)p0;
+            const i128 m_crt = crt_sum % big_p;
+            const i128 m_centered = m_crt > half_big_p ? m_crt - big_p : m_crt;
+            const i128 m_mod_q = ((m_centered % q128) + q128) % q128;
+            const u64 round_mod_q = (u64)(((round_pa_q % q128) + q128) % q128);
+            const u64 pm_mod_q = ref_mod_mul(p, (u64)m_mod_q, q);
+            result = (u64)(((u128)round_mod_q + pm_mod_q) % q);
+        }
     }
     if (comp < ncomp_r) R[item * r_stride + (long)comp * n + j] = result;
-    if (comp == 2 && D != nullptr) {
+    if (comp == 2) {
         u64 res[EXACTO_MAX_L];
         res[0] = result;
-        gadget_digits<false>(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
+        if (D16) gadget_digits<false, 1, DT>(res, 1, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
+        else if (D) gadget_digits<false, 1>(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
     }
 }
 
-void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int guse,
-                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K,
+void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, void* D16, bool d8, int guse,
+                      int items, int n, const CrtTables* ct, const PrimeConst* primes, int K, bool fast,
                       hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(hps_scale_kernel, dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,
-                       guse, n, K, ct, primes);
+#define HPS_(F, DT) hipLaunchKernelGGL((hps_scale_kernel<F, DT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, \
+                                       ncomp_r, D, (DT*)D16, guse, n, K, ct, primes)
+    if (fast) {
+        if (d8) HPS_(true, int8_t); else HPS_(true, int16_t);
+    } else {
+        if (d8) HPS_(false, int8_t); else HPS_(false, int16_t);
+    }
+#undef HPS_
 }
 
 // ---------------------------------------------------------------- standalone decomposition
@@ -1171,10 +1249,11 @@ void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys,
 // min(p1, p2) is a +/- b; beyond it the longer operand's component passes through, negated when
 // it is ct2's under subtraction.  ct1 [B][p1][L][n], ct2 [B][p2][L][n], out [B][max][L][n]; row =
 // (item * max + comp) * L + limb.  out may alias ct1 or ct2 only when its component count equals
-// that operand's (same strides).
+// that operand's (same strides): each thread reads its element before writing it, so a, b and out
+// are not __restrict__ (the host rejects any other overlap).
 __global__ void __launch_bounds__(TPB)
-bfv_addsub_kernel(int sub, const u64* __restrict__ a, int p1, const u64* __restrict__ b, int p2,
-                  u64* __restrict__ out, int n, int L, const PrimeConst* __restrict__ primes) {
+bfv_addsub_kernel(int sub, const u64* a, int p1, const u64* b, int p2, u64* out, int n, int L,
+                  const PrimeConst* __restrict__ primes) {
     ROW_SETUP(n)
     const int pm = p1 > p2 ? p1 : p2;
     const int limb = (int)(row % L);

@@ -76,10 +76,36 @@ def gather_to(shard_out: torch.Tensor, total: int, dst: int = 0):
     return torch.cat([parts[r][: shard(total, r, world)[1]] for r in range(world)])
 
 
-def limb_products(d: int) -> list[int]:
-    """Products per output limb k < d of a dbfv_mul with all-zero small representatives (every
-    BASELINE dBFV config): the pairs (i, j) with i + j = k, i.e. k + 1 of them."""
-    return [k + 1 for k in range(d)]
+def small_reps(base: int, d: int, plain: int) -> list[list[int]]:
+    """reps[j - d] = the base-b digits of base^j mod p for j = d .. 2d-2 (lattice.rs:104-122
+    compute_simple; p = 0 is 2^64 by wrapping_pow), as exacto_hip's dbfv_plan computes them."""
+    reps = []
+    for j in range(d, 2 * d - 1):
+        val = pow(base, j, 1 << 64) if plain == 0 else pow(base, j, plain)
+        dg = []
+        for _ in range(d):
+            dg.append(val % base)
+            val //= base
+        reps.append(dg)
+    return reps
+
+
+def limb_products(d: int, base: int | None = None, plain: int | None = None) -> list[int]:
+    """Products each output limb k < d of a dbfv_mul needs: the pairs (i, j) with a nonzero
+    coefficient for k -- 1 when i + j = k, reps[i + j - d][k] when i + j >= d (the reduce folding,
+    reduction.rs:34-52) -- the same rule as the library's dbfv_plan.  Without (base, plain) the
+    small representatives are taken as all zero (every BASELINE dBFV config): k + 1 pairs."""
+    reps = small_reps(base, d, plain) if base is not None else None
+    out = []
+    for k in range(d):
+        cnt = 0
+        for i in range(d):
+            for j in range(d):
+                s = i + j
+                coef = 1 if s == k else (reps[s - d][k] if (reps is not None and s >= d) else 0)
+                cnt += coef != 0
+        out.append(cnt)
+    return out
 
 
 def limb_partition(d: int, world: int, weights=None) -> list[list[int]]:

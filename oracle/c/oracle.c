@@ -600,11 +600,15 @@ int oracle_bfv_mul(int n, int L, const u64* q, int K, const u64* aux, u64 plain,
  * (eval.rs:124-132), then limbs j >= d folded into limbs i < d with the small representatives of
  * base^j mod p (lattice.rs:104-122; p = 0 is 2^64 by wrapping_pow), scaled by |coef| (NTT-domain
  * scalar_mul) and negated for coef < 0 (reduction.rs:65-93).  Depth guard: the caller's. */
-int oracle_dbfv_mul(int n, int L, const u64* q, u64 plain, u64 gbase, int G, int d, u64 base, u64 dplain,
-                    const u64* a, const u64* b, const u64* rlk, int nkeys, u64* out, int B, int threads) {
-    if (L > MAXL || L < 1 || d < 1) return 1;
+int oracle_dbfv_mul(int n, int L, const u64* q, int K, const u64* aux, u64 plain, u64 gbase, int G, int d,
+                    u64 base, u64 dplain, const u64* a, const u64* b, const u64* rlk, int nkeys, u64* out, int B,
+                    int threads) {
+    if (L > MAXL || L < 1 || d < 1 || (L == 1 && K > 2)) return 1;
+    /* the products dispatch as bfv_mul_no_relin does (eval.rs:99-107): L == 1 with an aux basis
+     * takes the literal HPS multiplier (u64_dbfv, presets.rs:61-75), otherwise the exact one */
+    const int hps = (L == 1 && K > 0);
     octx_t c;
-    octx_init(&c, n, L, q, 0, NULL, plain, gbase, G);
+    octx_init(&c, n, L, q, hps ? K : 0, aux, plain, gbase, G);
     const size_t ctw = (size_t)2 * L * n;
     const int guse = G < nkeys ? G : nkeys;
     const int R = 2 * d - 1;
@@ -616,7 +620,7 @@ int oracle_dbfv_mul(int n, int L, const u64* q, u64 plain, u64 gbase, int G, int
     for (long w = 0; w < (long)B * d * d; ++w) {
         const long item = w / (d * d);
         const int i = (int)(w % (d * d)) / d, j = (int)(w % d);
-        bfv_mul_one(&c, 0, a + ((size_t)item * d + i) * ctw, b + ((size_t)item * d + j) * ctw, rlk, guse, 1,
+        bfv_mul_one(&c, hps, a + ((size_t)item * d + i) * ctw, b + ((size_t)item * d + j) * ctw, rlk, guse, 1,
                     prod + (size_t)w * ctw);
     }
     u64* limbs = (u64*)calloc((size_t)R * ctw, sizeof(u64));
@@ -676,6 +680,36 @@ int oracle_ntt(int n, u64 q, u64* polys, int count, int inverse, int threads) {
     for (int b = 0; b < count; ++b) {
         if (inverse) ntt_inv(&p, polys + (size_t)b * n);
         else ntt_fwd(&p, polys + (size_t)b * n);
+    }
+    plan_free(&p);
+    return 0;
+}
+
+/* Negacyclic products through the NTT, as the reference's own test composes them (ntt.rs:181-195):
+ * out = INTT(NTT(a) (.) NTT(b)) per poly, a, b, out = [count][n] coefficient domain mod q (the cfg2
+ * CPU baseline: two forward transforms, the pointwise ref_mod_mul, one inverse + normalize). */
+int oracle_polymul(int n, u64 q, const u64* a, const u64* b, u64* out, int count, int threads) {
+    plan_t p;
+    plan_init(&p, n, q);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+#endif
+    {
+        u64* t = (u64*)malloc(sizeof(u64) * (size_t)n);
+#ifdef _OPENMP
+#pragma omp for
+#endif
+        for (int k = 0; k < count; ++k) {
+            u64* o = out + (size_t)k * n;
+            memcpy(o, a + (size_t)k * n, sizeof(u64) * (size_t)n);
+            memcpy(t, b + (size_t)k * n, sizeof(u64) * (size_t)n);
+            ntt_fwd(&p, o);
+            ntt_fwd(&p, t);
+            for (int j = 0; j < n; ++j) o[j] = ref_mod_mul(o[j], t[j], q);
+            ntt_inv(&p, o);
+        }
+        free(t);
     }
     plan_free(&p);
     return 0;

@@ -28,8 +28,10 @@ def _load():
         lib.oracle_bfv_mul.restype = I
         lib.oracle_ntt.argtypes = [I, U, P, I, I, I]
         lib.oracle_ntt.restype = I
-        lib.oracle_dbfv_mul.argtypes = [I, I, P, U, U, I, I, U, U, P, P, P, I, P, I, I]
+        lib.oracle_dbfv_mul.argtypes = [I, I, P, I, P, U, U, I, I, U, U, P, P, P, I, P, I, I]
         lib.oracle_dbfv_mul.restype = I
+        lib.oracle_polymul.argtypes = [I, U, P, P, P, I, I]
+        lib.oracle_polymul.restype = I
         _lib = lib
     return _lib
 
@@ -71,12 +73,24 @@ def dbfv_mul(dparams, a, b, rlk, threads=1):
     a, b, rlk = _u64(a), _u64(b), _u64(rlk)
     B, d, _, L, n = a.shape
     q = _u64(prm.ct_basis.moduli)
+    aux = _u64(prm.aux_basis.moduli) if prm.aux_basis is not None else np.zeros(1, np.uint64)
+    K = len(prm.aux_basis.moduli) if prm.aux_basis is not None else 0
     out = np.zeros_like(a)
-    rc = lib.oracle_dbfv_mul(n, L, q.ctypes.data, prm.plain_modulus, prm.gadget_base, prm.gadget_digits, d,
+    rc = lib.oracle_dbfv_mul(n, L, q.ctypes.data, K, aux.ctypes.data, prm.plain_modulus, prm.gadget_base,
+                             prm.gadget_digits, d,
                              dparams.base, dparams.plain_modulus, a.ctypes.data, b.ctypes.data,
                              rlk.ctypes.data if rlk.size else None, rlk.shape[0], out.ctypes.data, B, threads)
     if rc != 0:
         raise ValueError("oracle_dbfv_mul: unsupported parameters")
+    return out
+
+
+def polymul(n, q, a, b, threads=1):
+    """INTT(NTT(a) (.) NTT(b)) of coefficient-domain polys [count][n] mod q (ntt.rs:181-195)."""
+    lib = _load()
+    a, b = _u64(a), _u64(b)
+    out = np.empty_like(a)
+    lib.oracle_polymul(n, q, a.ctypes.data, b.ctypes.data, out.ctypes.data, a.size // n, threads)
     return out
 
 

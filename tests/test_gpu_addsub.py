@@ -67,3 +67,10 @@ def test_bfv_add_dev_in_place_and_alias_rule(gpu_available):
     with pytest.raises(ExactoError) as e:  # over the shorter one: rejected, never silently wrong
         ctx.bfv_add_dev(a, 3, b, 2, b, B)
     assert e.value.variant == "InvalidParam"
+    # a partial overlap (output shifted by one component into ct1) is rejected too
+    big = torch.zeros((B + 1) * 3 * n, dtype=torch.int64, device=dev)
+    x = big[: B * 3 * n]
+    o = big[n: n + B * 3 * n]
+    with pytest.raises(ExactoError) as e:
+        ctx.bfv_add_dev(x, 3, b, 2, o, B)
+    assert e.value.variant == "InvalidParam"

@@ -26,13 +26,17 @@ VARIANTS = {
     "polymul_pin": {"EXACTO_POLYMUL_PIN": "1"},
     "crt_fwd_pin": {"EXACTO_CRT_FWD": "4"},
     "crt_fwd_3waves": {"EXACTO_CRT_FWD": "3"},
+    # HPS: the literal i128 scale against the division-free one, per-product relinearisation against
+    # dbfv_mul's per-limb digit sums
+    "hps_literal": {"EXACTO_HPS_LITERAL": "1"},
+    "hps_per_product": {"EXACTO_HPS_SUM": "0"},
 }
 
 
 def _digests(extra_env):
     env = dict(os.environ)
     for k in ("EXACTO_TENSOR_PIN", "EXACTO_FWD_PIN", "EXACTO_NTT_PIPE", "EXACTO_POLYMUL_PIN", "EXACTO_TENSOR3",
-              "EXACTO_CRT_FWD"):
+              "EXACTO_CRT_FWD", "EXACTO_HPS_LITERAL", "EXACTO_HPS_SUM"):
         env.pop(k, None)
     env.update(extra_env)
     r = subprocess.run([sys.executable, os.path.join(HERE, "variant_digest.py")], env=env, capture_output=True,

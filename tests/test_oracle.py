@@ -339,3 +339,44 @@ def test_c_dbfv_mul_matches_python(base, d, p):
         cb = odbfv.DbfvCiphertext([np_to_ct(b[it, i], prm) for i in range(d)], d, 0, dp)
         want = np.stack([ct_to_np(l) for l in odbfv.dbfv_mul(ca, cb, rk).limbs])
         assert np.array_equal(got[it], want)
+
+
+def test_c_dbfv_mul_hps_matches_python():
+    """oracle/c oracle_dbfv_mul over the literal HPS multiplier (L = 1 with two aux primes, the
+    u64_dbfv preset's basis, presets.rs:61-75, at n = 16) == the Python restatement: every one of the
+    d^2 products dispatches to bfv_mul_hps (eval.rs:99-107, 157-413)."""
+    if not cref.available():
+        pytest.skip("oracle/c not built")
+    from bridge import np_to_ct, ct_to_np, np_to_rlk, uniform_residues
+    ref = P.u64_dbfv()
+    b0 = ref.bfv_params
+    n, d = 16, 8
+    prm = (P.BfvParamsBuilder().ring_degree(n).plain_modulus(b0.plain_modulus).ct_moduli(b0.ct_basis.moduli)
+           .aux_moduli(b0.aux_basis.moduli).gadget_base(b0.gadget_base).build())
+    dp = P.DbfvParams(prm, 256, d, 0)
+    rng = np.random.default_rng(9)
+    q = prm.ct_basis.moduli
+    a = uniform_residues(rng, (2, d, 2), q, n)
+    b = uniform_residues(rng, (2, d, 2), q, n)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
+    got = cref.dbfv_mul(dp, a, b, rlk, threads=2)
+    rk = np_to_rlk(rlk, prm)
+    for it in range(2):
+        ca = odbfv.DbfvCiphertext([np_to_ct(a[it, i], prm) for i in range(d)], d, 0, dp)
+        cb = odbfv.DbfvCiphertext([np_to_ct(b[it, i], prm) for i in range(d)], d, 0, dp)
+        want = np.stack([ct_to_np(l) for l in odbfv.dbfv_mul(ca, cb, rk).limbs])
+        assert np.array_equal(got[it], want)
+
+
+def test_c_polymul_matches_naive():
+    """oracle_polymul (the cfg2 CPU baseline: NTT, pointwise, INTT, ntt.rs:181-195) == mul_naive."""
+    if not cref.available():
+        pytest.skip("oracle/c not built")
+    n, q = 64, 1152921504606830593
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, q, size=(3, n), dtype=np.uint64)
+    b = rng.integers(0, q, size=(3, n), dtype=np.uint64)
+    got = cref.polymul(n, q, a, b, threads=2)
+    for k in range(3):
+        want = CoeffPoly.from_coeffs([int(x) for x in a[k]], q).mul_naive(CoeffPoly.from_coeffs([int(x) for x in b[k]], q))
+        assert [int(x) for x in got[k]] == want.coeffs

@@ -3,8 +3,9 @@ environment (run as a child process by tests/test_gpu_variants.py: each switch i
 process).  Prints one JSON object {case: sha256}.
 
 Cases: cfg3 bfv_mul_and_relin (n = 4096, 3 limbs: forward, inverse, tensor, key switch), cfg5
-dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels), and the fused
-NTT product at n = 4096 / 8192, out of place and in place on b.
+dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels), the HPS path
+(compact_bfv products, u64_dbfv dbfv_mul), and the fused NTT product at n = 4096 / 8192, out of
+place and in place on b.
 """
 
 import hashlib
@@ -51,6 +52,28 @@ def main():
     ctx5.load_relin_key(rlk5)
     out["cfg5_dbfv_mul"] = sha(ctx5.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
     out["cfg5_chain2"] = sha(ctx5.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2))
+
+    # HPS: compact_bfv (one aux prime) and u64_dbfv (two aux primes, dbfv_mul with summed digits)
+    cb = P.compact_bfv()
+    rng = np.random.default_rng(7004)
+    qc = cb.ct_basis.moduli
+    h1 = uniform_residues(rng, (8, 2), qc, 1024)
+    h2 = uniform_residues(rng, (8, 2), qc, 1024)
+    hk = uniform_residues(rng, (cb.gadget_digits, 2), qc, 1024)
+    hc = HipContext.from_params(cb)
+    hc.load_relin_key(hk)
+    out["compact_mul_relin"] = sha(hc.bfv_mul_and_relin(h1, h2))
+    out["compact_mul_no_relin"] = sha(hc.bfv_mul_no_relin(h1, h2))
+    du = P.u64_dbfv()
+    pu = du.bfv_params
+    rng = np.random.default_rng(7005)
+    qu = pu.ct_basis.moduli
+    ua = uniform_residues(rng, (2, du.num_digits, 2), qu, 4096)
+    ub = uniform_residues(rng, (2, du.num_digits, 2), qu, 4096)
+    uk = uniform_residues(rng, (pu.gadget_digits, 2), qu, 4096)
+    uc = HipContext.from_params(pu)
+    uc.load_relin_key(uk)
+    out["u64dbfv_dbfv_mul"] = sha(uc.dbfv_mul(du.num_digits, du.base, du.plain_modulus, ua, ub)[0])
 
     for nn, qs in ((4096, [1152921504606830593]), (8192, [1152921504606830593, 1152921504606748673])):
         rng = np.random.default_rng(7003 + nn)
