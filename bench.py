@@ -19,11 +19,13 @@ touching any GPU, and exits with its status; under torchrun WORLD_SIZE must equa
   --split batch (default): every rank processes its own batch shard, no data-path collective; the
       relinearisation key is made on rank 0 and broadcast by the library's RCCL (ncclBroadcast into
       each rank's resident key).  value = total units over all ranks / max-over-ranks time (weak).
-  --split limbs (dBFV configs): ONE dbfv_mul batch (the same B items on every rank) with its d output
-      limbs split across the ranks by product count (dbfv/eval.rs:109-132: limb k sums the pairs
-      i + j = k, so whole limbs need no cross-GPU sum); each rank computes its limbs, then an
-      all-gather assembles every limb on every rank (the next chain step needs them all).  value =
-      B units / max-over-ranks time (strong scaling: the total work is fixed).
+  --split limbs (dBFV configs): ONE dbfv_mul batch of B items split over the ranks in two dimensions
+      (exacto_amd.dist.split_plan): P_b item blocks x P_l output-limb groups, P_b P_l = N, the
+      factorisation with no idle rank and the smallest per-rank product count (limb k sums the pairs
+      i + j = k, dbfv/eval.rs:109-132, so whole limbs need no cross-GPU sum).  Each rank computes its
+      block, then the library's exacto_rccl_allgather_u64 assembles every item and limb on every
+      rank (with P_l = 1 a chain runs locally and gathers once; with P_l > 1 after every step).
+      value = B units / max-over-ranks time (strong scaling: the total work is fixed).
   --dry: no HIP calls at all (gloo on CPU, a stand-in step on CPU tensors of the same shapes): checks
       the launcher, the sharding / limb partition + gather and the timing path on a machine without
       a GPU.  Its numbers measure nothing.
@@ -501,30 +503,46 @@ def main():
         y = [uniform((B, d, 2)) for _ in range(nbuf)]
         outs = [torch.empty_like(x[0]) for _ in range(nbuf)]
         if args.split == "limbs":
-            parts = (xdist.limb_partition(d, world, xdist.limb_products(d, base, dplain)) if distributed
-                     else [list(range(d))])
-            mine = parts[rank]
-            compact = torch.zeros((B, max(len(mine), 1), 2, L, n), dtype=torch.int64, device=device)
+            # ONE dbfv_mul batch over all ranks, 2-D: item blocks x output-limb groups (split_plan)
+            wts = xdist.limb_products(d, base, dplain)
+            plan, pb, pl = xdist.split_plan(B, d, world, wts) if distributed else ([(0, B, list(range(d)))], 1, 1)
+            parts = {"item_blocks": pb, "limb_groups": pl, "ranks": [[c, ls] for _, c, ls in plan]}
+            s0, cnt, mine = plan[rank]
+            full = mine == list(range(d))
+            compact = torch.zeros((max(cnt, 1), max(len(mine), 1), 2, L, n), dtype=torch.int64, device=device)
             acc = [torch.empty_like(x[0]), torch.empty_like(x[0])]
+            if distributed and not args.dry:
+                allgather = lambda snd, rcv: ctx.allgather_u64(comm, snd, rcv, snd.numel())
+            else:
+                allgather = xdist.torch_allgather
 
-            def limbs_mul(src, yy, dst):
-                # this rank's output limbs, then every limb on every rank
-                if mine:
-                    if args.dry:   # stand-in: limb k <- src[:, k] + yy[:, k] (checks the gather below)
-                        torch.add(src[:, mine], yy[:, mine], out=compact[:, : len(mine)])
+            def part_mul(src, yy, dst, steps):
+                # this rank's items and limbs: `steps` chain steps when it holds whole items, else one
+                if cnt and mine:
+                    xs, ys = src[s0:s0 + cnt], yy[s0:s0 + cnt]
+                    if args.dry:   # stand-in: limb k <- src[:, k] + steps * yy[:, k] (checks the gather)
+                        torch.add(xs[:, mine], ys[:, mine], alpha=steps, out=compact[:cnt, : len(mine)])
+                    elif full and steps > 1:
+                        ctx.dbfv_mul_chain_dev(d, base, dplain, xs, ys, compact, cnt, steps)
+                    elif full:
+                        ctx.dbfv_mul_dev(d, base, dplain, xs, ys, compact, cnt)
                     else:
-                        ctx.dbfv_mul_limbs_dev(d, base, dplain, src, yy, compact, B, mine)
+                        ctx.dbfv_mul_limbs_dev(d, base, dplain, xs, ys, compact, cnt, mine)
                 if distributed:
-                    xdist.gather_limbs(compact[:, : len(mine)] if mine else compact[:, :0], parts, d, out=dst)
+                    xdist.gather_plan(compact[:cnt, : len(mine)], plan, rank, d, allgather, dst)
                 else:
                     dst.copy_(compact)
 
             def one(i):
-                # depth-`depth` chain (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220)
+                # depth-`depth` chain (paper_repro semantics, src/bin/paper_repro.rs:155-158, 217-220);
+                # whole items per rank (P_l = 1): the chain runs locally, one gather at the end
+                if pl == 1:
+                    part_mul(x[i], y[i], outs[i], depth)
+                    return
                 src = x[i]
-                for s in range(depth):
-                    dst = outs[i] if s == depth - 1 else acc[s % 2]
-                    limbs_mul(src, y[i], dst)
+                for st in range(depth):
+                    dst = outs[i] if st == depth - 1 else acc[st % 2]
+                    part_mul(src, y[i], dst, 1)
                     src = dst
         else:
             def one(i):
@@ -635,10 +653,13 @@ def main():
                        "limb_bits": max(q.bit_length() for q in moduli),
                        "aux_moduli": aux or None,
                        "plain_modulus": plain, "gadget_base": gbase, "gadget_digits": G,
-                       "batch_per_gpu": B, "global_batch": B * (world if args.split == "batch" else 1),
+                       "batch_per_gpu": B if args.split == "batch" else None,
+                       "global_batch": B * (world if args.split == "batch" else 1),
                        "batches_per_step": reps, "units_per_step": units_per_step,
                        "parallelism": (f"batch-shard x{world}" if args.split == "batch"
-                                       else f"dbfv output-limb split x{world}: {parts}")},
+                                       else f"one dbfv_mul batch split x{world}: {parts['item_blocks']} item "
+                                            f"blocks x {parts['limb_groups']} output-limb groups"),
+                       "split_plan": parts if args.split == "limbs" else None},
             "world_size": world,
             "backend": backend,
             "key_broadcast": key_collective,

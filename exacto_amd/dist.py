@@ -146,3 +146,68 @@ def gather_limbs(compact: torch.Tensor, parts: list[list[int]], d: int, out: tor
         if ls:
             out[:, ls] = got[r][:, : len(ls)]
     return out
+
+
+def split_plan(B: int, d: int, world: int, weights=None):
+    """2-D partition of ONE dbfv_mul batch (B items, d output limbs) over ``world`` ranks: P_b item
+    blocks x P_l limb groups, P_b P_l = world.  Rank r = ib * P_l + il computes the items
+    ``shard(B, ib, P_b)`` and the output limbs ``limb_partition(d, P_l, weights)[il]`` (whole limbs:
+    no cross-GPU sum, dbfv/eval.rs:109-132).  The factorisation taken is the one with no idle rank and
+    the smallest largest per-rank product count; ties go to fewer limb groups (a chain then needs no
+    exchange between its steps: every rank keeps whole items).  Only when every factorisation leaves
+    a rank idle (B P_l < world for all P_l <= d, e.g. a single dbfv_mul on more ranks than limbs) is
+    the least-idle one taken.  Deterministic: every rank computes the same plan without communicating.
+
+    Returns (plan, P_b, P_l) with plan[r] = (item_start, item_count, limbs)."""
+    w = limb_products(d) if weights is None else list(weights)
+    best = None
+    for pl in range(1, world + 1):
+        if world % pl:
+            continue
+        pb = world // pl
+        parts = limb_partition(d, pl, w)
+        plan = []
+        for r in range(world):
+            ib, il = divmod(r, pl)
+            s0, cnt = shard(B, ib, pb)
+            plan.append((s0, cnt, parts[il]))
+        loads = [cnt * sum(w[k] for k in ls) for _, cnt, ls in plan]
+        idle = sum(1 for (_, cnt, ls) in plan if cnt == 0 or not ls)
+        key = (idle, max(loads), pl)
+        if best is None or key < best[0]:
+            best = (key, plan, pb, pl)
+    return best[1], best[2], best[3]
+
+
+def gather_plan(compact: torch.Tensor, plan, rank: int, d: int, allgather, out: torch.Tensor):
+    """Assemble every rank's part of a split dbfv_mul on every rank.
+
+    compact: this rank's ``[item_count][len(limbs)][...]`` block (slot s = limb limbs[s]).  ``allgather(send,
+    recv)`` fills recv ``[world][...send.shape]`` with every rank's send block (the library's
+    ``exacto_rccl_allgather_u64`` on the GPU, torch.distributed on CPU): limbs are concatenated and
+    placed, never summed (an RCCL sum of residues would overflow mod q).  Blocks are padded to the
+    largest (items, limbs) block of the plan.  Writes ``out`` = ``[B][d][...]``."""
+    mi = max(c for _, c, _ in plan)
+    ml = max(len(ls) for _, _, ls in plan)
+    tail = tuple(compact.shape[2:])
+    _, cnt, ls = plan[rank]
+    if tuple(compact.shape[:2]) == (mi, ml) and compact.is_contiguous():
+        pad = compact
+    else:
+        pad = torch.zeros((mi, ml) + tail, dtype=compact.dtype, device=compact.device)
+        pad[:cnt, : len(ls)] = compact[:cnt, : len(ls)]
+    recv = torch.empty((len(plan), mi, ml) + tail, dtype=compact.dtype, device=compact.device)
+    allgather(pad, recv)
+    for r, (s0, c, lr) in enumerate(plan):
+        if c and lr:
+            if len(lr) == d and lr == list(range(d)):
+                out[s0:s0 + c] = recv[r, :c, :d]
+            else:
+                out[s0:s0 + c, lr] = recv[r, :c, : len(lr)]
+    return out
+
+
+def torch_allgather(send: torch.Tensor, recv: torch.Tensor):
+    """allgather for gather_plan over the default torch.distributed group (gloo or nccl)."""
+    dist.all_gather(list(recv.unbind(0)), send)
+

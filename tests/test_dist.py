@@ -142,11 +142,94 @@ def test_bench_dry_gpus2_relaunches_torchrun():
 
 
 def test_bench_dry_gpus2_limb_split_gathers_every_limb():
-    rc, line, r = _bench("--gpus", "2", "--dry", "--config", "cfg5", "--split", "limbs", "--batch", "2",
+    rc, line, r = _bench("--gpus", "2", "--dry", "--config", "cfg5", "--split", "limbs", "--batch", "1",
                          "--steps", "2", "--warmup", "1", "--min-time", "0.1")
     assert rc == 0, r.stderr[-2000:]
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["dry_gather_ok"] is True
-    assert "[[0, 3, 4, 7], [1, 2, 5, 6]]" in line["config"]["parallelism"]
+    # one item: its limbs split 18 + 18 products over the two ranks, gathered after every chain step
+    plan = line["config"]["split_plan"]
+    assert plan["item_blocks"] == 1 and plan["limb_groups"] == 2
+    assert plan["ranks"] == [[1, [0, 3, 4, 7]], [1, [1, 2, 5, 6]]]
+
+
+def test_bench_dry_gpus8_cfg4_split_keeps_every_rank_busy():
+    """Verdict r3 item 5: ONE cfg4 dbfv_mul batch (d = 2) over 8 ranks leaves no rank idle (items x
+    limb groups), and every item's every limb is assembled on every rank (gloo, 8 CPU processes)."""
+    rc, line, r = _bench("--gpus", "8", "--dry", "--config", "cfg4", "--split", "limbs", "--batch", "16",
+                         "--steps", "2", "--warmup", "1", "--min-time", "0.1")
+    assert rc == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 8 and line["dry_gather_ok"] is True
+    ranks = line["config"]["split_plan"]["ranks"]
+    assert len(ranks) == 8 and all(cnt > 0 and limbs for cnt, limbs in ranks)
+    assert sum(cnt for cnt, _ in ranks) * 1 == 16 * line["config"]["split_plan"]["limb_groups"]
+
+
+def test_split_plan_shapes():
+    from exacto_amd.dist import split_plan
+    # cfg4 batch over 8 ranks: whole items (no exchange between chain steps), 2 items each
+    plan, pb, pl = split_plan(16, 2, 8)
+    assert (pb, pl) == (8, 1) and all(c == 2 and ls == [0, 1] for _, c, ls in plan)
+    # one cfg5 dbfv_mul on 8 ranks: one limb each, products 1..8 (the limb dimension is all there is)
+    plan, pb, pl = split_plan(1, 8, 8)
+    assert (pb, pl) == (1, 8) and sorted(k for _, _, ls in plan for k in ls) == list(range(8))
+    # two cfg5 items on 4 ranks: 2 item blocks x 2 limb groups (18 products per rank), none idle
+    plan, pb, pl = split_plan(2, 8, 4)
+    assert (pb, pl) == (2, 2)
+    assert all(c == 1 and sum(k + 1 for k in ls) == 18 for _, c, ls in plan)
+    # a single cfg4 dbfv_mul cannot fill 8 ranks (3 products): least idle
+    plan, pb, pl = split_plan(1, 2, 8)
+    assert sum(1 for _, c, ls in plan if c and ls) == 2
+    # every (item, limb) covered exactly once
+    for B, d, world in ((5, 3, 6), (7, 8, 8), (3, 2, 4), (64, 8, 8)):
+        plan, _, _ = split_plan(B, d, world)
+        cover = sorted((b, k) for s0, c, ls in plan for b in range(s0, s0 + c) for k in ls)
+        assert cover == [(b, k) for b in range(B) for k in range(d)]
+
+
+def test_limb_products_follow_the_reps():
+    """limb weights from the pair / coefficient rule of dbfv_plan: with nonzero small
+    representatives the high pairs fold into low limbs (oracle/dbfv.py small_reps, reduce)."""
+    from oracle import dbfv as odbfv
+    for base, d, p in ((256, 2, 65536), (256, 8, 0), (7, 4, 1000), (3, 3, 20)):
+        reps = odbfv.small_reps(base, d, p)
+        want = [sum(1 for i in range(d) for j in range(d)
+                    if i + j == k or (i + j >= d and reps[i + j - d][k] != 0)) for k in range(d)]
+        assert limb_products(d, base, p) == want
+    assert limb_products(8, 256, 0) == limb_products(8)   # zero reps: k + 1 pairs
+    assert limb_products(4, 7, 1000) != limb_products(4)
+
+
+def _plan_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from exacto_amd.dist import split_plan, gather_plan, torch_allgather
+        B, d = 3, 5
+        plan, _, _ = split_plan(B, d, world)
+        full = torch.arange(B * d * 4, dtype=torch.int64).reshape(B, d, 4)
+        s0, c, ls = plan[rank]
+        compact = full[s0:s0 + c][:, ls].clone()
+        out = torch.full_like(full, -1)
+        gather_plan(compact, plan, rank, d, torch_allgather, out)
+        q.put((rank, bool(torch.equal(out, full))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_gather_plan(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res)
 
 
 def test_bench_world_size_mismatch_exits_nonzero():
