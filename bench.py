@@ -89,7 +89,7 @@ PUBLISHED = {
 # profiled kernel families (exacto_hip.h exacto_prof_read kinds, context.hip ProfKind)
 KINDS = {0: "fwd_ntt", 1: "inv_ntt", 2: "tensor_inv", 3: "polymul", 4: "exact_lift", 5: "exact_scale",
          6: "ks32_digit_ntt", 7: "ks32_mac", 8: "ks32_crt", 9: "dbfv_pairsum", 10: "psum_scale",
-         11: "tensor_c2_inv", 12: "ks32_digit_sum", 13: "dbfv_combine", 14: "hps_extend", 15: "relin_mac",
+         12: "ks32_digit_sum", 13: "dbfv_combine", 14: "hps_extend", 15: "relin_mac",
          16: "hps_scale"}
 
 
@@ -146,25 +146,19 @@ def kernel_names(n, L, S, cfg, env=os.environ):
         fwd = f"ntt_fwd_pin_kernel<{logn}> + {gfwd}" if near_q else gfwd
         inv = f"ntt_inv_pin_kernel<{logn}> + {ginv}" if near_q else ginv
         tensor = f"ntt_inv_tensor_kernel<{logn}, {'true' if max(primes) < (1 << 60) else 'false'}, false>"
-        return {0: fwd, 1: inv, 2: tensor, 5: "hps_scale_kernel", 13: "dbfv_combine_kernel", 14: "hps_extend_kernel",
-                15: "relin_mac_lds_kernel", 16: "hps_scale_kernel"}
+        return {0: fwd, 1: inv, 2: tensor, 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel",
+                14: "hps_extend_kernel", 15: "relin_mac_lds_kernel", 16: "hps_scale_kernel<true, *>"}
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    fwd = ("ntt_fwd_pipe_kernel" if asm and logn == 12 and env.get("EXACTO_NTT_PIPE", "0") != "0"
-           else f"ntt_fwd_pin_kernel<{logn}>" if asm and on("EXACTO_FWD_PIN")
-           else f"ntt_fwd_asm_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>")
-    # the asm inverse is the pinned-home kernel (ntt.hip EXACTO_NTT_PIN, a build-time switch)
+    fwd = f"ntt_fwd_pin_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>"
     inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}, true>"
     tp = env.get("EXACTO_TENSOR_PIN", "")
     pin = asm and on("EXACTO_NTT_ASM_INV") and (tp != "0" if tp else logn == 13)
-    t3 = env.get("EXACTO_TENSOR3", "1" if logn == 13 else "0") == "1"
-    tensor = (f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor3_kernel<{logn}>" if t3
-              else f"ntt_inv_tensor_kernel<{logn}, true, true>")
-    polymul = (f"ntt_polymul_pin_kernel<{logn}>" if env.get("EXACTO_POLYMUL_PIN", "0") == "1"
-               else f"ntt_polymul_kernel<{logn}>")
+    tensor = f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor_kernel<{logn}, true, true>"
+    polymul = f"ntt_polymul_kernel<{logn}>"
     return {0: fwd, 1: inv, 2: tensor, 3: polymul, 4: f"exact_lift_sp_kernel<{L}>",
             5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
             8: f"ks32_crt_kernel<{logn}, {S}>", 9: "dbfv_pairsum_kernel", 10: f"exact_psum_sp_kernel<{L}>",
-            11: f"ntt_inv_tensor_c2_kernel<{logn}>", 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel"}
+            12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel"}
 
 
 def _entry(rec, name, share=None):

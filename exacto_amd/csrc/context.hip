@@ -208,15 +208,10 @@ struct exacto_ctx {
     CrtTables h_crt{};
     u64* d_scal = nullptr;
     u64* d_rlk = nullptr;
-    u64* d_rlk_s = nullptr;  // Shoup companions of the key (fused key switching)
+    u64* d_rlk_s = nullptr;  // Shoup companions of the key (limb-wise relinearisation MAC)
     size_t rlk_keys = 0, rlk_cap = 0, rlk_s_cap = 0;
     bool rlk_s_valid = false;
-    bool fused_ks = false;  // EXACTO_FUSED_KS=1: spills at 16 values per thread, slower today
     bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
-    // EXACTO_NTT_PIPE=1: the persistent LDS-DMA forward kernel at n = 4096 instead of the pinned-home
-    // one-workgroup-per-polynomial kernel (same box: 117-118 vs 108-109 us per cfg3 launch, the step
-    // within 0.3 %)
-    bool ntt_pipe = false;
     bool ntt_asm_inv = true;  // EXACTO_NTT_ASM_INV=0: compiler-scheduled inverse NTT (A/B)
     // relinearisation MAC in an auxiliary basis of S 31-bit primes (ks32.hip; EXACTO_KS32=0: the
     // limb-wise 60-bit digit NTTs + relin_mac)
@@ -228,12 +223,6 @@ struct exacto_ctx {
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
-    // EXACTO_CRT_FWD=2/3/4: the key switch's lift and the forward NTT of bfv_mul_and_relin's outputs in
-    // one kernel (ks32_crt_fwd_kernel, 2 / 3 waves per SIMD; 4: ks32_crt_fwd_pin_kernel, pinned rounds,
-    // 13-22 VGPRs spilled in the lift: cfg3 413k vs 429k/s same box, round 3).  Off by default: cfg3 398.3k -> 391.3k/s
-    // (3 waves, a few spills) and 386.5k/s (2 waves): the lift's 126-VGPR phase and the transform do
-    // not share a register budget well, and the separate forward is the persistent LDS-DMA kernel
-    int crt_fwd = 0;
     // dBFV psum (EXACTO_PSUM=0: off): an output limb's c0 / c1 scaled once from the sum of its
     // products' tensors in the auxiliary primes (run_mul, dbfv_mul_core); psum_max = the largest
     // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
@@ -857,9 +846,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     }
     if (const char* e = getenv("EXACTO_DEBUG_SCRATCH")) c->debug_scratch = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DBFV_GROUP_MB")) c->dbfv_group_bytes = (size_t)std::max(1, atoi(e)) << 20;
-    if (const char* e = getenv("EXACTO_FUSED_KS")) c->fused_ks = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
-    if (const char* e = getenv("EXACTO_NTT_PIPE")) c->ntt_pipe = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM_INV")) c->ntt_asm_inv = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_LANES")) c->lanes = std::max(1, std::min(EXACTO_MAX_LANES, atoi(e)));
@@ -868,7 +855,6 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
-    if (const char* e = getenv("EXACTO_CRT_FWD")) c->crt_fwd = atoi(e);
     if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
     c->hps_fast = c->path == EXACTO_PATH_HPS && c->ctq[0] > (1ull << 32) && c->plain < c->ctq[0] &&
                   c->plain < (1ull << 32);
@@ -1014,8 +1000,7 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
         lazy &= c->primes[t] < (1ull << 60);
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
     }
-    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, c->ntt_pipe,
-               near60 && c->ntt_asm_inv);
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, near60 && c->ntt_asm_inv);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1031,23 +1016,9 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
     // algorithmic bytes per (item, prime): the four operands a0, a1, b0, b1 in and the three
     // components out (7 polys); psum's auxiliary primes only c2 = a1 b1 (2 in, 1 out)
     const double pb = 8.0 * c->n;
-    if (p2only && inverse_tensor_split(c->logn)) {
-        {   // ciphertext primes: all three components
-            ProfScope ps(c, PK_TENSOR, (u64)cnt * 3 * c->L, pb * 7.0 * cnt * c->L);
-            launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60,
-                              p2only, 0);
-            CHECK_LAUNCH();
-        }
-        ProfScope ps(c, PK_TENSOR_C2, (u64)cnt * c->K, pb * 3.0 * cnt * c->K);
-        launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60,
-                          p2only, 1);
-        CHECK_LAUNCH();
-        return 0;
-    }
     const double per_item = p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP;
     ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), per_item * cnt);
-    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
-                      -1);
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1215,12 +1186,6 @@ static int ensure_rs_wide(exacto_ctx* c) {
     return 0;
 }
 
-static bool lazy_ok(const exacto_ctx* c, int base, int period) {
-    bool lazy = true;
-    for (int t = base; t < base + period; ++t) lazy &= c->primes[t] < (1ull << 60);
-    return lazy;
-}
-
 // ============================================================== multiplication pipeline
 
 // products [0, P): ct1 = op.a + off_a(p), ct2 = op.b + off_b(p) (each [2][L][n], NTT domain).
@@ -1251,7 +1216,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
     }
     if (int e = ensure_workspace(c, C)) return e;
     // int16 gadget digits (base <= 2^16, exact path): the scale kernel writes each digit once
-    const bool d16 = relin && guse > 0 && c->digit16 && !c->fused_ks && c->path != EXACTO_PATH_HPS &&
+    const bool d16 = relin && guse > 0 && c->digit16 && c->path != EXACTO_PATH_HPS &&
                      c->gbase <= 65536;
     // ... and then the key switch runs over the integers in the 31-bit basis (ks32.hip)
     const bool k32 = d16 && c->ks32 && c->S32 > 0;
@@ -1367,17 +1332,6 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
         rb.src = R; rb.src_off = nullptr; rb.src_item_stride = out_stride;
         rb.dst = R; rb.dst_item_stride = out_stride;
         rb.ppi = ncomp * L; rb.prime_base = 0; rb.period = L;
-        if (relin && guse > 0 && c->fused_ks) {
-            // 7+8 fused: NTT(r0, r1) + sum_g NTT(d_g) (.) rlk_g, one launch, digits never stored in NTT form
-            if (int e = ensure_rlk_companions(c)) return e;
-            KsArgs ka{};
-            ka.R = R; ka.r_off = nullptr; ka.r_stride = out_stride; ka.r_ntt = 0; ka.L = L;
-            ka.D = c->ws_D; ka.guse = guse; ka.rlk = c->d_rlk; ka.rlk_s = c->d_rlk_s;
-            ka.out = R; ka.out_stride = out_stride;
-            launch_keyswitch(ka, cnt, c->logn, lazy_ok(c, 0, L), c->d_primes, c->stream);
-            CHECK_LAUNCH();
-            continue;
-        }
         if (k32) {
             // 7'+8'. the key switch over the integers (ks32.hip): digits -> NTT mod p_s, MAC with the
             // key in the same basis, inverse NTT + centred lift, added to R mod q_l in the
@@ -1391,21 +1345,12 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                     ProfScope pm(c, PK_KS_MAC, (u64)cnt * c->S32, 4.0 * n * cnt * c->S32 * (guse + 2.0 * L));
                     ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
                 }
-                // lift + the forward NTT of R in one kernel when the asm forward rounds serve R's primes
-                bool fused = false;
-                if (!skip_fwd && c->crt_fwd > 0 && c->ntt_asm && ncomp == 2) {
-                    bool near = true;
-                    for (int l = 0; l < L; ++l) near &= c->primes[l] < (1ull << 60) && c->primes[l] > (1ull << 60) - (1ull << 24);
-                    fused = near && launch_ks32_crt_fwd(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32,
-                                                        c->d_primes, c->stream, c->crt_fwd);
-                }
-                if (!fused) {   // per (item, component, limb): S 31-bit sums in, R in and out
+                {   // per (item, component, limb): S 31-bit sums in, R in and out
                     ProfScope pc(c, PK_KS_CRT, (u64)cnt * 2 * L, (double)n * cnt * 2 * L * (4.0 * c->S32 + 16.0));
                     ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
                              c->stream);
                 }
                 CHECK_LAUNCH();
-                if (fused) continue;   // R is relinearised and in the NTT domain
             }
         }
         if (skip_fwd) continue;   // (hps_defer: digits and c0 / c1 are the caller's now)
@@ -1907,7 +1852,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     // The primary 31-bit basis when it holds the sums, else the wide one (primes up to 2^31).
     const size_t gu = std::min<size_t>(c->G, c->rlk_keys);
     const int m = c->cached_sum_m;
-    const bool on = c->S32 > 0 && c->ks32 && m > 0 && c->digit16 && c->gbase <= 65536 && !c->fused_ks &&
+    const bool on = c->S32 > 0 && c->ks32 && m > 0 && c->digit16 && c->gbase <= 65536 &&
                     c->rlk_loaded && gu > 0;
     const bool use_prim = on && m <= c->ks32_sum_max;
     const bool use_wide = on && !use_prim && c->kw.S > 0 && m <= c->kw.sum_max;
@@ -1926,7 +1871,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     // 8 instead of 36 products' worth of 10 forward NTTs and one MAC per dbfv_mul).
     const bool hps_sum = c->path == EXACTO_PATH_HPS && c->hps_sum_env && m > 0 && c->gbase <= 65536 &&
                          (u64)m * (c->gbase / 2) <= 32767 && c->rlk_loaded && gu > 0 && c->n >= 1024 &&
-                         !c->deferred_code && !c->fused_ks;
+                         !c->deferred_code;
     if (hps_sum) {
         if (grow((u64**)&c->d_dall, &c->dall_cap, std::max<size_t>((size_t)P * gu * c->n * sizeof(int16_t), 8)) ||
             grow((u64**)&c->d_dk, &c->dk_cap, std::max<size_t>(Bd * gu * c->n * 2, 8)) ||

@@ -66,29 +66,11 @@ struct CrtTables {
 };
 
 // lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)
-// asm_fwd: every prime of the batch is in (2^60 - 2^32, 2^60) and the hand-scheduled forward
-// kernel (ntt_asm.inc) may be used for n = 4096 / 8192
-// pipe: n = 4096 forward transforms run on the persistent LDS-DMA kernel (ntt_fwd_pipe_kernel)
-// asm_inv: same prime window as asm_fwd, inverse transforms at n = 4096 / 8192 run the generated
-// Gentleman-Sande rounds (ntt_inv_asm_kernel)
+// asm_fwd / asm_inv: every prime of the batch is in (2^60 - 2^32, 2^60): the forward / inverse
+// transforms at n = 4096 / 8192 run the pinned-home kernels over the generated rounds (ntt_asm.inc)
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd = false, bool pipe = false, bool asm_inv = false);
+                hipStream_t s, bool asm_fwd = false, bool asm_inv = false);
 
-// Fused relinearisation: see keyswitch_kernel in ntt.hip.
-struct KsArgs {
-    const u64* R;        // c0', c1' sources: [2][L][n] per item (coefficient or NTT domain)
-    const u64* r_off;    // per-item element offsets or nullptr -> item * r_stride
-    long r_stride;
-    int r_ntt;           // R already in the NTT domain
-    int L;
-    const u64* D;        // gadget digits, coefficient domain, [guse][L][n] per item (contiguous)
-    int guse;
-    const u64* rlk;      // [keys][2][L][n]
-    const u64* rlk_s;    // Shoup companions of rlk
-    u64* out;            // [2][L][n] per item (may alias R)
-    long out_stride;
-};
-void launch_keyswitch(const KsArgs& a, int items, int logn, bool lazy, const PrimeConst* primes, hipStream_t s);
 void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
                              hipStream_t s);
 
@@ -125,11 +107,6 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
               const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);
-// ks32_crt followed by the forward NTT of R's rows (row (item, c, l) mod q_l), fused (ntt.hip; n =
-// 4096 / 8192, S = 2 / 3, every q_l 2^60 - d with d < 2^24; false = not launched)
-bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn,
-                         const Ks32Tables* KT, const Prime32* primes, const PrimeConst* qprimes, hipStream_t s,
-                         int waves);
 
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item
@@ -161,11 +138,7 @@ void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period,
 // p2only: every component of the ciphertext primes, the third only of the auxiliary primes (dBFV
 // psum; asm_inv and n = 4096 / 8192 only)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false,
-                       int part = -1);
-// psum (p2only) at this size runs as two launches (the ciphertext primes' three components, then the
-// auxiliary primes' third): launch_inv_tensor part 0 / part 1 time them apart
-bool inverse_tensor_split(int logn);
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);

@@ -188,9 +188,6 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTa
 #ifndef EXACTO_NTT_TOUT
 #define EXACTO_NTT_TOUT 1  // forward: transpose through LDS so the output stores coalesce
 #endif
-#ifndef EXACTO_NTT_TIN
-#define EXACTO_NTT_TIN 0   // inverse: coalesced loads, transposed through LDS (measured slower)
-#endif
 #ifdef EXACTO_NTT_WAVES
 #define NTT_OCC __attribute__((amdgpu_waves_per_eu(EXACTO_NTT_WAVES)))
 #else
@@ -317,270 +314,6 @@ __device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
     if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
 }
 
-#ifndef EXACTO_ASM_WAVES
-#define EXACTO_ASM_WAVES 3
-#endif
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(EXACTO_ASM_WAVES)))
-ntt_fwd_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
-    constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const int p = blockIdx.x;
-    const int item = p / nb.ppi, sub = p - item * nb.ppi;
-    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
-    const u64 q = P.q;
-    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
-                     (long)sub * N;
-    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
-
-    u64 x[16];
-    load_coeffs<N>(x, nb, src, item, sub, q, tid);
-
-    const AsmK K = make_asmk(q);
-    fwd_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_fwd), K);
-
-    // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
-    int t2 = tid;
-    asm volatile("" : "+v"(t2));
-    lds_barrier();
-    lds_store_x<0>(lds, x, t2);
-    lds_barrier();
-    lds_load_x<LOGN - 4>(lds, x, t2);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
-}
-
-// ---------------------------------------------------------------- forward, persistent + LDS-DMA prefetch
-
-// The kernel above loads a polynomial, transforms it and stores it; its co-resident workgroups
-// start together and stay in phase, so the chip alternates between a memory phase and a compute
-// phase ("what bounds the forward transform").  This form keeps a fixed set of
-// workgroups resident (2 per CU, 64 KiB of LDS each) and streams polynomials through them:
-// while polynomial p is transformed in registers, polynomial p + grid is already on its way
-// from HBM into the other half of the workgroup's LDS by global_load_lds (LDS-DMA, no VGPRs).
-//
-// Every vector-memory operation inside the loop is an inline-asm statement (the DMA and the
-// output stores), so hipcc's waitcnt pass sees no loads to wait for and the counted
-// `s_waitcnt vmcnt(16)` at the top of each iteration (this wave's 16 output stores of the
-// previous polynomial may stay in flight) is the only wait on the DMA.  Twiddles: round 0 is
-// block-uniform (scalar loads, lgkmcnt); rounds 1 and 2 are per-thread and stay in VGPRs for
-// as long as the workgroup's prime does not change -- with the grid a multiple of the batch's
-// prime period, never.
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t lds_u32(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// one wave-instruction of LDS-DMA: 64 lanes x 16 B from per-lane gsrc to lds_dst + 16 * lane
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_dst)
-                 : "memory");
-}
-
-// This wave's share of one polynomial's source bytes -> LDS image at lds_base (natural order).
-template <int BYTES, int WAVES>
-__device__ __forceinline__ void dma_share(const void* src, uint32_t lds_base, int wave, int lane) {
-    constexpr int PER = BYTES / WAVES;
-    static_assert(PER % 1024 == 0, "a wave moves whole 1 KiB pieces");
-    const char* s = (const char*)src + wave * PER + lane * 16;
-    const uint32_t d = __builtin_amdgcn_readfirstlane(lds_base + wave * PER);
-#pragma unroll
-    for (int i = 0; i < PER / 1024; ++i) dma16(s + i * 1024, d + i * 1024);
-}
-
-__device__ __forceinline__ u64 sload_u64(const u64* p) {
-    u64 r;
-    asm volatile("s_load_dwordx2 %0, %1, 0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
-    return r;
-}
-
-// Round-0 twiddles of an n = 4096 transform (indices 1..15, block-uniform) by scalar loads.
-__device__ __forceinline__ void sload_round0_tw(TwPair (&tw)[15], const TwPair* tab) {
-    u32x4 v[15];
-    asm volatile(
-        "s_load_dwordx4 %0, %15, 16\n\ts_load_dwordx4 %1, %15, 32\n\ts_load_dwordx4 %2, %15, 48\n\t"
-        "s_load_dwordx4 %3, %15, 64\n\ts_load_dwordx4 %4, %15, 80\n\ts_load_dwordx4 %5, %15, 96\n\t"
-        "s_load_dwordx4 %6, %15, 112\n\ts_load_dwordx4 %7, %15, 128\n\ts_load_dwordx4 %8, %15, 144\n\t"
-        "s_load_dwordx4 %9, %15, 160\n\ts_load_dwordx4 %10, %15, 176\n\ts_load_dwordx4 %11, %15, 192\n\t"
-        "s_load_dwordx4 %12, %15, 208\n\ts_load_dwordx4 %13, %15, 224\n\ts_load_dwordx4 %14, %15, 240\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=s"(v[0]), "=s"(v[1]), "=s"(v[2]), "=s"(v[3]), "=s"(v[4]), "=s"(v[5]), "=s"(v[6]), "=s"(v[7]),
-          "=s"(v[8]), "=s"(v[9]), "=s"(v[10]), "=s"(v[11]), "=s"(v[12]), "=s"(v[13]), "=s"(v[14])
-        : "s"(tab)
-        : "memory");
-#pragma unroll
-    for (int i = 0; i < 15; ++i) {
-        tw[i].w = (u64)v[i].x | ((u64)v[i].y << 32);
-        tw[i].ws = (u64)v[i].z | ((u64)v[i].w << 32);
-    }
-}
-
-// 16 coalesced 8-byte stores per thread: element tid + k*T of dst <- x[k] (byte offsets
-// off[j] = 8*tid + j*4096 with immediate 0 / 2048).  The trailing s_nop keeps hipcc from
-// reusing the data registers before the last store has read them.  The leading s_nop 4: the base
-// address is an SGPR pair, and when hipcc reloads a spilled SGPR right before the statement
-// (v_readlane_b32, a VALU write) a vector-memory read of it needs 5 wait states, which hipcc's
-// hazard recognizer does not insert for an instruction inside inline asm -- without it a build
-// whose spill placement differed (more SGPR spills) stored through a stale base and faulted
-// (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION, round 3).
-__device__ __forceinline__ void store_poly4096(u64* dst, const u64 (&x)[16], const uint32_t (&off)[8]) {
-    asm volatile(
-        "s_nop 4\n\t"
-        "global_store_dwordx2 %16, %0, %24\n\tglobal_store_dwordx2 %16, %1, %24 offset:2048\n\t"
-        "global_store_dwordx2 %17, %2, %24\n\tglobal_store_dwordx2 %17, %3, %24 offset:2048\n\t"
-        "global_store_dwordx2 %18, %4, %24\n\tglobal_store_dwordx2 %18, %5, %24 offset:2048\n\t"
-        "global_store_dwordx2 %19, %6, %24\n\tglobal_store_dwordx2 %19, %7, %24 offset:2048\n\t"
-        "global_store_dwordx2 %20, %8, %24\n\tglobal_store_dwordx2 %20, %9, %24 offset:2048\n\t"
-        "global_store_dwordx2 %21, %10, %24\n\tglobal_store_dwordx2 %21, %11, %24 offset:2048\n\t"
-        "global_store_dwordx2 %22, %12, %24\n\tglobal_store_dwordx2 %22, %13, %24 offset:2048\n\t"
-        "global_store_dwordx2 %23, %14, %24\n\tglobal_store_dwordx2 %23, %15, %24 offset:2048\n\t"
-        "s_nop 1"
-        :
-        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]), "v"(x[8]),
-          "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(x[12]), "v"(x[13]), "v"(x[14]), "v"(x[15]), "v"(off[0]),
-          "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]), "s"(dst)
-        : "memory");
-}
-
-struct PipeSrc {
-    const void* src;  // u64 polynomial or int16 digit row
-    int prime;        // index into primes[]
-    u64* dst;
-};
-
-// Source / destination / prime of polynomial p (all block-uniform; src_off by a scalar load).
-__device__ __forceinline__ PipeSrc pipe_locate(const NttBatch& nb, int p, int N) {
-    const int item = p / nb.ppi, sub = p - item * nb.ppi;
-    PipeSrc r;
-    r.prime = nb.prime_base + sub % nb.period;
-    if (nb.src16) {
-        r.src = nb.src16 + (long)item * nb.src16_item_stride + (long)(sub / nb.period) * N;
-    } else {
-        const long base = nb.src_off ? (long)sload_u64(nb.src_off + item) : (long)item * nb.src_item_stride;
-        r.src = nb.src + base + (long)sub * N;
-    }
-    r.dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
-    return r;
-}
-
-template <int LOGN>
-__device__ __forceinline__ void pipe_issue(const NttBatch& nb, const PipeSrc& s, uint32_t lds_base, int wave,
-                                           int lane) {
-    constexpr int N = 1 << LOGN, WAVES = N / 16 / 64;
-    if (nb.src16) dma_share<N * 2, WAVES>(s.src, lds_base, wave, lane);
-    else dma_share<N * 8, WAVES>(s.src, lds_base, wave, lane);
-}
-
-// EXACTO_PIPE_PROBE (measurement builds only, wrong results): 1 = no DMA and no stores (compute
-// and LDS exchanges alone), 2 = no butterfly rounds (memory and LDS exchanges alone)
-#ifndef EXACTO_PIPE_PROBE
-#define EXACTO_PIPE_PROBE 0
-#endif
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-ntt_fwd_pipe_kernel(NttBatch nb, const PrimeConst* __restrict__ primes, int count) {
-    constexpr int LOGN = 12, N = 1 << LOGN, T = N / 16;
-    __shared__ u64 lds[2 * N];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    int p = blockIdx.x;
-    if (p >= count) return;
-    const uint32_t lds0 = lds_u32(lds);
-
-    uint32_t off[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) off[j] = 8 * tid + 4096 * j;
-
-    PipeSrc cur = pipe_locate(nb, p, N);
-    if (EXACTO_PIPE_PROBE != 1) pipe_issue<LOGN>(nb, cur, lds0, wave, lane);
-
-    int have = -1;
-    AsmK K{};
-    TwPair tw1[15], tw2[15];
-    u64 q = 0;
-    const TwPair* tab = nullptr;
-    int buf = 0;
-    bool first = true;
-    for (;;) {
-        if (cur.prime != have) {
-            // (re)load the prime's constants and the per-thread twiddles of rounds 1 and 2; the
-            // empty asm consumes them so that hipcc waits for these loads here, before the next
-            // DMA is issued, not at their first use in the loop
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const PrimeConst& P = primes[cur.prime];
-            q = P.q;
-            tab = P.tw_fwd;
-            const TwTab tt = tw_table(tab);
-            load_round_tw<LOGN, 4, 7, 4>(tw1, tid, tt);
-            load_round_tw<LOGN, 0, 3, 0>(tw2, tid, tt);
-#pragma unroll
-            for (int i = 0; i < 15; ++i)
-                asm volatile("" ::"v"(tw1[i].w), "v"(tw1[i].ws), "v"(tw2[i].w), "v"(tw2[i].ws));
-            K = make_asmk(q);
-            have = cur.prime;
-        }
-        // this wave's DMA of polynomial p has landed (the 16 younger ops are the previous
-        // polynomial's stores); the barrier makes every wave's share visible
-        if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        first = false;
-        lds_barrier();
-        u64* L0 = lds + buf * N;
-        u64 x[16];
-        if (nb.src16) {
-            const int16_t* s16 = reinterpret_cast<const int16_t*>(L0);
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const i64 d = s16[tid + k * T];
-                x[k] = d < 0 ? q + (u64)d : (u64)d;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) x[k] = L0[tid + k * T];
-        }
-        TwPair tw0[15];
-        sload_round0_tw(tw0, tab);  // its lgkmcnt(0) also retires the reads above
-        // prefetch the next polynomial into the other half (free: its last reads were in the
-        // previous iteration, before the barrier above)
-        const int pn = p + (int)gridDim.x;
-        PipeSrc nxt{};
-        if (pn < count) {
-            nxt = pipe_locate(nb, pn, N);
-            if (EXACTO_PIPE_PROBE != 1) pipe_issue<LOGN>(nb, nxt, lds0 + (buf ^ 1) * N * 8, wave, lane);
-        }
-        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 0>::run(x, tw0, K);
-        int t2 = tid;
-        asm volatile("" : "+v"(t2));
-        lds_barrier();
-        lds_store_x<8>(L0, x, t2);
-        lds_barrier();
-        lds_load_x<4>(L0, x, t2);
-        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 1>::run(x, tw1, K);
-        lds_barrier();
-        lds_store_x<4>(L0, x, t2);
-        lds_barrier();
-        lds_load_x<0>(L0, x, t2);
-        if (EXACTO_PIPE_PROBE != 2) FwdRoundAsm<LOGN, 2>::run(x, tw2, K);
-        // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
-        lds_barrier();
-        lds_store_x<0>(L0, x, t2);
-        lds_barrier();
-        lds_load_x<LOGN - 4>(L0, x, t2);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (EXACTO_PIPE_PROBE != 1) store_poly4096(cur.dst, x, off);
-        if (pn >= count) break;
-        p = pn;
-        cur = nxt;
-        buf ^= 1;
-    }
-}
-
 // ---------------------------------------------------------------- inverse
 
 template <int LOGN, int LO, int BLO, int BHI>
@@ -698,14 +431,7 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
 
     u64 x[16];
-    if constexpr (EXACTO_NTT_TIN) {
-        // coalesced loads (element tid+k*T), then transpose to 16*tid+k through LDS
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
-        lds_store<LOGN - 4>(lds, x, tid);
-        lds_barrier();
-        lds_load<0>(lds, x, tid);
-    } else {
+    {   // element 16*tid + k (coalesced loads + an LDS transpose measured slower, round 1)
         const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -747,67 +473,18 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
     if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
 }
 
-// The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread).
-// EXACTO_ASM_TIN = 0: each thread loads its 16 consecutive words (8 x 16 B at a 128-B lane stride:
-// every wave-load touches 64 cache lines); 1: coalesced 8-B loads of element tid + k*T (every
-// wave-load 512 contiguous bytes), transposed through LDS (one store/load pass, one barrier).
-#ifndef EXACTO_ASM_TIN
-#define EXACTO_ASM_TIN 0
-#endif
+// The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread): each
+// thread loads its 16 consecutive words (8 x 16 B).  (Coalesced 8-B loads transposed through LDS
+// measured neutral for the asm inverse and the tensor kernel, round 3, and were removed.)
 template <int N>
 __device__ __forceinline__ void load_rows16(u64 (&x)[16], const u64* __restrict__ src, int tid) {
-    if constexpr (EXACTO_ASM_TIN) {
+    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * (N / 16)];
-    } else {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const ulonglong2 v = s2[k];
-            x[2 * k] = v.x;
-            x[2 * k + 1] = v.y;
-        }
+    for (int k = 0; k < 8; ++k) {
+        const ulonglong2 v = s2[k];
+        x[2 * k] = v.x;
+        x[2 * k + 1] = v.y;
     }
-}
-
-// x from load_rows16 -> element 16*tid + k in x[k] (the transpose when EXACTO_ASM_TIN; the LDS
-// image is free until the first round's exchange, which starts with a barrier)
-template <int LOGN>
-__device__ __forceinline__ void rows16_to_inv_layout(u64 (&x)[16], u64* lds, int tid) {
-    if constexpr (EXACTO_ASM_TIN) {
-        int t2 = tid;
-        asm volatile("" : "+v"(t2));
-        lds_store_x<LOGN - 4>(lds, x, t2);
-        lds_barrier();
-        lds_load_x<0>(lds, x, t2);
-    }
-}
-
-template <int LOGN>
-__device__ __forceinline__ void load_inv_input(u64 (&x)[16], const u64* __restrict__ src, u64* lds, int tid) {
-    load_rows16<1 << LOGN>(x, src, tid);
-    rows16_to_inv_layout<LOGN>(x, lds, tid);
-}
-
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(EXACTO_ASM_WAVES)))
-ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
-    constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const int p = blockIdx.x;
-    const int item = p / nb.ppi, sub = p - item * nb.ppi;
-    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
-    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
-                     (long)sub * N;
-    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
-    u64 x[16];
-    load_inv_input<LOGN>(x, src, lds, tid);
-    const AsmK K = make_asmk_inv(P);
-    inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), K);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
 // ---------------------------------------------------------------- pinned-home rounds
@@ -847,7 +524,7 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     }
 
 // The inverse rounds over the pinned homes (inputs < 4q; output element LAST_LO-layout, canonical):
-// ntt_inv_asm_kernel's twiddles and exchanges.  A macro because the homes are the enclosing
+// inv_rounds_asm's twiddles and exchanges.  A macro because the homes are the enclosing
 // kernel's register variables.
 #define PIN_INV_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
     {                                                                                            \
@@ -879,7 +556,7 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     }
 
 // The forward rounds over the pinned homes (canonical inputs, element tid + k T; canonical outputs,
-// element 16 tid + k): ntt_fwd_asm_kernel's twiddles and exchanges.
+// element 16 tid + k): fwd_rounds_asm's twiddles and exchanges.
 #define PIN_FWD_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
     {                                                                                            \
         const AsmK pin_K = (K_);                                                                 \
@@ -910,12 +587,8 @@ ntt_inv_asm_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         }                                                                                        \
     }
 
-#ifndef EXACTO_NTT_PIN
-#define EXACTO_NTT_PIN 1   // 0: launch_ntt's n = 4096 / 8192 asm inverse is ntt_inv_asm_kernel (A/B builds)
-#endif
-
-// Inverse NTT, n = 4096 / 8192, pinned homes: the rounds of ntt_inv_asm_kernel (same twiddles,
-// exchanges, bounds and output layout).
+// Inverse NTT, n = 4096 / 8192, pinned homes: the generated inverse rounds (inv_rounds_asm's twiddles,
+// exchanges, bounds and output layout) on values bound to fixed VGPR pairs for the whole kernel.
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
@@ -948,7 +621,7 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 #undef PIN_OUT
 }
 
-// Forward NTT, n = 4096 / 8192, pinned homes: ntt_fwd_asm_kernel's rounds, exchanges and
+// Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds, exchanges and
 // coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
@@ -1111,8 +784,6 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     auto mulr = [&](u64 a, u64 b) {
         return ASM ? mulmod_near60(a, b, dq) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
     };
-    // (ASM + EXACTO_ASM_TIN: coalesced operand loads; the pointwise products do not care about the
-    // layout, and the one component is transposed before the rounds)
     auto load = [&](const u64* src, u64 (&v)[16]) {
         if constexpr (ASM) {
             load_rows16<N>(v, src, tid);
@@ -1162,7 +833,6 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         }
     }
     if constexpr (ASM) {
-        rows16_to_inv_layout<LOGN>(x, lds, tid);
         const AsmK AK = make_asmk_inv(P);
         inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
@@ -1373,299 +1043,17 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = xa[k];
 }
 
-// Buffer-resource row access for the pinned kernels: one block-uniform descriptor (SGPRs) per
-// polynomial, one shared lane offset (VGPR) and a per-row SGPR/constant offset, so that the 16 rows
-// of a thread cost no per-lane 64-bit pointers (which do not fit beside the homes).
-typedef __amdgpu_buffer_rsrc_t BufRes;
-typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ BufRes poly_res(const u64* p, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<u64*>(p), (short)0, bytes, 0x00020000);
-}
-__device__ __forceinline__ u32x2v bld64(BufRes r, int voff, int soff) {
-    return __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
-}
-__device__ __forceinline__ void bst64(uint32_t lo, uint32_t hi, BufRes r, int voff, int soff) {
-    u32x2v v;
-    v.x = lo;
-    v.y = hi;
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, soff, 0);
-}
-
-// ntt_polymul_kernel over pinned homes, four waves per SIMD: a is transformed in the homes and its
-// evaluations parked in the block's own output rows (coalesced; this thread's words only, read back
-// by the same thread, so no barrier: the L2 usually still holds them), then b is transformed, a's
-// evaluations are read back, the product formed into the homes (MulNear60PinAsm, < 2q) and
-// inverse-transformed over the parked words.  One set of values in registers instead of two (the
-// register-resident form holds 32 more VGPRs and spills at three waves per SIMD).
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_polymul_pin_kernel(const u64* A, const u64* B, u64* out, int period, const PrimeConst* __restrict__ primes) {
-    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
-    constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const long p = blockIdx.x;
-    const PrimeConst& P = primes[(int)(blockIdx.x % (unsigned)period)];
-    const u64 q = P.q;
-    const BufRes ra = poly_res(A + p * N, N * 8), rb = poly_res(B + p * N, N * 8), ro = poly_res(out + p * N, N * 8);
-    const int vrow = 8 * tid;                                  // element tid + k T: soffset 8 k T
-    EXACTO_PIN_DECL
-#define PIN_INA(k) { const u32x2v v_ = bld64(ra, vrow, 8 * (k) * T); xl##k = v_.x; xh##k = v_.y; }
-    PIN_X16(PIN_INA)
-#undef PIN_INA
-    const AsmK K = make_asmk(q);
-    const TwTab tf = tw_table(P.tw_fwd);
-    PIN_FWD_ROUNDS(LOGN, lds, tid, tf, K)
-#define PIN_PARK(k) bst64(xl##k, xh##k, ro, vrow, 8 * (k) * T);
-    PIN_X16(PIN_PARK)
-#undef PIN_PARK
-#define PIN_INB(k) { const u32x2v v_ = bld64(rb, vrow, 8 * (k) * T); xl##k = v_.x; xh##k = v_.y; }
-    PIN_X16(PIN_INB)
-#undef PIN_INB
-    // a fresh copy of tid for b's rounds: otherwise hipcc keeps a's twiddle addresses live (spilled)
-    int tid2 = tid;
-    asm volatile("" : "+v"(tid2));
-    PIN_FWD_ROUNDS(LOGN, lds, tid2, tf, K)
-    const uint32_t dq = (uint32_t)((1ull << 60) - q), e16 = 16 * dq;
-    // products in two halves: 8 parked words loaded together, then four ordered (volatile) product
-    // pairs into the homes; the statements also fence the inverse's twiddle loads below them
-#define PIN_LDP(k) const u32x2v u##k##_ = bld64(ro, vrow, 8 * (k) * T);
-#define PIN_MUL(k0, k1)                                                                              \
-    {                                                                                                \
-        u64 r0_, r1_;                                                                                \
-        MulNear60PinVAsm<2>::run(r0_, r1_, ((u64)u##k0##_.y << 32) | u##k0##_.x, PIN_GET(k0),        \
-                                 ((u64)u##k1##_.y << 32) | u##k1##_.x, PIN_GET(k1), dq, e16);        \
-        PIN_SET(k0, r0_) PIN_SET(k1, r1_)                                                            \
-    }
-    {
-        PIN_LDP(0) PIN_LDP(1) PIN_LDP(2) PIN_LDP(3) PIN_LDP(4) PIN_LDP(5) PIN_LDP(6) PIN_LDP(7)
-        PIN_MUL(0, 1) PIN_MUL(2, 3) PIN_MUL(4, 5) PIN_MUL(6, 7)
-    }
-    {
-        PIN_LDP(8) PIN_LDP(9) PIN_LDP(10) PIN_LDP(11) PIN_LDP(12) PIN_LDP(13) PIN_LDP(14) PIN_LDP(15)
-        PIN_MUL(8, 9) PIN_MUL(10, 11) PIN_MUL(12, 13) PIN_MUL(14, 15)
-    }
-#undef PIN_MUL
-#undef PIN_LDP
-    int tid3 = tid;
-    asm volatile("" : "+v"(tid3));
-    // the twiddle table is read-only memory, whose loads move freely; an opaque copy of the pointer
-    // defined here keeps them below the products
-    const TwPair* ti = P.tw_inv;
-    asm volatile("" : "+s"(ti));
-    PIN_INV_ROUNDS(LOGN, lds, tid3, tw_table(ti), make_asmk_inv(P))
-    // element elem_index<LAST_LO>(tid, k) = base(tid) | k << LAST_LO
-    const int vout = 8 * elem_index<LAST_LO>(tid3, 0);
-#define PIN_OUT(k) bst64(xl##k, xh##k, ro, vout, 8 * ((k) << LAST_LO));
-    PIN_X16(PIN_OUT)
-#undef PIN_OUT
-}
-
-// The key switch's lift (ks32_crt_values: S inverse 32-bit transforms, centred Garner lift, + the
-// scaled component) and the forward 60-bit transform of the result in one workgroup per (item, c,
-// l): the coefficient-domain relinearised component never goes to HBM and back (bfv_mul_and_relin's
-// steps 8 and 9).  The lift leaves element k T + tid in x[k], the forward rounds' input layout.
-// W: waves per SIMD the register budget targets (3: 168 VGPRs, a few spilled; 2: no spills)
-template <int LOGN, int S, int W>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(W)))
-ks32_crt_fwd_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
-                    const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
-                    const PrimeConst* __restrict__ qprimes) {
-    constexpr int N = 1 << LOGN, T = N / 16;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;             // (item, cl)
-    u64 x[16];
-    ks32_crt_values<LOGN, S>(x, U, R, r_stride, L, b, reinterpret_cast<uint32_t*>(lds), tid, KT, primes, qprimes);
-    const uint32_t CL = 2 * L;
-    const long item = b / CL;
-    const int cl = (int)(b - (uint32_t)item * CL);
-    const PrimeConst& P = qprimes[cl % L];
-    lds_barrier();   // the lift's last LDS reads are done before the forward rounds reuse lds
-    fwd_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
-    int t2 = tid;
-    asm volatile("" : "+v"(t2));
-    lds_barrier();
-    lds_store_x<0>(lds, x, t2);
-    lds_barrier();
-    lds_load_x<LOGN - 4>(lds, x, t2);
-    u64* dst = R + item * r_stride + (long)cl * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
-}
-
-// ks32_crt_fwd_kernel with the forward rounds over pinned homes (waves = 4 at launch_ks32_crt_fwd):
-// the lift's values go into the homes, PIN_FWD_ROUNDS, one LDS transpose, coalesced stores.
-template <int LOGN, int S>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ks32_crt_fwd_pin_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
-                        const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
-                        const PrimeConst* __restrict__ qprimes) {
-    static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
-    constexpr int N = 1 << LOGN, T = N / 16;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const uint32_t b = blockIdx.x;             // (item, cl)
-    EXACTO_PIN_DECL
-    {
-        u64 x[16];
-        ks32_crt_values<LOGN, S>(x, U, R, r_stride, L, b, reinterpret_cast<uint32_t*>(lds), tid, KT, primes, qprimes);
-#define PIN_FROM_X(k) PIN_SET(k, x[k])
-        PIN_X16(PIN_FROM_X)
-#undef PIN_FROM_X
-    }
-    const uint32_t CL = 2 * L;
-    const long item = b / CL;
-    const int cl = (int)(b - (uint32_t)item * CL);
-    const PrimeConst& P = qprimes[cl % L];
-    lds_barrier();   // the lift's last LDS reads are done before the forward rounds reuse lds
-    PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q))
-    PIN_EXCHANGE(lds, tid, 0, LOGN - 4)
-    u64* dst = R + item * r_stride + (long)cl * N + tid;
-#define PIN_OUT(k) dst[(k) * T] = PIN_GET(k);
-    PIN_X16(PIN_OUT)
-#undef PIN_OUT
-}
-
-bool launch_ks32_crt_fwd(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn,
-                         const Ks32Tables* KT, const Prime32* primes, const PrimeConst* qprimes, hipStream_t s,
-                         int waves) {
-    const dim3 grid((unsigned)((long)items * 2 * L));
-#define CF_(LG, S_, W_) hipLaunchKernelGGL((ks32_crt_fwd_kernel<LG, S_, W_>), grid, dim3((1 << LG) / 16), 0, s, U, R, \
-                                           r_stride, L, KT, primes, qprimes)
-#define CFP_(LG, S_) hipLaunchKernelGGL((ks32_crt_fwd_pin_kernel<LG, S_>), grid, dim3((1 << LG) / 16), 0, s, U, R, \
-                                         r_stride, L, KT, primes, qprimes)
-#define CFW_(LG, S_) do { if (waves == 4) CFP_(LG, S_); else if (waves == 2) CF_(LG, S_, 2); else CF_(LG, S_, 3); } while (0)
-    if (items <= 0) return true;
-    if (logn == 12 && S == 3) CFW_(12, 3);
-    else if (logn == 13 && S == 3) CFW_(13, 3);
-    else if (logn == 12 && S == 2) CFW_(12, 2);
-    else if (logn == 13 && S == 2) CFW_(13, 2);
-    else return false;
-#undef CFW_
-#undef CFP_
-#undef CF_
-    return true;
-}
-
 bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,
                     hipStream_t s) {
-    // EXACTO_POLYMUL_PIN=1: the pinned form (4 waves per SIMD, a parked in out's rows) instead of
-    // ntt_polymul_kernel (2 waves): measured slower, 866-876 vs 806 us per cfg2 launch (same box), so
-    // off.  It parks a's evaluations before it reads b: never when out is b (in place on b).
-    static const bool pin_env = [] { const char* e = std::getenv("EXACTO_POLYMUL_PIN"); return e && e[0] == '1'; }();
-    const bool pin = pin_env && out != B;
-    if (pin && logn == 12)
-        hipLaunchKernelGGL(ntt_polymul_pin_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
-    else if (pin && logn == 13)
-        hipLaunchKernelGGL(ntt_polymul_pin_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
-    else if (logn == 12)
+    // (a pinned-home form at 4 waves per SIMD, a parked in out's rows, measured 866-876 vs 806 us per
+    // cfg2 launch and was removed, round 4)
+    if (logn == 12)
         hipLaunchKernelGGL(ntt_polymul_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
     else if (logn == 13)
         hipLaunchKernelGGL(ntt_polymul_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
     else
         return false;
     return true;
-}
-
-// ---------------------------------------------------------------- fused key switching
-
-// One workgroup per (product, limb i) of relinearize (keyswitch.rs:86-95):
-//   out_c[i] = NTT(R_c[i]) + sum_{g < guse} NTT(D_g[i]) (.) rlk_g,c[i]     (c = 0, 1)
-// The G forward transforms of the gadget digits never leave the chip: each digit is
-// transformed in registers/LDS and immediately multiply-accumulated (Shoup, with the
-// key's precomputed companions) into two register accumulators kept in [0, 2q).
-// R_c may already be in the NTT domain (r_ntt = 1, standalone relinearize).
-template <int LOGN, bool LAZY>
-__global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16, 3)
-keyswitch_kernel(KsArgs a, const PrimeConst* __restrict__ primes) {
-    constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
-    __shared__ u64 lds[N];
-    const int tid = T < 64 ? vtid() : (int)threadIdx.x;
-    const int L = a.L;
-    const long item = blockIdx.x / L;
-    const int i = (int)(blockIdx.x - item * L);
-    const PrimeConst& P = primes[i];
-    const u64 q = P.q, q2 = P.two_q, q8 = 8 * q, nq = (u64)0 - q;
-    const long Ln = (long)L * N;
-
-    auto ntt_canon = [&](u64 (&x)[16]) {
-        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, tw_table(P.tw_fwd), nq, q2, q8);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            u64 v = x[k];
-            if (LAZY) {
-                v = v >= q8 ? v - q8 : v;
-                v = v >= 4 * q ? v - 4 * q : v;
-            }
-            v = v >= q2 ? v - q2 : v;
-            x[k] = v >= q ? v - q : v;
-        }
-    };
-    auto load_coeff = [&](u64 (&x)[16], const u64* src) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
-    };
-    auto load_ntt = [&](u64 (&x)[16], const u64* src) {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const ulonglong2 v = s2[k];
-            x[2 * k] = v.x;
-            x[2 * k + 1] = v.y;
-        }
-    };
-
-    const u64* rbase = a.R + (a.r_off ? (long)a.r_off[item] : item * a.r_stride);
-    u64 acc0[16], acc1[16];
-    if (a.r_ntt) {
-        load_ntt(acc0, rbase + (long)i * N);
-        load_ntt(acc1, rbase + Ln + (long)i * N);
-    } else {
-        load_coeff(acc0, rbase + (long)i * N);
-        ntt_canon(acc0);
-        load_coeff(acc1, rbase + Ln + (long)i * N);
-        ntt_canon(acc1);
-    }
-    const u64* dbase = a.D + item * (long)a.guse * Ln + (long)i * N;
-    for (int g = 0; g < a.guse; ++g) {
-        u64 x[16];
-        load_coeff(x, dbase + g * Ln);
-        fwd_rounds<LOGN, 0, LAZY, false>(x, lds, tid, tw_table(P.tw_fwd), nq, q2, q8);  // any value < 2^64 is a valid Shoup input
-        const long ko = ((long)(2 * g) * L + i) * N + 16 * tid;
-        const ulonglong2* k0 = reinterpret_cast<const ulonglong2*>(a.rlk + ko);
-        const ulonglong2* k0s = reinterpret_cast<const ulonglong2*>(a.rlk_s + ko);
-        const ulonglong2* k1 = reinterpret_cast<const ulonglong2*>(a.rlk + ko + Ln);
-        const ulonglong2* k1s = reinterpret_cast<const ulonglong2*>(a.rlk_s + ko + Ln);
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            // keep at most two groups of key loads in flight (register pressure: the two
-            // accumulators already hold 64 VGPRs)
-            if (h % 2 == 0) asm volatile("" ::: "memory");
-            const ulonglong2 w0 = k0[h], w0s = k0s[h], w1 = k1[h], w1s = k1s[h];
-            u64 t;
-            t = acc0[2 * h] + shoup_mul_nq(x[2 * h], w0.x, w0s.x, nq);
-            acc0[2 * h] = t >= q2 ? t - q2 : t;
-            t = acc0[2 * h + 1] + shoup_mul_nq(x[2 * h + 1], w0.y, w0s.y, nq);
-            acc0[2 * h + 1] = t >= q2 ? t - q2 : t;
-            t = acc1[2 * h] + shoup_mul_nq(x[2 * h], w1.x, w1s.x, nq);
-            acc1[2 * h] = t >= q2 ? t - q2 : t;
-            t = acc1[2 * h + 1] + shoup_mul_nq(x[2 * h + 1], w1.y, w1s.y, nq);
-            acc1[2 * h + 1] = t >= q2 ? t - q2 : t;
-        }
-    }
-    u64* obase = a.out + item * a.out_stride + (long)i * N + 16 * tid;
-    ulonglong2* o0 = reinterpret_cast<ulonglong2*>(obase);
-    ulonglong2* o1 = reinterpret_cast<ulonglong2*>(obase + Ln);
-#pragma unroll
-    for (int h = 0; h < 8; ++h) {
-        u64 a0 = acc0[2 * h], a1 = acc0[2 * h + 1], b0 = acc1[2 * h], b1 = acc1[2 * h + 1];
-        o0[h] = make_ulonglong2(a0 >= q ? a0 - q : a0, a1 >= q ? a1 - q : a1);
-        o1[h] = make_ulonglong2(b0 >= q ? b0 - q : b0, b1 >= q ? b1 - q : b1);
-    }
 }
 
 // rlk_s = floor(rlk * 2^64 / q_limb) (Shoup companions of the resident key, computed once)
@@ -1690,114 +1078,6 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
     else
         hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
-}
-
-// One workgroup per (item, prime) for all three tensor components: the four operands are read once
-// (the per-component form reads eight), c0 = a0 b0, c1 = a0 b1 + a1 b0, c2 = a1 b1 are formed in
-// registers, and the three inverse transforms run back to back with the other components held
-// in registers (2 waves per SIMD).  n = 4096 / 8192, special primes (mulmod_near60, asm rounds).
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(2)))
-ntt_inv_tensor3_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                       const PrimeConst* __restrict__ primes, int per) {
-    constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
-    __shared__ u64 lds[N];
-    __shared__ u64 stash[N];   // c2 while c0 and c1 are transformed (lane-interleaved: no bank conflicts)
-    const int tid = threadIdx.x;
-    const int NP = L + K;
-    // per = NP, or L (psum: the auxiliary primes' third components by ntt_inv_tensor_c2_kernel)
-    const long p = blockIdx.x;
-    const long item = p / per;
-    const int t = (int)(p - item * per);
-    const PrimeConst& P = primes[t];
-    const u64 *A0, *A1, *B0, *B1;
-    if (t < L) {
-        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
-        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
-        A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
-        B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
-    } else if (op.ea) {
-        const u64* EA = op.ea + (long)op.ea_off[item] + (long)(t - L) * N;
-        const u64* EB = op.eb + (long)op.eb_off[item] + (long)(t - L) * N;
-        A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
-    } else {
-        const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
-        A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
-    }
-    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
-    auto load = [&](const u64* src, u64 (&v)[16]) {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const ulonglong2 w = s2[k];
-            v[2 * k] = w.x;
-            v[2 * k + 1] = w.y;
-        }
-    };
-    u64 c0[16], c1[16];
-    {
-        u64 a0[16], a1[16], b0[16], b1[16];
-        load(A0, a0);
-        load(B0, b0);
-        load(A1, a1);
-        load(B1, b1);
-#pragma unroll
-        for (int k = 0; k < 16; k += 2) {
-            u64 p0, p1, s0, s1;
-            mul2_near60<false>(p0, a1[k], b1[k], p1, a1[k + 1], b1[k + 1], dq);
-            stash[k * T + tid] = p0;
-            stash[(k + 1) * T + tid] = p1;
-            mul2_near60<false>(p0, a0[k], b1[k], p1, a0[k + 1], b1[k + 1], dq);
-            mul2_near60<false>(s0, a1[k], b0[k], s1, a1[k + 1], b0[k + 1], dq);
-            c1[k] = p0 + s0;             // < 4q
-            c1[k + 1] = p1 + s1;
-            mul2_near60<false>(c0[k], a0[k], b0[k], c0[k + 1], a0[k + 1], b0[k + 1], dq);
-        }
-    }
-    const AsmK AK = make_asmk_inv(P);
-    const TwTab ti = tw_table(P.tw_inv);
-    u64* dst = Tout + (item * 3 * NP + t) * N;   // [item][c][prime][n]
-    inv_rounds_asm<LOGN, 0>(c0, lds, tid, ti, AK);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = c0[k];
-    inv_rounds_asm<LOGN, 0>(c1, lds, tid, ti, AK);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[(long)NP * N + elem_index<LAST_LO>(tid, k)] = c1[k];
-    u64 c2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c2[k] = stash[k * T + tid];   // this thread's own words: no barrier
-    inv_rounds_asm<LOGN, 0>(c2, lds, tid, ti, AK);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[2L * NP * N + elem_index<LAST_LO>(tid, k)] = c2[k];
-}
-
-// psum: the third tensor component alone in the auxiliary primes (shared extensions), block =
-// (item, a): c2 = a1 b1 of prime L + a, inverse-transformed into T[item][2][L + a].
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
-ntt_inv_tensor_c2_kernel(Operands op, u64* __restrict__ Tout, int L, int K, const PrimeConst* __restrict__ primes) {
-    constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
-    __shared__ u64 lds[N];
-    const int tid = threadIdx.x;
-    const long item = blockIdx.x / K;
-    const int a = (int)(blockIdx.x - item * K);
-    const PrimeConst& P = primes[L + a];
-    const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
-    const ulonglong2* s1 = reinterpret_cast<const ulonglong2*>(op.ea + (long)op.ea_off[item] + (long)(K + a) * N + 16 * tid);
-    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(op.eb + (long)op.eb_off[item] + (long)(K + a) * N + 16 * tid);
-    u64 x[16];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const ulonglong2 u = s1[e], v = s2[e];
-        mul2_near60<false>(x[2 * e], u.x, v.x, x[2 * e + 1], u.y, v.y, dq);
-    }
-    inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
-    u64* dst = Tout + ((item * 3 + 2) * (L + K) + L + a) * N;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dst[elem_index<LAST_LO>(tid, e)] = x[e];
 }
 
 // dBFV, psum (dbfv_mul_core): the auxiliary-prime residues of each output limb's c0 and c1 tensors
@@ -1849,18 +1129,10 @@ void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int n
                        terms, primes);
 }
 
-// one workgroup per (item, prime) at n = 8192 (cfg5 +1.6 % A/B); at n = 4096 the per-component
-// form at 3 waves per SIMD is faster (327 vs 335 us per cfg3 chunk).  EXACTO_TENSOR3=0/1 forces.
-static bool tensor3_at(int logn) {
-    static const int t3env = [] { const char* e = std::getenv("EXACTO_TENSOR3"); return e ? (e[0] == '1') : -1; }();
-    return t3env >= 0 ? t3env == 1 : logn == 13;
-}
-
-// pinned-home kernels (runtime A/B switches, read once).  Tensor: ntt_inv_tensor_pin_kernel at
-// n = 8192 replaces tensor3 + tensor_c2 (cfg5 1996 -> 2175 chains/s, same box); at n = 4096 the
-// 3-wave ntt_inv_tensor_kernel stays (pinned 297-302 vs 295-296 us per cfg3 launch).
-// EXACTO_TENSOR_PIN=0: never, =1: at both sizes.  EXACTO_FWD_PIN=0: the forward
-// ntt_fwd_asm_kernel instead of ntt_fwd_pin_kernel (n = 8192: 41 -> 33 us per cfg5 launch).
+// Pinned-home tensor kernel (runtime A/B switch, read once): ntt_inv_tensor_pin_kernel at n = 8192
+// (it replaced the one-block-per-(item, prime) tensor3 + tensor_c2 pair: cfg5 1996 -> 2175 chains/s,
+// same box); at n = 4096 the 3-wave ntt_inv_tensor_kernel stays (pinned 297-302 vs 295-296 us per
+// cfg3 launch).  EXACTO_TENSOR_PIN=0: never, =1: at both sizes.
 static int env_switch(const char* name, int dflt) {
     const char* e = std::getenv(name);
     return e && e[0] ? (e[0] != '0') : dflt;
@@ -1869,43 +1141,18 @@ static bool tensor_pin_at(int logn) {
     static const int on = env_switch("EXACTO_TENSOR_PIN", -1);
     return on < 0 ? logn == 13 : on && (logn == 12 || logn == 13);
 }
-static bool fwd_pin() {
-    static const int on = env_switch("EXACTO_FWD_PIN", 1);
-    return on;
-}
-
-bool inverse_tensor_split(int logn) {
-    return (logn == 12 || logn == 13) && !tensor_pin_at(logn) && tensor3_at(logn);
-}
 
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int part = -1) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
-    const bool t3 = tensor3_at(LOGN);
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv && tensor_pin_at(LOGN)) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L, K,
                                primes, remap, p2only);
-            return;
-        }
-        if (asm_inv && t3) {
-            // blocks = items * 3 (L + K); psum: the ciphertext primes here, the auxiliary c2 apart
-            const long items = blocks / (3 * (L + K));
-            if (p2only) {
-                if (part != 1)
-                    hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * L), dim3(threads), 0, s, op, extP, T,
-                                       L, K, primes, L);
-                if (part != 0)
-                    hipLaunchKernelGGL((ntt_inv_tensor_c2_kernel<LOGN>), dim3(items * K), dim3(threads), 0, s, op, T, L,
-                                       K, primes);
-            } else {
-                hipLaunchKernelGGL((ntt_inv_tensor3_kernel<LOGN>), dim3(items * (L + K)), dim3(threads), 0, s, op, extP, T,
-                                   L, K, primes, L + K);
-            }
             return;
         }
         if (asm_inv) {
@@ -1924,12 +1171,12 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int part) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
-        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, part);
-        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, part);
+        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
+        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
         return;
     }
     switch (logn) {
@@ -1948,47 +1195,20 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
     }
 }
 
-static int cu_count() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-    }
-    return cus;
-}
-
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd, bool pipe, bool asm_inv) {
+                hipStream_t s, bool asm_fwd, bool asm_inv) {
     if (count <= 0) return;
-    if (asm_fwd && pipe && !inverse && logn == 12) {
-        // two resident workgroups per CU; a grid that is a multiple of the prime period keeps
-        // every workgroup on one prime (twiddles loaded once)
-        const int slots = 2 * cu_count();
-        int grid = slots >= nb.period ? (slots / nb.period) * nb.period : slots;
-        if (grid > count) grid = count;
-        hipLaunchKernelGGL(ntt_fwd_pipe_kernel, dim3(grid), dim3(256), 0, s, nb, primes, count);
+    // n = 4096 / 8192, every prime of the batch in (2^60 - 2^32, 2^60): the pinned-home kernels (the
+    // non-pinned asm kernels and the persistent LDS-DMA forward kernel measured slower and were removed,
+    // DESIGN.md §6)
+    if (asm_fwd && !inverse && (logn == 12 || logn == 13)) {
+        if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
-    if (asm_fwd && !inverse && logn == 12) {
-        if (fwd_pin()) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_fwd_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        return;
-    }
-    if (asm_inv && inverse && logn == 12) {
-        if (EXACTO_NTT_PIN) hipLaunchKernelGGL((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_inv_asm_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        return;
-    }
-    if (asm_inv && inverse && logn == 13) {
-        if (EXACTO_NTT_PIN) hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_inv_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
-        return;
-    }
-    if (asm_fwd && !inverse && logn == 13) {
-        if (fwd_pin()) hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_fwd_asm_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+    if (asm_inv && inverse && (logn == 12 || logn == 13)) {
+        if (logn == 12) hipLaunchKernelGGL((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     switch (logn) {
@@ -2004,34 +1224,6 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         case 13: launch_one<13>(nb, count, inverse, lazy, primes, s); break;
         case 14: launch_one<14>(nb, count, inverse, lazy, primes, s); break;
         default: break;  // rejected at context creation
-    }
-}
-
-template <int LOGN>
-static void launch_ks(const KsArgs& a, int blocks, bool lazy, const PrimeConst* primes, hipStream_t s) {
-    constexpr int threads = (1 << LOGN) / 16;
-    if (lazy)
-        hipLaunchKernelGGL((keyswitch_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, a, primes);
-    else
-        hipLaunchKernelGGL((keyswitch_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, a, primes);
-}
-
-void launch_keyswitch(const KsArgs& a, int items, int logn, bool lazy, const PrimeConst* primes, hipStream_t s) {
-    const int blocks = items * a.L;
-    if (blocks <= 0) return;
-    switch (logn) {
-        case 4: launch_ks<4>(a, blocks, lazy, primes, s); break;
-        case 5: launch_ks<5>(a, blocks, lazy, primes, s); break;
-        case 6: launch_ks<6>(a, blocks, lazy, primes, s); break;
-        case 7: launch_ks<7>(a, blocks, lazy, primes, s); break;
-        case 8: launch_ks<8>(a, blocks, lazy, primes, s); break;
-        case 9: launch_ks<9>(a, blocks, lazy, primes, s); break;
-        case 10: launch_ks<10>(a, blocks, lazy, primes, s); break;
-        case 11: launch_ks<11>(a, blocks, lazy, primes, s); break;
-        case 12: launch_ks<12>(a, blocks, lazy, primes, s); break;
-        case 13: launch_ks<13>(a, blocks, lazy, primes, s); break;
-        case 14: launch_ks<14>(a, blocks, lazy, primes, s); break;
-        default: break;
     }
 }
 

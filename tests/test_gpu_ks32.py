@@ -111,29 +111,3 @@ def test_ks32_automorphism_matches_limbwise(gpu_available, n, which, B, keys, ch
         if n <= 1024:
             keyset = obfv.GaloisKey(np_to_rlk(gk, prm).keys, element, prm)
             assert np.array_equal(got[0], ct_to_np(obfv.bfv_apply_automorphism(np_to_ct(ct[0], prm), keyset)))
-
-
-@pytest.mark.parametrize("n,which,waves", [(4096, "cfg3", "3"), (4096, "cfg3", "2"), (8192, "cfg5", "3")])
-def test_fused_lift_forward_opt_in(gpu_available, n, which, waves):
-    """EXACTO_CRT_FWD (opt-in): the ks32 lift and the forward NTT of the outputs in one kernel
-    (ks32_crt_fwd_kernel) equal the separate kernels bit for bit."""
-    prm = _params(which, n)
-    q = prm.ct_basis.moduli
-    rng = np.random.default_rng(77 + n)
-    ct1 = uniform_residues(rng, (3, 2), q, n)
-    ct2 = uniform_residues(rng, (3, 2), q, n)
-    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
-    outs = []
-    for v in (waves, "0"):
-        old = os.environ.get("EXACTO_CRT_FWD")
-        os.environ["EXACTO_CRT_FWD"] = v
-        try:
-            ctx = HipContext.from_params(prm, device=0)
-        finally:
-            if old is None:
-                del os.environ["EXACTO_CRT_FWD"]
-            else:
-                os.environ["EXACTO_CRT_FWD"] = old
-        ctx.load_relin_key(rlk)
-        outs.append(ctx.bfv_mul_and_relin(ct1, ct2))
-    assert np.array_equal(outs[0], outs[1])

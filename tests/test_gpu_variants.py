@@ -1,12 +1,15 @@
-"""The kernel-selection switches give bit-identical results: every A/B alternative that ships in
-the library (the pinned-home forward / tensor / polymul kernels against the asm, pipe, tensor3 +
-tensor_c2 and register-resident forms; the fused ks32 lift + forward kernels against the separate
-ones) computes the same outputs as the default selection.
+"""Every selection switch the library reads gives bit-identical results: each alternative kernel or
+path computes the same outputs as the default selection.
 
-Each switch is read once per process, so each variant runs tests/variant_digest.py in a child
-process (sequentially, one GPU process at a time) and the digests are compared with the default's.
-The default selection itself is pinned to the oracle by the rest of the suite (test_gpu_golden.py
-digests, test_gpu_ntt.py, test_gpu_psum.py); bit-exact, integer work.
+The switches are read once per process, so each variant runs tests/variant_digest.py in a child
+process (sequentially, one GPU process at a time) over the case groups the switch affects, and the
+digests are compared with the default's.  The default selection itself is pinned to the oracle by
+the rest of the suite (test_gpu_golden.py digests, test_gpu_published.py, test_gpu_ntt.py,
+test_gpu_psum.py); bit-exact, integer work.
+
+Not listed (no effect on results): EXACTO_SCRATCH_POOL / EXACTO_DEBUG_SCRATCH / EXACTO_DEBUG_FILL
+(allocation diagnostics, tools/diag.sh), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
+EXACTO_PROF_RAW (profiling arithmetic), EXACTO_RCCL_LIB (library path).
 """
 
 import json
@@ -19,38 +22,66 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# name: (environment, case groups of tests/variant_digest.py)
 VARIANTS = {
-    "tensor_pin_both": {"EXACTO_TENSOR_PIN": "1"},
-    "tensor_pin_none": {"EXACTO_TENSOR_PIN": "0"},
-    "asm_fwd_and_pipe": {"EXACTO_FWD_PIN": "0", "EXACTO_NTT_PIPE": "1"},
-    "polymul_pin": {"EXACTO_POLYMUL_PIN": "1"},
-    "crt_fwd_pin": {"EXACTO_CRT_FWD": "4"},
-    "crt_fwd_3waves": {"EXACTO_CRT_FWD": "3"},
+    "tensor_pin_both": ({"EXACTO_TENSOR_PIN": "1"}, ["cfg3", "cfg4"]),
+    "tensor_pin_none": ({"EXACTO_TENSOR_PIN": "0"}, ["cfg5"]),
+    "ntt_asm_off": ({"EXACTO_NTT_ASM": "0"}, ["cfg3", "cfg5", "hps"]),
+    "ntt_asm_inv_off": ({"EXACTO_NTT_ASM_INV": "0"}, ["cfg3", "cfg5", "hps"]),
+    "one_lane": ({"EXACTO_DUAL_STREAM": "0"}, ["cfg3", "cfg5"]),
+    "three_lanes": ({"EXACTO_LANES": "3"}, ["cfg3"]),
+    "share_ext_off": ({"EXACTO_SHARE_EXT": "0"}, ["cfg4", "cfg5", "hps"]),
+    "digit16_off": ({"EXACTO_DIGIT16": "0"}, ["cfg3", "cfg4"]),
+    "digit8_off": ({"EXACTO_DIGIT8": "0"}, ["cfg5", "hps"]),
+    "ks32_off": ({"EXACTO_KS32": "0"}, ["cfg3", "cfg4", "cfg5"]),
+    "ks32_wide_off": ({"EXACTO_KS32_WIDE": "0"}, ["cfg4"]),
+    "ks32_wide_primary": ({"EXACTO_KS32_WIDE": "2"}, ["cfg3", "cfg4"]),
+    "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
+    "dot30_off": ({"EXACTO_DOT30": "0"}, ["cfg3", "cfg5"]),
+    "xcd_remap_off": ({"EXACTO_XCD_REMAP": "0"}, ["cfg3"]),
+    "mac_lds_off": ({"EXACTO_MAC_LDS": "0"}, ["hps"]),
     # HPS: the literal i128 scale against the division-free one, per-product relinearisation against
     # dbfv_mul's per-limb digit sums
-    "hps_literal": {"EXACTO_HPS_LITERAL": "1"},
-    "hps_per_product": {"EXACTO_HPS_SUM": "0"},
+    "hps_literal": ({"EXACTO_HPS_LITERAL": "1"}, ["hps"]),
+    "hps_per_product": ({"EXACTO_HPS_SUM": "0"}, ["hps"]),
 }
+SWITCHES = sorted({k for env, _ in VARIANTS.values() for k in env})
 
 
-def _digests(extra_env):
+def _digests(extra_env, groups):
     env = dict(os.environ)
-    for k in ("EXACTO_TENSOR_PIN", "EXACTO_FWD_PIN", "EXACTO_NTT_PIPE", "EXACTO_POLYMUL_PIN", "EXACTO_TENSOR3",
-              "EXACTO_CRT_FWD", "EXACTO_HPS_LITERAL", "EXACTO_HPS_SUM"):
+    for k in SWITCHES:
         env.pop(k, None)
     env.update(extra_env)
-    r = subprocess.run([sys.executable, os.path.join(HERE, "variant_digest.py")], env=env, capture_output=True,
-                       text=True, timeout=240)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "variant_digest.py"), *groups], env=env,
+                       capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 @pytest.fixture(scope="module")
 def default_digests(gpu_available):
-    return _digests({})
+    return _digests({}, [])
+
+
+def test_every_library_switch_is_covered():
+    """Every runtime switch the library source reads is either a variant here or listed above as
+    result-neutral."""
+    import re
+    src = os.path.join(os.path.dirname(HERE), "exacto_amd", "csrc")
+    found = set()
+    for f in os.listdir(src):
+        if f.endswith((".hip", ".hpp")):
+            with open(os.path.join(src, f)) as fh:
+                found |= set(re.findall(r'(?:getenv|env_switch)\("(EXACTO_[A-Z0-9_]+)"', fh.read()))
+    neutral = {"EXACTO_SCRATCH_POOL", "EXACTO_DEBUG_SCRATCH", "EXACTO_DEBUG_FILL", "EXACTO_DBFV_GROUP_MB",
+               "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB"}
+    assert found - neutral == set(SWITCHES), found ^ (set(SWITCHES) | neutral)
 
 
 @pytest.mark.parametrize("name", sorted(VARIANTS))
 def test_variant_matches_default(default_digests, name):
-    got = _digests(VARIANTS[name])
-    assert got == default_digests, {k: (got.get(k), v) for k, v in default_digests.items() if got.get(k) != v}
+    env, groups = VARIANTS[name]
+    got = _digests(env, groups)
+    want = {k: v for k, v in default_digests.items() if k in got}
+    assert got and got == want, {k: (got.get(k), v) for k, v in want.items() if got.get(k) != v}

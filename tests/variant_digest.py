@@ -1,11 +1,14 @@
-"""Digests of the hot path's outputs under the kernel-selection switches of this process's
+"""Digests of the hot path's outputs under the kernel / path selection switches of this process's
 environment (run as a child process by tests/test_gpu_variants.py: each switch is read once per
-process).  Prints one JSON object {case: sha256}.
+process).  Prints one JSON object {case: sha256}.  argv: the case groups to run (default: all).
 
-Cases: cfg3 bfv_mul_and_relin (n = 4096, 3 limbs: forward, inverse, tensor, key switch), cfg5
-dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels), the HPS path
-(compact_bfv products, u64_dbfv dbfv_mul), and the fused NTT product at n = 4096 / 8192, out of
-place and in place on b.
+Case groups:
+  cfg3    bfv_mul_and_relin, n = 4096, 3 limbs (forward, inverse, tensor, ks32 key switch), 160
+          products in pipeline chunks of 64 (three chunks: both lanes, or three with EXACTO_LANES=3)
+  cfg4    dbfv_mul d = 2 (n = 4096, 3 limbs: psum, the wide 31-bit basis for int32 digit sums)
+  cfg5    dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels)
+  hps     compact_bfv products (one aux prime) and a u64_dbfv dbfv_mul (two aux primes, digit sums)
+  polymul the fused NTT product at n = 4096 / 8192, out of place and in place on b
 """
 
 import hashlib
@@ -23,24 +26,40 @@ from bridge import uniform_residues  # noqa: E402
 from oracle import params as P  # noqa: E402
 from exacto_amd._ffi import HipContext  # noqa: E402
 
+GROUPS = ("cfg3", "cfg4", "cfg5", "hps", "polymul")
+
 
 def sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint64).tobytes()).hexdigest()
 
 
-def main():
-    import torch
-    out = {}
+def cfg3(out):
     prm = P.cfg3_params(4096)
     q, n = prm.ct_basis.moduli, 4096
     rng = np.random.default_rng(7001)
-    ct1 = uniform_residues(rng, (8, 2), q, n)
-    ct2 = uniform_residues(rng, (8, 2), q, n)
+    ct1 = uniform_residues(rng, (160, 2), q, n)
+    ct2 = uniform_residues(rng, (160, 2), q, n)
     rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
     ctx = HipContext.from_params(prm)
+    ctx.set_chunk(64)
     ctx.load_relin_key(rlk)
     out["cfg3_mul_relin"] = sha(ctx.bfv_mul_and_relin(ct1, ct2))
 
+
+def cfg4(out):
+    dp = P.cfg4_params(4096)
+    prm = dp.bfv_params
+    q, d = prm.ct_basis.moduli, dp.num_digits
+    rng = np.random.default_rng(7006)
+    a = uniform_residues(rng, (3, d, 2), q, 4096)
+    b = uniform_residues(rng, (3, d, 2), q, 4096)
+    rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, 4096)
+    ctx = HipContext.from_params(prm)
+    ctx.load_relin_key(rlk)
+    out["cfg4_dbfv_mul"] = sha(ctx.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
+
+
+def cfg5(out):
     dp = P.cfg5_params(8192)
     prm5 = dp.bfv_params
     q5, d = prm5.ct_basis.moduli, dp.num_digits
@@ -53,7 +72,8 @@ def main():
     out["cfg5_dbfv_mul"] = sha(ctx5.dbfv_mul(d, dp.base, dp.plain_modulus, a, b)[0])
     out["cfg5_chain2"] = sha(ctx5.dbfv_mul_chain(d, dp.base, dp.plain_modulus, a, b, 2))
 
-    # HPS: compact_bfv (one aux prime) and u64_dbfv (two aux primes, dbfv_mul with summed digits)
+
+def hps(out):
     cb = P.compact_bfv()
     rng = np.random.default_rng(7004)
     qc = cb.ct_basis.moduli
@@ -75,6 +95,9 @@ def main():
     uc.load_relin_key(uk)
     out["u64dbfv_dbfv_mul"] = sha(uc.dbfv_mul(du.num_digits, du.base, du.plain_modulus, ua, ub)[0])
 
+
+def polymul(out):
+    import torch
     for nn, qs in ((4096, [1152921504606830593]), (8192, [1152921504606830593, 1152921504606748673])):
         rng = np.random.default_rng(7003 + nn)
         c = HipContext(nn, qs, plain_modulus=257)
@@ -89,6 +112,12 @@ def main():
         c.synchronize()
         out[f"polymul_{nn}"] = sha(o.cpu().numpy().view(np.uint64))
         out[f"polymul_{nn}_inplace"] = sha(dy.cpu().numpy().view(np.uint64))
+
+
+def main():
+    out = {}
+    for g in (sys.argv[1:] or GROUPS):
+        globals()[g](out)
     print(json.dumps(out))
 
 

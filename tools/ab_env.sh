@@ -2,7 +2,7 @@
 # Same-box A/B of runtime switches on bench.py lines: each variant is a comma-separated list of
 # VAR=value settings ("-" = the defaults), run alternately, two repetitions per config.
 # usage: bash tools/ab_env.sh <name> "<variant> <variant> ..." [configs]
-#   e.g. bash tools/ab_env.sh pin "- EXACTO_TENSOR_PIN=0 EXACTO_FWD_PIN=0" cfg3 cfg5
+#   e.g. bash tools/ab_env.sh pin "- EXACTO_TENSOR_PIN=0 EXACTO_TENSOR_PIN=1" cfg3 cfg5
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/${1:-abenv}; VARS=${2:--}; shift 2
 mkdir -p $O

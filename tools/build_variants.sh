@@ -30,22 +30,14 @@ for v in "$@"; do
     as1) build as1 -DEXACTO_TW_AS=1 ;;
     as1_w4) build as1_w4 -DEXACTO_TW_AS=1 -DEXACTO_NTT_WAVES=4 ;;
     as4_w4) build as4_w4 -DEXACTO_NTT_WAVES=4 ;;
-    old) build old -DEXACTO_NTT_TOUT=0 -DEXACTO_NTT_TIN=0 ;;
-    tout) build tout -DEXACTO_NTT_TIN=0 ;;
-    tin) build tin -DEXACTO_NTT_TOUT=0 ;;
+    notout) build notout -DEXACTO_NTT_TOUT=0 ;;
     nopre) build nopre -DEXACTO_NTT_PRELOAD=0 ;;
     nopre_w5) build nopre_w5 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=5 ;;
     nopre_w6) build nopre_w6 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=6 ;;
     w5) build w5 -DEXACTO_NTT_WAVES=5 ;;
     ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
-    noaddx) build noaddx -DEXACTO_ASM_ADDX=0 ;;
     nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
-    tin) build tin -DEXACTO_ASM_TIN=1 ;;
-    n1shift) build_gen n1shift EXACTO_ASM_N1SHIFT=1 ;;
-    nopin) build nopin -DEXACTO_NTT_PIN=0 ;;
-    pipe_p1) build pipe_p1 -DEXACTO_PIPE_PROBE=1 ;;
-    pipe_p2) build pipe_p2 -DEXACTO_PIPE_PROBE=2 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done

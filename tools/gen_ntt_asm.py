@@ -60,7 +60,6 @@ W = int(os.environ.get("EXACTO_ASM_STREAMS", "2"))       # butterflies interleav
 SGPR_C = [80, 82, 84, 88, 90, 92][:max(W, 2)]            # carry pair of each stream
 SGPR_SD = 86                  # sink for the carry-out of v_mad_u64_u32 where it is not used
 INV_BOUND_IN = 4              # inverse round 0 input bound (the fused tensor's c1 < 4q)
-N1SHIFT = os.environ.get("EXACTO_ASM_N1SHIFT", "0") == "1"   # qh.lo * n1 by shift + sub (A/B)
 
 
 def v(i):
@@ -177,16 +176,8 @@ def shoup_seq(st, yl, yh, w0, w1, s0, s1, T, c, approx, fixup=True, E=None, adde
         Ins(f"v_mad_u64_u32 {A}, {SD}, {yh}, {s1}, {A}", wr=[SD]),
         Ins(f"v_mad_u64_u32 {E}, {SD}, {lo(A)}, {st.n0()}, {E}", wr=[SD]),
     ]
-    if N1SHIFT:
-        # qh.lo * n1 with n1 = 2^32 - 2^28 is -(qh.lo << 28) mod 2^32: a shift and a subtraction
-        # instead of a multiply (B is free once its high word has moved to A.lo)
-        seq += [
-            Ins(f"v_lshlrev_b32 {hi(B)}, 28, {lo(A)}"),
-            Ins(f"v_sub_u32 {lo(F)}, {lo(F)}, {hi(B)}"),
-        ]
-    else:
-        seq.append(Ins(f"v_mad_u64_u32 {F}, {SD}, {lo(A)}, {st.n1()}, {F}", wr=[SD]))
     seq += [
+        Ins(f"v_mad_u64_u32 {F}, {SD}, {lo(A)}, {st.n1()}, {F}", wr=[SD]),
         Ins(f"v_mad_u64_u32 {F}, {SD}, {hi(A)}, {st.n0()}, {F}", wr=[SD]),
     ]
     if fixup:
@@ -744,12 +735,10 @@ HEADER = """// GENERATED by tools/gen_ntt_asm.py -- do not edit.
 // generator's docstring.  Included inside namespace exacto by ntt.hip.
 #pragma once
 
-#ifndef EXACTO_ASM_APPROX
-#define EXACTO_ASM_APPROX 1   // Shoup quotient without the low-low partial product (T < 3q)
-#endif
-#ifndef EXACTO_ASM_ADDX
-#define EXACTO_ASM_ADDX 1     // forward butterflies: X as the Shoup chain's addend (one add less)
-#endif
+// Emitted forms (measured, DESIGN.md §4): the approximate Shoup quotient (no low-low partial
+// product, T < 3q) and, in forward butterflies, X as the Shoup chain's free addend.  The exact
+// quotient and the separate X + T add are still modelled by the generator (tools/asm_sim.py checks
+// both) but no longer emitted.
 
 struct AsmK {
     uint32_t n0, n1;      // 2^64 - q (n1 = 0xF0000000 for the primes of this path)
@@ -790,25 +779,20 @@ def main():
     parts = [HEADER, pin_homes_decl(), "\n", MulPair(2).emit(), "\n", MulPair(1).emit(), "\n",
              MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinAsm", volatile=False).emit(), "\n",
              MulPair(2, base=PIN_BASE - 28, struct="MulNear60PinVAsm").emit(), "\n"]
-    for approx in (True, False):
-        parts.append(f"#if {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
-        for logn in (12, 13):
-            for addx in (True, False):
-                parts.append(f"#if {'' if addx else '!'}EXACTO_ASM_ADDX\n\n")
-                for r in range((logn + 3) // 4):
-                    parts.append(Round(logn, r, approx, addx).emit())
-                    parts.append("\n")
-                parts.append(f"#endif  // {'' if addx else '!'}EXACTO_ASM_ADDX\n\n")
-            for rd in inv_rounds(logn, approx):
-                parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
-                parts.append("\n")
-            for r in range((logn + 3) // 4):
-                parts.append(Round(logn, r, approx, True, pinned=True).emit())
-                parts.append("\n")
-            for rd in inv_rounds_pinned(logn, approx):
-                parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
-                parts.append("\n")
-        parts.append(f"#endif  // {'' if approx else '!'}EXACTO_ASM_APPROX\n\n")
+    approx, addx = True, True
+    for logn in (12, 13):
+        for r in range((logn + 3) // 4):
+            parts.append(Round(logn, r, approx, addx).emit())
+            parts.append("\n")
+        for rd in inv_rounds(logn, approx):
+            parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
+            parts.append("\n")
+        for r in range((logn + 3) // 4):
+            parts.append(Round(logn, r, approx, True, pinned=True).emit())
+            parts.append("\n")
+        for rd in inv_rounds_pinned(logn, approx):
+            parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
+            parts.append("\n")
     with open(OUT, "w") as f:
         f.write("".join(parts).rstrip("\n") + "\n")
     print("wrote", OUT)
