@@ -623,7 +623,10 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 
 // Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds, exchanges and
 // coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
-template <int LOGN>
+// PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic
+// canonical inputs, no global loads, stores skipped at run time), 2 = memory only (loads, the
+// same LDS exchanges and stores, no butterflies and no twiddle loads).
+template <int LOGN, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
@@ -637,7 +640,12 @@ ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     const u64 q = P.q;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     EXACTO_PIN_DECL
-    if (nb.src16) {
+    if constexpr (PROBE == 1) {
+        const u64 h = ((u64)p << 20) ^ (u64)tid;
+#define PIN_SYN(k) PIN_SET(k, ((h + (k)) * 0x9E3779B97F4A7C15ull) & ((1ull << 59) - 1))
+        PIN_X16(PIN_SYN)
+#undef PIN_SYN
+    } else if (nb.src16) {
         const int16_t* s16 = nb.src16 + (long)item * nb.src16_item_stride + (long)(sub / nb.period) * N + tid;
 #define PIN_IN16(k) { const i64 d_ = s16[(k) * T]; PIN_SET(k, d_ < 0 ? q + (u64)d_ : (u64)d_) }
         PIN_X16(PIN_IN16)
@@ -649,9 +657,18 @@ ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         PIN_X16(PIN_IN64)
 #undef PIN_IN64
     }
-    PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q))
+    if constexpr (PROBE == 2) {   // the exchanges of PIN_FWD_ROUNDS without its butterflies
+        PIN_EXCHANGE(lds, tid, LOGN - 4, LOGN - 8)
+        PIN_EXCHANGE(lds, tid, LOGN - 8, LOGN == 12 ? 0 : 1)
+        if constexpr (LOGN == 13) PIN_EXCHANGE(lds, tid, 1, 0)
+    } else {
+        PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q))
+    }
     // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
     PIN_EXCHANGE(lds, tid, 0, LOGN - 4)
+    if constexpr (PROBE == 1) {
+        if (nb.dst_item_stride != -7) return;   // never stored; the compiler cannot drop the work
+    }
 #define PIN_OUT(k) dst[tid + (k) * T] = PIN_GET(k);
     PIN_X16(PIN_OUT)
 #undef PIN_OUT
@@ -742,7 +759,9 @@ __device__ __forceinline__ long xcd_group_remap(long b, long total, int G) {
     return ((slot / G) * 8 + x) * G + slot % G;
 }
 
-template <int LOGN, bool LAZY, bool ASM = false>
+// PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic operands
+// instead of the loads, stores skipped at run time).
+template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
@@ -756,10 +775,12 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     const int NP = L + K;
     // the three components of one (item, prime) read overlapping inputs (c1 reads c0's and c2's):
     // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
-    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
     // p2only (dBFV psum: the P residues of c0 / c1 summed by launch_dbfv_pairsum): 3L + K blocks per item, every
     // component of the ciphertext primes, the third only of the auxiliary primes
     const int per = p2only ? 3 * L + K : 3 * NP;
+    // groups of 3 keep each (item, prime)'s components together only while every item's blocks are a
+    // multiple of 3; p2only's 3L + K is not (cfg5: 17), so there a whole item is one group
+    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
     const long item = p / per;
     const int rem = (int)(p - item * per);
     const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);
@@ -785,7 +806,11 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         return ASM ? mulmod_near60(a, b, dq) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
     };
     auto load = [&](const u64* src, u64 (&v)[16]) {
-        if constexpr (ASM) {
+        if constexpr (PROBE == 1) {
+            const u64 h = (u64)(src - op.a) ^ ((u64)tid << 40);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = ((h + k) * 0x9E3779B97F4A7C15ull) & ((1ull << 59) - 1);
+        } else if constexpr (ASM) {
             load_rows16<N>(v, src, tid);
         } else {
             const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
@@ -838,6 +863,9 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
+    if constexpr (PROBE == 1) {
+        if (remap != -7) return;   // never stored; the compiler cannot drop the work
+    }
     u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
@@ -857,8 +885,9 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const int NP = L + K;
-    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, 3) : (long)blockIdx.x;
     const int per = p2only ? 3 * L + K : 3 * NP;
+    // p2only: a whole item per group (see ntt_inv_tensor_kernel)
+    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
     const long item = p / per;
     const int rem = (int)(p - item * per);
     const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);

@@ -115,6 +115,11 @@ def polymul(out):
 
 
 def main():
+    # torch's HIP runtime first, as in the pytest parent and the bench: both the library and torch's
+    # bundled libamdhip64 carry the soname libamdhip64.so.7, and the process keeps whichever loads
+    # first (with the library first, torch.cuda found no GPU on a round-4 box)
+    import torch
+    torch.cuda.init()
     out = {}
     for g in (sys.argv[1:] or GROUPS):
         globals()[g](out)
