@@ -293,6 +293,14 @@ struct exacto_ctx {
     size_t ext_a_cap = 0, ext_b_cap = 0;
     u64* chain_buf = nullptr;  // dBFV chain ping-pong buffers
     size_t chain_bytes = 0;
+    // dBFV chain, psum path: each step's relinearised limbs also in the coefficient domain (they are
+    // there before the final forward NTT), so the next step's extension lifts them directly instead
+    // of inverse-transforming its NTT-domain input (dbfv_mul_group, exacto_dbfv_mul_chain_dev)
+    u64* chain_coef = nullptr;
+    size_t chain_coef_bytes = 0;
+    u64* coef_out = nullptr;        // set by the chain: where this step's coefficient form goes
+    const u64* coef_in = nullptr;   // set by the chain: the coefficient form of this step's `a`
+    bool coef_written = false;      // reported back: coef_out holds this step's results
     u64* dec_buf = nullptr;    // decryption phase [B][L][n]
     size_t dec_bytes = 0;
     u64* dig_buf = nullptr;    // dBFV decrypted digits [B][d][n]
@@ -366,11 +374,13 @@ static hipError_t dev_alloc(void** p, size_t bytes) {
     return e;
 }
 
-// Device -> device copies of the library, as a kernel (every size here is whole u64 words).  The
-// bootstrap copied its input into a re-used pool block with an asynchronous runtime copy, and the
-// next kernel sometimes read the block's previous contents (the C++ test's bootstrap of 1 came back
-// as the bootstrap of 0, DESIGN.md §6 "Fixed"); a kernel's writes reach the next kernel on the
-// stream like any kernel output.  Device fills likewise (launch_fill_u32).
+// Device -> device copies of the library, as a kernel (every size here is whole u64 words); device
+// fills likewise (launch_fill_u32).  Round 3 replaced hipMemcpyAsync / hipMemsetAsync with these
+// while chasing an intermittent stale bootstrap result; round 4 measured that the runtime's own
+// device-to-device copy is a blit kernel on the same queue (__amd_rocclr_copyBuffer) and never read
+// stale in 180k replays of the bootstrap's sequence (tools/d2d_repro.cpp), so the change is not a
+// fix of a runtime fault.  It stays: every device-side operation of the library is a
+// kernel of its own, one code path, visible by name in kernel traces.
 static hipError_t dev_copy(void* dst, const void* src, size_t bytes, hipStream_t s) {
     launch_copy_u64(static_cast<u64*>(dst), static_cast<const u64*>(src), (long)(bytes / 8), s);
     return hipGetLastError();
@@ -651,10 +661,25 @@ static int build_tables(exacto_ctx* c) {
     for (int t = 0; t < NP; ++t) C.hq[t] = H.mod(c->primes[t]);
     if (c->path == EXACTO_PATH_HPS) {
         const u64 q = qv[0];
-        for (int a = 0; a < K && a < 2; ++a) C.hps_qinv[a] = invmod_h(q % pv[a], pv[a]);
+        for (int a = 0; a < K && a < 2; ++a) {
+            C.hps_qinv[a] = invmod_h(q % pv[a], pv[a]);
+            C.hps_qinv_s[a] = shoup_h(C.hps_qinv[a], pv[a]);
+        }
+        if (c->plain < q) C.hps_pc = (u64)(((u128)c->plain << 64) / q);
         if (K == 2) {
             C.hps_p1_inv_p0 = invmod_h(pv[1] % pv[0], pv[0]);
             C.hps_p0_inv_p1 = invmod_h(pv[0] % pv[1], pv[1]);
+            set_shoup(C.hps_t_w[0], C.hps_t_ws[0], mulmod_h(C.hps_qinv[0], C.hps_p1_inv_p0, pv[0]), pv[0]);
+            set_shoup(C.hps_t_w[1], C.hps_t_ws[1], mulmod_h(C.hps_qinv[1], C.hps_p0_inv_p1, pv[1]), pv[1]);
+            set_shoup(C.hps_pq_w[0], C.hps_pq_ws[0], pv[1] % q, q);
+            set_shoup(C.hps_pq_w[1], C.hps_pq_ws[1], pv[0] % q, q);
+            const u128 P = (u128)pv[0] * pv[1];
+            const u64 Pq = (u64)(P % q);
+            C.hps_kPq[0] = 0;
+            C.hps_kPq[1] = Pq;
+            C.hps_kPq[2] = (u64)(((u128)Pq * 2) % q);
+            C.hps_P[0] = (u64)P; C.hps_P[1] = (u64)(P >> 64);
+            C.hps_halfP[0] = (u64)(P >> 1); C.hps_halfP[1] = (u64)(P >> 65);
         }
     } else {
         for (int a = 0; a < K; ++a)
@@ -848,6 +873,10 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_DBFV_GROUP_MB")) c->dbfv_group_bytes = (size_t)std::max(1, atoi(e)) << 20;
     if (const char* e = getenv("EXACTO_NTT_ASM")) c->ntt_asm = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_NTT_ASM_INV")) c->ntt_asm_inv = atoi(e) != 0;
+    // products per pipeline chunk: 512 at cfg3's n (L + K) = 4096 x 7, more where a product is smaller,
+    // so that every chunk's launches (and workspace, ~1.4 GB) stay about the same size (compact_bfv,
+    // n = 1024 with L + K = 2: 7168 products per chunk instead of launches of a few blocks per CU)
+    c->chunk = (size_t)std::min<long>(8192, std::max<long>(512, 512L * 4096 * 7 / ((long)n * (c->L + c->K)) / 64 * 64));
     if (const char* e = getenv("EXACTO_DUAL_STREAM")) c->dual = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_LANES")) c->lanes = std::max(1, std::min(EXACTO_MAX_LANES, atoi(e)));
     if (const char* e = getenv("EXACTO_SHARE_EXT")) c->share_ext = atoi(e) != 0;
@@ -871,7 +900,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
-    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->dec_buf); free_dev(c->dig_buf);
+    free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->chain_coef); free_dev(c->dec_buf); free_dev(c->dig_buf);
     for (LaneSet& l : c->xl) {
         if (l.stream) { (void)hipStreamSynchronize(l.stream); (void)hipStreamDestroy(l.stream); }
         if (l.join) (void)hipEventDestroy(l.join);
@@ -1787,25 +1816,30 @@ static int dbfv_params_check(size_t d, uint64_t base, uint64_t plain) {
 // inverse NTT, its exact (or HPS) extension to the auxiliary primes and their forward NTT
 // (pipeline steps 1-3) are computed here once per ciphertext, ext = [ct][2][K][n], instead of
 // once per product.  The results are identical: steps 1-3 depend on the ciphertext alone.
-static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext) {
+// coef: the same ciphertexts already in the coefficient domain (a dBFV chain's previous step,
+// [ct][2][L][n]), or nullptr: the inverse NTT is skipped and the lift reads them directly.
+static int extend_cts(exacto_ctx* c, const u64* cts, size_t ncts, u64* ext, const u64* coef = nullptr) {
     const int n = c->n, L = c->L, K = c->K;
     const long Ln2 = 2L * L * n, Kn2 = 2L * K * n;
     if (int e = ensure_workspace(c, std::min<size_t>(c->chunk, (ncts + 1) / 2))) return e;
-    const size_t G = 2 * c->ws_items;  // ciphertexts per pass: coefQ holds 4 polys x L per item
+    const size_t G = coef ? ncts : 2 * c->ws_items;  // ciphertexts per pass: coefQ holds 4 polys x L per item
     for (size_t g0 = 0; g0 < ncts; g0 += G) {
         const long cnt = (long)std::min(G, ncts - g0);
-        NttBatch nb{};
-        nb.src = cts + g0 * Ln2; nb.src_off = nullptr; nb.src_item_stride = Ln2;
-        nb.dst = c->ws_coefQ; nb.dst_item_stride = Ln2;
-        nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
-        if (int e = run_ntt(c, nb, cnt * 2 * L, true)) return e;
+        const u64* cq = coef ? coef + g0 * Ln2 : c->ws_coefQ;
+        if (!coef) {
+            NttBatch nb{};
+            nb.src = cts + g0 * Ln2; nb.src_off = nullptr; nb.src_item_stride = Ln2;
+            nb.dst = c->ws_coefQ; nb.dst_item_stride = Ln2;
+            nb.ppi = 2 * L; nb.prime_base = 0; nb.period = L;
+            if (int e = run_ntt(c, nb, cnt * 2 * L, true)) return e;
+        }
         u64* eo = ext + g0 * Kn2;
         if (c->path == EXACTO_PATH_HPS) {
             ProfScope pl(c, PK_HPS_EXT, 2ull * cnt, 8.0 * (1 + K) * n * 2.0 * cnt);
-            launch_hps_extend(c->ws_coefQ, eo, 2 * cnt, n, c->d_primes, K, c->stream);
+            launch_hps_extend(cq, eo, 2 * cnt, n, c->d_primes, K, c->stream);
         } else {
             ProfScope pl(c, PK_LIFT, 2ull * cnt, 8.0 * (L + K) * n * 2.0 * cnt);
-            launch_exact_lift(c->ws_coefQ, eo, 2 * cnt, n, c->d_crt, c->d_primes, L, K,
+            launch_exact_lift(cq, eo, 2 * cnt, n, c->d_crt, c->d_primes, L, K,
                               crt_mode(c), c->stream);
         }
         CHECK_LAUNCH();
@@ -1834,7 +1868,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     if (c->share_ext && c->K > 0 && !c->deferred_code) {
         const size_t nct = B * d, bytes = nct * 2 * c->K * poly_bytes(c);
         if (grow(&c->ext_a, &c->ext_a_cap, bytes)) return EXACTO_ERR_HIP;
-        if (int e = extend_cts(c, a, nct, c->ext_a)) return e;
+        if (int e = extend_cts(c, a, nct, c->ext_a, c->coef_in)) return e;
         if (!b_extended) {
             if (grow(&c->ext_b, &c->ext_b_cap, bytes)) return EXACTO_ERR_HIP;
             if (int e = extend_cts(c, b, nct, c->ext_b)) return e;
@@ -1904,13 +1938,17 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     for (u64 q : c->primes) near60 &= q < (1ull << 60) && q > (1ull << 60) - (1ull << 24);
     const bool psum = sum_ks && c->psum_env && m <= c->psum_max && op.ea != nullptr && near60 &&
                       (c->logn == 12 || c->logn == 13) && exact_scale_sp_ok(c->L, c->K, crt_mode(c));
+    // chain (psum): the limbs are formed in the coefficient domain in coef_out and forward-transformed
+    // from there into out, so coef_out keeps them for the next step's extension
+    u64* cf = psum && c->coef_out ? c->coef_out : out;
+    c->coef_written = false;
     if (psum) {
         c->psum.on = true;
         c->psum.d = (int)dout;
         c->psum.npairs = npairs;
         c->psum.term_start = c->d_term_start;
         c->psum.terms = c->d_terms;
-        c->psum.out = out;
+        c->psum.out = cf;
     }
     bool coef = false;
     const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
@@ -1945,7 +1983,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         }
         {
             ProfScope pc(c, PK_KS_CRT, (u64)Bd * 2 * c->L, nn * Bd * 2 * c->L * (4.0 * S + 16.0));
-            ks32_crt(c->d_uk, out, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
+            ks32_crt(c->d_uk, cf, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
         }
         CHECK_LAUNCH();
     }
@@ -1962,9 +2000,12 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         db.src16_item_stride = (long)gu * c->n;
         if (int e = run_ntt(c, db, (long)Bd * gu * c->L, false)) return e;
     }
-    if (coef)
-        if (int e = run_ntt(c, contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n), (long)B * dout * 2 * c->L, false))
-            return e;
+    if (coef) {
+        NttBatch ob = contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n);
+        ob.src = cf;   // (== out unless a chain keeps the coefficient form)
+        if (int e = run_ntt(c, ob, (long)B * dout * 2 * c->L, false)) return e;
+        c->coef_written = cf != out;
+    }
     if (hps_sum) {
         ProfScope pm(c, PK_RELIN_MAC, (u64)Bd, 8.0 * c->n * c->L * Bd * (4.0 + gu));
         launch_relin_mac(out, 2L * c->L * c->n, c->d_hdig, c->d_rlk, c->d_rlk_s, (int)gu, out, 2L * c->L * c->n,
@@ -1997,6 +2038,9 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
                             4 * n * d * 2 * L * S;                          // key-switch sums
     const size_t Bg = std::max<size_t>(1, budget / std::max<size_t>(per_item, 1));
     if (B <= Bg) return dbfv_mul_group(c, d, base, plain, a, b, out, B, b_extended, limbs);
+    // several groups: no coefficient-form carry between chain steps (its buffers are whole-batch)
+    c->coef_in = nullptr;
+    c->coef_out = nullptr;
     const size_t ctw = 2 * L * n;
     for (size_t g0 = 0; g0 < B; g0 += Bg) {
         const size_t cnt = std::min(Bg, B - g0);
@@ -2160,14 +2204,30 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     }
     if (int e = dbfv_params_check(d, base, plain)) return e;
     if (B == 0) return 0;
+    // the coefficient form of each step's result (psum path, one item group) goes to chain_coef, and
+    // the next step lifts it directly: one batched inverse NTT of its input less per step
+    const bool carry = depth > 1 && c->share_ext && c->K > 0;
+    if (carry) {
+        size_t cap = c->chain_coef_bytes;
+        if (grow(&c->chain_coef, &cap, 2 * bytes)) return EXACTO_ERR_HIP;
+        c->chain_coef_bytes = cap;
+    }
     const uint64_t* src = x;
-    for (size_t k = 0; k < depth; ++k) {
+    const u64* src_coef = nullptr;
+    int rc = 0;
+    for (size_t k = 0; k < depth && rc == 0; ++k) {
         uint64_t* dst = (k + 1 == depth) ? out : c->chain_buf + (k % 2) * (bytes / sizeof(u64));
+        c->coef_in = src_coef;
+        c->coef_out = carry && k + 1 < depth ? c->chain_coef + (k % 2) * (bytes / sizeof(u64)) : nullptr;
         // y's extensions are computed by the first step and reused by the others
-        if (int e = dbfv_mul_core(c, d, base, plain, src, y, dst, B, k > 0)) return e;
+        rc = dbfv_mul_core(c, d, base, plain, src, y, dst, B, k > 0);
+        src_coef = c->coef_out && c->coef_written ? c->coef_out : nullptr;
         src = dst;
     }
-    return 0;
+    c->coef_in = nullptr;
+    c->coef_out = nullptr;
+    c->coef_written = false;
+    return rc;
 }
 
 extern "C" int exacto_dbfv_mul_chain(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* x,
@@ -2979,8 +3039,7 @@ static int boot_pair_check(exacto_ctx* o, exacto_ctx* b) {
 // boot context's): o's stream is rebound to b's for the call, so that every hand-off between the
 // contexts (the inputs uploaded on b's stream and copied on o's, the modulus-switched rows written on
 // o's and read on b's) is ordered by the runtime instead of by host-side synchronisation alone.
-// (Made while chasing an intermittent failure of the C++ test's bootstrap case, which it did not
-// remove; the cause was the runtime copy into a re-used block, see dev_copy and DESIGN.md §6.)
+// (Made while chasing an intermittent failure of the C++ test's bootstrap case)
 struct StreamRebind {
     exacto_ctx* c;
     hipStream_t saved;

@@ -63,6 +63,13 @@ struct CrtTables {
     // HPS (single q, 1 or 2 aux primes), eval.rs:257-413
     u64 hps_qinv[2];        // q^-1 mod p_j
     u64 hps_p1_inv_p0, hps_p0_inv_p1;
+    // division-free HPS scale (hps_scale_kernel FAST): every product by a constant as a Shoup product
+    u64 hps_pc;             // floor(p 2^64 / q): the quotient estimate of round(p a / q), and p's Shoup companion mod q
+    u64 hps_qinv_s[2];      // Shoup companions of hps_qinv (mod p_j)
+    u64 hps_t_w[2], hps_t_ws[2];   // K = 2: q^-1 p1^-1 mod p0, q^-1 p0^-1 mod p1 (m's CRT coefficients, folded)
+    u64 hps_pq_w[2], hps_pq_ws[2]; // K = 2: p1 mod q, p0 mod q
+    u64 hps_kPq[3];         // K = 2: k P mod q, k = 0, 1, 2 (P = p0 p1)
+    u64 hps_P[2], hps_halfP[2];    // K = 2: P and floor(P / 2) as (lo, hi)
 };
 
 // lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)

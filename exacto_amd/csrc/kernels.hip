@@ -889,24 +889,23 @@ void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d,
 
 // ---------------------------------------------------------------- HPS scale (eval.rs:257-413)
 
-// HPS round(p a_c / q) + p m (mod q) without i128 division (FAST: q > 2^32 and p < min(q, 2^32)).
+// HPS round(p a_c / q) + p m (mod q) without any division (FAST: q > 2^32 and p < min(q, 2^32)).
 // Every step is exact integer arithmetic, so the result equals the literal form below bit for bit:
-//   * the rounding quotient x / q, x = p |a_c| + floor(q/2) < 2^95, is at most p/2 + 1 < 2^31: a
-//     double estimate is off by at most one and is corrected against the exact 128-bit remainder;
-//   * the m-recovery products are canonical residues, so the Barrett mul_mod equals ref_mod_mul's
-//     exact u128 % (and its Barrett branch for moduli <= 2^32, exact below m^2);
-//   * (a + b) mod q for the integer sum round + p m is formed from each part mod q (a ring map):
-//     m mod q with |m| < 2^111 splits as hi 2^64 + lo, both reduced.
-__device__ __forceinline__ u64 hps_round_mod(u64 a, u64 q, u64 p, const PrimeConst& Pq) {
+//   * est = floor((p |a_c| + floor(q/2)) / q) < p/2 + 1 < 2^31: with pc = floor(p 2^64 / q),
+//     hi64(|a_c| pc) is floor(p |a_c| / q) or one less (|a_c| < 2^61), so est is that plus 0, 1 or 2,
+//     decided on the remainder x - e q, which lies in [0, 3q) and so is exact in 64-bit wrapping
+//     arithmetic (q < 2^62);
+//   * every product by a constant is a Shoup product (the unique residue, as ref_mod_mul's u128 %);
+//   * (a + b) mod q for the integer sum round + p m is formed from each part mod q (a ring map).
+__device__ __forceinline__ u64 hps_round_mod(u64 a, u64 q, u64 p, u64 pc) {
     const bool neg = a > q / 2;
     const u64 mag = neg ? q - a : a;                      // |a_c|
-    const u128 x = (u128)p * mag + (q / 2);
-    u64 est = (u64)((double)x / (double)q);
-    i128 r = (i128)x - (i128)((u128)est * q);
-    while (r < 0) { --est; r += q; }
-    while (r >= (i128)q) { ++est; r -= q; }
-    // round_pa_q = +/- est; mod q (est < 2^31 < q)
-    return (neg && est) ? q - est : est;
+    u64 e = mulhi64(mag, pc);
+    u64 r = p * mag + (q >> 1) - e * q;                   // exact: the true value is in [0, 3q)
+    if (r >= q) { ++e; r -= q; }
+    if (r >= q) ++e;
+    // round_pa_q = +/- e; mod q (e < 2^31 < q)
+    return (neg && e) ? q - e : e;
 }
 
 __device__ __forceinline__ u64 hps_ext_fast(u64 a, u64 q, const PrimeConst& P) {
@@ -946,39 +945,40 @@ hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, 
     u64 result;
     if (FAST) {
         const PrimeConst& Pq = primes[0];
-        const u64 rq = hps_round_mod(a, q, p, Pq);
+        const u64 rq = hps_round_mod(a, q, p, C->hps_pc);
         u64 mq;   // m mod q, Euclidean
         if (K == 1) {
             // eval.rs:301-332
             const PrimeConst& P1 = primes[1];
             const u64 bp = P1.q;
             const u64 diff = sub_mod(Tin[n], hps_ext_fast(a, q, P1), bp);
-            const u64 m_raw = mul_mod(diff, C->hps_qinv[0], P1);
+            const u64 m_raw = shoup_mul_red(diff, C->hps_qinv[0], C->hps_qinv_s[0], bp);
             const bool mneg = m_raw > bp / 2;
             const u64 mag = mneg ? bp - m_raw : m_raw;
             const u64 r = reduce64(mag, q, Pq.mu64);
             mq = (mneg && r) ? q - r : r;
         } else {
-            // eval.rs:349-404: m from its residues mod p0, p1 by CRT, centred mod P = p0 p1
-            const PrimeConst& P0 = primes[1];
-            const PrimeConst& P1 = primes[2];
-            const u64 p0 = P0.q, p1 = P1.q;
-            const u64 m0 = mul_mod(sub_mod(Tin[n], hps_ext_fast(a, q, P0), p0), C->hps_qinv[0], P0);
-            const u64 m1 = mul_mod(sub_mod(Tin[2L * n], hps_ext_fast(a, q, P1), p1), C->hps_qinv[1], P1);
-            const u64 t0 = mul_mod(m0, C->hps_p1_inv_p0, P0);
-            const u64 t1 = mul_mod(m1, C->hps_p0_inv_p1, P1);
-            const u128 bigp = (u128)p0 * p1;
+            // eval.rs:349-404: m from its residues mod p0, p1 by CRT, centred mod P = p0 p1.
+            // t_j = (T_j - a mod p_j) q^-1 p_{1-j}^-1 mod p_j (one folded constant each); the CRT sum
+            // t0 p1 + t1 p0 < 2P decides how many P to subtract (k = 0, 1, 2: the Euclidean residue,
+            // then the centring), and m mod q = t0 (p1 mod q) + t1 (p0 mod q) - k (P mod q).
+            const u64 p0 = primes[1].q, p1 = primes[2].q;
+            const u64 t0 = shoup_mul_red(sub_mod(Tin[n], hps_ext_fast(a, q, primes[1]), p0), C->hps_t_w[0],
+                                         C->hps_t_ws[0], p0);
+            const u64 t1 = shoup_mul_red(sub_mod(Tin[2L * n], hps_ext_fast(a, q, primes[2]), p1), C->hps_t_w[1],
+                                         C->hps_t_ws[1], p1);
+            const u128 bigp = ((u128)C->hps_P[1] << 64) | C->hps_P[0];
+            const u128 halfp = ((u128)C->hps_halfP[1] << 64) | C->hps_halfP[0];
             u128 mc = (u128)t0 * p1 + (u128)t1 * p0;           // < 2 P
-            if (mc >= bigp) mc -= bigp;
-            const bool mneg = mc > bigp / 2;
-            const u128 mag = mneg ? bigp - mc : mc;
-            // mag mod q = (hi (2^64 mod q) + lo) mod q
-            const u64 c64 = reduce64((u64)0 - q, q, Pq.mu64);
-            const u64 hi = reduce64((u64)(mag >> 64), q, Pq.mu64);
-            const u64 r = add_mod(mul_mod(hi, c64, Pq), reduce64((u64)mag, q, Pq.mu64), q);
-            mq = (mneg && r) ? q - r : r;
+            int k = 0;
+            if (mc >= bigp) { mc -= bigp; k = 1; }
+            if (mc > halfp) ++k;
+            const u64 s = add_mod(shoup_mul_red(t0, C->hps_pq_w[0], C->hps_pq_ws[0], q),
+                                  shoup_mul_red(t1, C->hps_pq_w[1], C->hps_pq_ws[1], q), q);
+            mq = sub_mod(s, C->hps_kPq[k], q);
         }
-        result = add_mod(rq, mul_mod(p, mq, Pq), q);
+        // p < q: pc = floor(p 2^64 / q) is p's Shoup companion mod q
+        result = add_mod(rq, shoup_mul_red(mq, p, C->hps_pc, q), q);
     } else {
         const i128 q128 = (i128)q;
         const u64 half_q = q / 2;

@@ -621,11 +621,28 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 #undef PIN_OUT
 }
 
+// Probe mode 3 (tools/ntt_probe.hip): the first generation of resident blocks (`slots`, one per CU
+// per step of blockIdx / 256) start staggered by `ph` of PHASES block lifetimes, so that loads and
+// arithmetic of co-resident blocks stop running in phase; later blocks inherit their slot's offset.
+template <int PHASES>
+__device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
+    if ((int)blockIdx.x >= slots) return;
+    const int ph = (int)(blockIdx.x / 256) % PHASES;
+    for (int i = 0; i < ph * sleeps_per_phase; ++i) __builtin_amdgcn_s_sleep(16);   // ~1024 cycles each
+}
+#ifndef EXACTO_PROBE_SLEEPS_FWD
+#define EXACTO_PROBE_SLEEPS_FWD 11      // a quarter of a 4096-point forward block's ~21 us lifetime
+#endif
+#ifndef EXACTO_PROBE_SLEEPS_TENSOR
+#define EXACTO_PROBE_SLEEPS_TENSOR 14   // a third of a cfg3 tensor block's ~21 us lifetime
+#endif
+
 // Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds, exchanges and
 // coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic
 // canonical inputs, no global loads, stores skipped at run time), 2 = memory only (loads, the
-// same LDS exchanges and stores, no butterflies and no twiddle loads).
+// same LDS exchanges and stores, no butterflies and no twiddle loads), 3 = the product kernel with
+// its first generation staggered (probe_stagger).
 template <int LOGN, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
@@ -639,6 +656,7 @@ ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
     const u64 q = P.q;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    if constexpr (PROBE == 3) probe_stagger<4>(1024, EXACTO_PROBE_SLEEPS_FWD);
     EXACTO_PIN_DECL
     if constexpr (PROBE == 1) {
         const u64 h = ((u64)p << 20) ^ (u64)tid;
@@ -759,8 +777,24 @@ __device__ __forceinline__ long xcd_group_remap(long b, long total, int G) {
     return ((slot / G) * 8 + x) * G + slot % G;
 }
 
+// Block -> (prime t, component c) within one item's blocks (`rem`): the ciphertext primes' three
+// components back to back (c1 re-reads c0's and c2's operands: adjacent blocks of one XCD group load
+// them at the same time, so the L2 serves the repeats), then p2only's auxiliary-prime c2 blocks.
+// (Round 4: placing the c1 blocks after all c0 / c2 blocks of the item instead raised the cfg5
+// tensor's reads from 1.30x to 1.62x algorithmic: by then the operands had left the 4 MB L2.)
+__device__ __forceinline__ void tensor_unit(int rem, int L, int p2only, int& t, int& c) {
+    if (!p2only || rem < 3 * L) {
+        t = rem / 3;
+        c = rem - 3 * t;
+    } else {
+        t = L + (rem - 3 * L);
+        c = 2;
+    }
+}
+
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic operands
-// instead of the loads, stores skipped at run time).
+// instead of the loads, stores skipped at run time), 2 = no transform (the loads, the pointwise
+// products and the stores), 3 = the product kernel with its first generation staggered.
 template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
@@ -772,6 +806,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     __shared__ u64 lds[N];
     const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
+    if constexpr (PROBE == 3) probe_stagger<3>(768, EXACTO_PROBE_SLEEPS_TENSOR);
     const int NP = L + K;
     // the three components of one (item, prime) read overlapping inputs (c1 reads c0's and c2's):
     // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
@@ -783,8 +818,8 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
     const long item = p / per;
     const int rem = (int)(p - item * per);
-    const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);
-    const int c = (!p2only || rem < 3 * L) ? rem - t * 3 : 2;
+    int t, c;
+    tensor_unit(rem, L, p2only, t, c);
     const PrimeConst& P = primes[t];
     const u64 *A0, *A1, *B0, *B1;
     if (t < L) {
@@ -857,7 +892,9 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
             }
         }
     }
-    if constexpr (ASM) {
+    if constexpr (PROBE == 2) {
+        // no transform: the products are stored as they are
+    } else if constexpr (ASM) {
         const AsmK AK = make_asmk_inv(P);
         inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
@@ -890,8 +927,8 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
     const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
     const long item = p / per;
     const int rem = (int)(p - item * per);
-    const int t = (!p2only || rem < 3 * L) ? rem / 3 : L + (rem - 3 * L);
-    const int c = (!p2only || rem < 3 * L) ? rem - t * 3 : 2;
+    int t, c;
+    tensor_unit(rem, L, p2only, t, c);
     const PrimeConst& P = primes[t];
     const u64 *A0, *A1, *B0, *B1;
     if (t < L) {

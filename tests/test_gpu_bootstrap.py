@@ -177,3 +177,51 @@ def test_errors(gpu_available):
     with pytest.raises(ExactoError) as e:
         _ffi.bfv_bootstrap_raw(orig, boot, ct3, np.zeros((2, 1, 16), dtype=np.uint64), [1], qp, [], np.zeros((0,)))
     assert "bootstrap requires degree-1 ciphertext" in str(e.value)
+
+
+def test_bootstrap_zero_then_one_reuses_scratch(gpu_available, monkeypatch):
+    """Regression for round 3's stale bootstrap result: the trivial ciphertexts of 0
+    and then of 1, as two calls on the same two contexts, so the second call gets the first call's
+    pool blocks and io buffer back; EXACTO_DEBUG_SCRATCH=1 (read at context creation) fills every
+    block with 0xFF when it is handed out, so a read of anything the second call did not write
+    itself shows.  Each call is bit-exact against the oracle (bfv_host.rs:131-205)."""
+    monkeypatch.setenv("EXACTO_DEBUG_SCRATCH", "1")
+    orig_p, boot_p, qp = bootstrap_test_params()
+    orig, boot = HipContext.from_params(orig_p), HipContext.from_params(boot_p)
+    rng = np.random.default_rng(67)
+    n = 16
+    bq = boot_p.ct_basis.moduli
+    bsk = uniform_residues(rng, (2,), bq, n)
+    rlk = uniform_residues(rng, (3, 2), bq, n)
+    boot.load_relin_key(rlk)
+    els = ob.required_trace_elements(n)
+    gks = uniform_residues(rng, (len(els), 2, 2), bq, n)
+    rpoly = ob.compute_rounding_poly(5, qp, 29)
+    keys = {k: obfv.GaloisKey(np_to_rlk(gks[e], boot_p).keys, k, boot_p) for e, k in enumerate(els)}
+    orlk = np_to_rlk(rlk, boot_p)
+    outs = []
+    for v in (0, 1, 0, 1):
+        ct = orig.trivial_encrypt([v])
+        got = _ffi.bfv_bootstrap_raw(orig, boot, ct, bsk, rpoly, qp, els, gks)
+        want = ob.bfv_bootstrap(np_to_ct(ct[0], orig_p), np_to_ct(bsk, boot_p), orlk, keys, rpoly, qp)
+        assert np.array_equal(got[0], ct_to_np(want)), v
+        outs.append(got[0])
+    assert not np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("reps", [2])
+def test_cpp_bootstrap_reps_debug_scratch(gpu_available, reps):
+    """The C++ host API's bootstrap sequence (trivial 0..4 through include/exacto.hpp, the case that
+    failed in round 3) repeated in one process with EXACTO_DEBUG_SCRATCH=1: every output decrypts
+    to its input and equals the first repetition's (tests/cpp/test_api.cpp boot_repro)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    binary = os.path.join(root, "build", "test_api")
+    if not os.path.exists(binary):
+        from test_cpp_api import compile_test_api
+        binary = compile_test_api()
+    env = dict(os.environ, EXACTO_DEBUG_SCRATCH="1")
+    r = subprocess.run([binary, "--boot-reps", str(reps)], capture_output=True, text=True, timeout=300, env=env)
+    print(r.stdout)
+    assert r.returncode == 0 and f"boot_repro reps={reps} wrong=0 differ=0" in r.stdout, r.stdout + r.stderr

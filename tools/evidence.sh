@@ -33,4 +33,7 @@ V1="SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT
 EXACTO_DUAL_STREAM=0 timeout -s KILL 300 rocprofv3 --pmc $V1 -d $E/valu -o run --output-format csv -- $P > $E/valu.log 2>&1
 python3 $R/tools/pmc_traffic.py $E > $E/traffic.json
 python3 $R/tools/valu_report.py "rocprofv3 --pmc $V1 -- bench.py --config $CFG --steps 2 --warmup 1 --reps 1 (one lane)" $E/valu > $E/valu.json
+# keep what comes back under gpurun's 64 MiB: the per-dispatch CSVs are summarised above
+find $E -name "*kernel_trace.csv" -size +2M -delete
+find $E -name "*counter_collection.csv" -size +2M -exec gzip -f {} \;
 echo done

@@ -98,18 +98,26 @@ int main(int argc, char** argv) {
     const double f_full = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<LOGN, 0>), dim3(polys), dim3(256), 0, 0, nb, d_pc); });
     const double f_comp = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<LOGN, 1>), dim3(polys), dim3(256), 0, 0, nb, d_pc); });
     const double f_mem = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<LOGN, 2>), dim3(polys), dim3(256), 0, 0, nb, d_pc); });
+    const double f_stag = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<LOGN, 3>), dim3(polys), dim3(256), 0, 0, nb, d_pc); });
     const double t_full = timed([&] {
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 0>), dim3(tblocks), dim3(256), 0, 0, op, E, Tt, 3, 4, d_pc, 1, 0);
     });
     const double t_comp = timed([&] {
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 1>), dim3(tblocks), dim3(256), 0, 0, op, E, Tt, 3, 4, d_pc, 1, 0);
     });
+    const double t_mem = timed([&] {
+        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 2>), dim3(tblocks), dim3(256), 0, 0, op, E, Tt, 3, 4, d_pc, 1, 0);
+    });
+    const double t_stag = timed([&] {
+        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 3>), dim3(tblocks), dim3(256), 0, 0, op, E, Tt, 3, 4, d_pc, 1, 0);
+    });
     const double fbytes = 16.0 * N * polys, tbytes = 7.0 * 8 * N * items * NP;
     std::printf("{\"fwd_pin_polys\": %ld, \"fwd_full_us\": %.2f, \"fwd_compute_only_us\": %.2f, \"fwd_memory_only_us\": %.2f, "
-                "\"fwd_full_GBs\": %.1f, \"fwd_compute_over_full\": %.3f, "
+                "\"fwd_staggered_us\": %.2f, \"fwd_full_GBs\": %.1f, \"fwd_compute_over_full\": %.3f, "
                 "\"tensor12_blocks\": %ld, \"tensor_full_us\": %.2f, \"tensor_compute_only_us\": %.2f, "
+                "\"tensor_no_transform_us\": %.2f, \"tensor_staggered_us\": %.2f, "
                 "\"tensor_full_GBs\": %.1f, \"tensor_compute_over_full\": %.3f, \"reps\": %d}\n",
-                polys, f_full, f_comp, f_mem, fbytes / (f_full * 1e3), f_comp / f_full, tblocks, t_full, t_comp,
-                tbytes / (t_full * 1e3), t_comp / t_full, reps);
+                polys, f_full, f_comp, f_mem, f_stag, fbytes / (f_full * 1e3), f_comp / f_full, tblocks, t_full, t_comp,
+                t_mem, t_stag, tbytes / (t_full * 1e3), t_comp / t_full, reps);
     return 0;
 }

@@ -20,6 +20,9 @@ import os
 import sys
 
 
+GRID = {}   # (file, dispatch id) -> grid size in threads
+
+
 def per_dispatch(path, counter):
     """{kernel name: {dispatch id: value}} (counter summed over the dimensions rocprofv3 reports)."""
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -29,6 +32,7 @@ def per_dispatch(path, counter):
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")
             vals[name][(f, int(r["Dispatch_Id"]))] += float(r["Counter_Value"])
+            GRID[(f, int(r["Dispatch_Id"]))] = int(r.get("Grid_Size") or 0)
     return vals
 
 
@@ -51,12 +55,27 @@ if cf:
                           "write_factor_measured": known / (1024 * med(wk)) if wk else None}
 fetch = per_dispatch(os.path.join(out, "fetch"), "FETCH_SIZE")
 write = per_dispatch(os.path.join(out, "write"), "WRITE_SIZE")
+# The passes run the bench command, whose latency block adds batch-1 calls (small grids) to the
+# batches the roofline is about: the averages are per grid size, and the kernel's top-level figures
+# are those of its LARGEST grid (a full batch, the launches bench.py times).
+res["note"] = "top-level figures per kernel: its dispatches of the largest grid size; by_grid: all sizes"
 for name in sorted(set(fetch) | set(write)):
-    rd = [2 * 1024 * v for v in fetch.get(name, {}).values()]
-    wr = [1024 * v for v in write.get(name, {}).values()]
-    if not rd or not wr:
+    fd, wd = fetch.get(name, {}), write.get(name, {})
+    if not fd or not wd:
         continue
-    res["kernels"][name] = {"dispatches": len(rd), "read_bytes_avg": sum(rd) / len(rd),
-                            "write_bytes_avg": sum(wr) / len(wr),
-                            "traffic_bytes_avg": sum(rd) / len(rd) + sum(wr) / len(wr)}
+    by = {}
+    for grid in sorted({GRID[k] for k in fd} | {GRID[k] for k in wd}):
+        rd = [2 * 1024 * v for k, v in fd.items() if GRID[k] == grid]
+        wr = [1024 * v for k, v in wd.items() if GRID[k] == grid]
+        if rd and wr:
+            by[grid] = {"dispatches": len(rd), "read_bytes_avg": sum(rd) / len(rd),
+                        "write_bytes_avg": sum(wr) / len(wr),
+                        "traffic_bytes_avg": sum(rd) / len(rd) + sum(wr) / len(wr)}
+    if not by:
+        continue
+    top = dict(by[max(by)])
+    top["grid_threads"] = max(by)
+    if len(by) > 1:
+        top["by_grid"] = {str(g): v for g, v in by.items()}
+    res["kernels"][name] = top
 print(json.dumps(res, indent=1))
