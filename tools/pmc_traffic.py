@@ -15,6 +15,7 @@ usage: python3 tools/pmc_traffic.py <dir with fetch/ write/ [cal_fetch/ cal_writ
 import collections
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -26,8 +27,8 @@ GRID = {}   # (file, dispatch id) -> grid size in threads
 def per_dispatch(path, counter):
     """{kernel name: {dispatch id: value}} (counter summed over the dimensions rocprofv3 reports)."""
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
-    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv*"), recursive=True):
+        for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")

@@ -15,25 +15,35 @@ usage: python3 tools/valu_report.py "<source description>" <pmc dir> [<pmc dir> 
 import collections
 import csv
 import glob
+import gzip
 import json
 import sys
 
 src = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
+grids = {}
 for d in sys.argv[2:]:
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
+    for f in glob.glob(f"{d}/**/*counter_collection.csv*", recursive=True):
+        op = gzip.open(f, "rt") if f.endswith(".gz") else open(f)
+        for r in csv.DictReader(op):
             k = (d, int(r["Dispatch_Id"]))
             vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
             names[k] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            grids[k] = int(r.get("Grid_Size") or 0)
+# the bench command's latency block adds batch-1 dispatches (small grids): keep each kernel's
+# dispatches of its largest grid size (the full batches the roofline is about)
+top = {}
+for k, nm in names.items():
+    top[nm] = max(top.get(nm, 0), grids[k])
+vals = {k: v for k, v in vals.items() if grids[k] == top[names[k]]}
 # the passes are separate runs of the same program: dispatch ids line up per kernel name in order
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for k, v in sorted(vals.items()):
     for c, x in v.items():
         agg[names[k]][c].append(x)
 out = {"source": src,
-       "note": "per-dispatch averages; SQ_* counts are chip totals (cycle counters in quad-cycles); "
+       "note": "per-dispatch averages over each kernel's largest-grid dispatches; SQ_* counts are chip totals (cycle counters in quad-cycles); "
                "GRBM_GUI_ACTIVE summed over 8 XCDs (divided back in gpu_cycles)",
        "kernels": {}}
 
