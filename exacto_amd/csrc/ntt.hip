@@ -794,7 +794,9 @@ __device__ __forceinline__ void tensor_unit(int rem, int L, int p2only, int& t, 
 
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic operands
 // instead of the loads, stores skipped at run time), 2 = no transform (the loads, the pointwise
-// products and the stores), 3 = the product kernel with its first generation staggered.
+// products and the stores), 3 = the product kernel with its first generation staggered.  (Round 4
+// also measured the next generation's operands prefetched into the L2 by scalar loads before or
+// after the transform: 296 -> 357 us, removed.)
 template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
@@ -821,20 +823,24 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     int t, c;
     tensor_unit(rem, L, p2only, t, c);
     const PrimeConst& P = primes[t];
+    // the four operand polynomials of (item, prime t)
+    auto operands = [&](long it, int tt, const u64*& A0, const u64*& A1, const u64*& B0, const u64*& B1) {
+        if (tt < L) {
+            const u64* A = op.a + (op.a_off ? (long)op.a_off[it] : it * op.a_stride);
+            const u64* B = op.b + (op.b_off ? (long)op.b_off[it] : it * op.b_stride);
+            A0 = A + (long)tt * N; A1 = A + (long)(L + tt) * N;
+            B0 = B + (long)tt * N; B1 = B + (long)(L + tt) * N;
+        } else if (op.ea) {  // shared per-ciphertext extensions (dBFV)
+            const u64* EA = op.ea + (long)op.ea_off[it] + (long)(tt - L) * N;
+            const u64* EB = op.eb + (long)op.eb_off[it] + (long)(tt - L) * N;
+            A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
+        } else {
+            const u64* E = extP + it * 4 * K * N + (long)(tt - L) * N;
+            A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
+        }
+    };
     const u64 *A0, *A1, *B0, *B1;
-    if (t < L) {
-        const u64* A = op.a + (op.a_off ? (long)op.a_off[item] : item * op.a_stride);
-        const u64* B = op.b + (op.b_off ? (long)op.b_off[item] : item * op.b_stride);
-        A0 = A + (long)t * N; A1 = A + (long)(L + t) * N;
-        B0 = B + (long)t * N; B1 = B + (long)(L + t) * N;
-    } else if (op.ea) {  // shared per-ciphertext extensions (dBFV)
-        const u64* EA = op.ea + (long)op.ea_off[item] + (long)(t - L) * N;
-        const u64* EB = op.eb + (long)op.eb_off[item] + (long)(t - L) * N;
-        A0 = EA; A1 = EA + (long)K * N; B0 = EB; B1 = EB + (long)K * N;
-    } else {
-        const u64* E = extP + item * 4 * K * N + (long)(t - L) * N;
-        A0 = E; A1 = E + (long)K * N; B0 = E + 2L * K * N; B1 = E + 3L * K * N;
-    }
+    operands(item, t, A0, A1, B0, B1);
     // ASM: every prime is 2^60 - d with d < 2^24 (launch_inv_tensor's caller checks)
     const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
     auto mulr = [&](u64 a, u64 b) {
