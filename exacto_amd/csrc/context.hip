@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -323,6 +325,7 @@ struct exacto_ctx {
     size_t terms_cap = 0;
     // per-call scratch: the context's own stream-ordered pool (Scratch)
     hipMemPool_t pool = nullptr;
+    bool own_pool = false;   // pool created for this context alone (EXACTO_SCRATCH_POOL=own)
     bool debug_scratch = false;
     size_t dbfv_group_bytes = (size_t)16384 << 20;  // dbfv_mul item groups (EXACTO_DBFV_GROUP_MB)
     // profiling
@@ -844,26 +847,42 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
     c->own_stream = true;
     {
-        // Per-call scratch (Scratch) comes from a stream-ordered pool of the context's own.  Its freed
-        // blocks stay mapped for reuse instead of going back to the driver at every synchronisation
-        // (release threshold 0 is the default): no map/unmap per call, and on this ROCm 7.2 stack
-        // blocks re-acquired after such a release gave wrong results at n = 16 (DESIGN.md §3,
-        // "Scratch"), which keeping them mapped avoids.  Only this pool is configured; the device's
-        // default pool keeps its settings for everything else in the process.
+        // Per-call scratch (Scratch) comes from a stream-ordered pool created by the library, one per
+        // device and shared by every context on it.  Its freed blocks stay mapped for reuse instead of
+        // going back to the driver at every synchronisation (release threshold 0 is the default), and
+        // the device's default pool keeps its settings for everything else in the process.
+        // One pool per context instead (EXACTO_SCRATCH_POOL=own, rounds 1-4) made the bootstrap's
+        // n = 16 scratch read back zeros written by no kernel of the library in 4 of 20 runs of the
+        // C++ API test, 13 of 20 with destroyed contexts' pools kept alive, and 0 of 20 with one pool
+        // for all contexts (tools/r4_bootab.sh).
         // EXACTO_SCRATCH_POOL=default: the device's default pool (threshold raised there), for A/B
         const char* pe = getenv("EXACTO_SCRATCH_POOL");
-        const bool own = !(pe && std::strcmp(pe, "default") == 0);
-        hipMemPoolProps props{};
-        props.allocType = hipMemAllocationTypePinned;
-        props.location.type = hipMemLocationTypeDevice;
-        props.location.id = device;
+        const std::string mode = pe ? pe : "shared";
         uint64_t thr = ~0ull;
-        if (own && hipMemPoolCreate(&c->pool, &props) == hipSuccess &&
-            hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess) {
-            // this pool only
-        } else {
-            if (c->pool) (void)hipMemPoolDestroy(c->pool);
-            c->pool = nullptr;   // Scratch uses the device's default pool, kept mapped the same way
+        auto make_pool = [&](hipMemPool_t* p) {
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = device;
+            if (hipMemPoolCreate(p, &props) != hipSuccess) return (*p = nullptr, false);
+            if (hipMemPoolSetAttribute(*p, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess) return true;
+            (void)hipMemPoolDestroy(*p);
+            return (*p = nullptr, false);
+        };
+        if (mode == "own") {
+            c->own_pool = make_pool(&c->pool);
+        } else if (mode != "default") {
+            static std::mutex mu;
+            static std::map<int, hipMemPool_t> shared;   // never destroyed: lives as long as the process
+            std::lock_guard<std::mutex> g(mu);
+            auto it = shared.find(device);
+            if (it == shared.end()) {
+                hipMemPool_t p = nullptr;
+                if (make_pool(&p)) it = shared.emplace(device, p).first;
+            }
+            if (it != shared.end()) c->pool = it->second;
+        }
+        if (!c->pool) {   // Scratch uses the device's default pool, kept mapped the same way
             hipMemPool_t dp;
             if (hipDeviceGetDefaultMemPool(&dp, device) == hipSuccess)
                 (void)hipMemPoolSetAttribute(dp, hipMemPoolAttrReleaseThreshold, &thr);
@@ -898,6 +917,9 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    // EXACTO_LEAK_CTX=1 (diagnostic of DESIGN.md §3): keep every allocation of a destroyed context
+    static const bool leak = [] { const char* e = getenv("EXACTO_LEAK_CTX"); return e && e[0] == '1'; }();
+    if (leak) return;
     for (auto& r : c->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
     free_dev(c->d_primes); free_dev(c->d_tw); free_dev(c->d_crt); free_dev(c->d_scal); free_dev(c->d_rlk); free_dev(c->d_rlk_s);
     free_dev(c->ws_coefQ); free_dev(c->ws_extP); free_dev(c->ws_T); free_dev(c->ws_D); free_dev(c->chain_buf); free_dev(c->chain_coef); free_dev(c->dec_buf); free_dev(c->dig_buf);
@@ -916,7 +938,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->pool) (void)hipMemPoolDestroy(c->pool);
+    if (c->own_pool && c->pool) (void)hipMemPoolDestroy(c->pool);
     delete c;
 }
 
@@ -1661,6 +1683,15 @@ static int host_call(exacto_ctx* c, const std::vector<std::pair<const void*, siz
     if (int e = fn(dins, dout)) return e;
     HIP_TRY(hipMemcpyAsync(host_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    static const bool dbg = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
+    if (dbg && out_bytes <= 64 * 8) {   // (the bootstrap diagnostic: what the host received)
+        u64 hsh = 1469598103934665603ull;
+        const u64* ho = static_cast<const u64*>(host_out);
+        for (size_t k = 0; k < out_bytes / 8; ++k) hsh = (hsh ^ ho[k]) * 1099511628211ull;
+        std::fprintf(stderr, "boot-dbg host_out       %016llx [%llu %llu %llu %llu]\n", (unsigned long long)hsh,
+                     (unsigned long long)ho[0], (unsigned long long)(out_bytes > 8 ? ho[1] : 0),
+                     (unsigned long long)(out_bytes > 16 ? ho[2] : 0), (unsigned long long)(out_bytes > 24 ? ho[3] : 0));
+    }
     return 0;
 }
 
@@ -3121,6 +3152,59 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     auto ok = [&](hipError_t e, const char* what) {
         if (rc == 0 && e != hipSuccess) rc = fail(EXACTO_ERR_HIP, std::string("HIP error: ") + what);
     };
+    // EXACTO_DEBUG_BOOT=1 (diagnostic of DESIGN.md §3's intermittent result): snapshots of every
+    // intermediate (first 64 words) copied on the stream as the call runs, printed to stderr at the end
+    static const bool dbg = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
+    static u64* dbuf = nullptr;
+    constexpr int DW = 64, DN = 16;
+    std::vector<std::pair<std::string, size_t>> dnames;
+    if (dbg && !dbuf) (void)hipMalloc((void**)&dbuf, DN * DW * sizeof(u64));
+    auto snap = [&](const std::string& name, const u64* p, size_t words) {
+        if (!dbg || !dbuf || dnames.size() >= (size_t)DN) return;
+        const size_t w = std::min<size_t>(words, DW);
+        launch_copy_u64(dbuf + dnames.size() * DW, p, (long)w, b->stream);
+        dnames.emplace_back(name, w);
+    };
+    // multi-XCD snapshots: 16 blocks read the same words (first 4 each) and report their XCD
+    static u64* xbuf = nullptr;
+    static uint32_t* xcc = nullptr;
+    constexpr int XB = 16, XN = 4;
+    std::vector<std::string> xnames;
+    if (dbg && !xbuf) {
+        (void)hipMalloc((void**)&xbuf, XN * XB * 4 * sizeof(u64));
+        (void)hipMalloc((void**)&xcc, XN * XB * sizeof(uint32_t));
+    }
+    auto xsnap = [&](const std::string& name, const u64* p) {
+        if (!dbg || !xbuf || xnames.size() >= (size_t)XN) return;
+        launch_xcd_probe(p, xbuf + xnames.size() * XB * 4, 4, xcc + xnames.size() * XB, XB, b->stream);
+        xnames.push_back(name);
+    };
+    auto dump = [&]() {
+        if (dbg && !xnames.empty()) {
+            std::vector<u64> hx(XN * XB * 4);
+            std::vector<uint32_t> hc(XN * XB);
+            (void)hipMemcpyAsync(hx.data(), xbuf, hx.size() * sizeof(u64), hipMemcpyDeviceToHost, b->stream);
+            (void)hipMemcpyAsync(hc.data(), xcc, hc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream);
+            (void)hipStreamSynchronize(b->stream);
+            for (size_t i = 0; i < xnames.size(); ++i) {
+                std::string line = "boot-dbg xcd " + xnames[i] + ":";
+                for (int k = 0; k < XB; ++k)
+                    line += " x" + std::to_string(hc[i * XB + k]) + "=" + std::to_string(hx[(i * XB + k) * 4]);
+                std::fprintf(stderr, "%s\n", line.c_str());
+            }
+        }
+        if (!dbg || dnames.empty()) return;
+        std::vector<u64> h(DN * DW);
+        (void)hipMemcpyAsync(h.data(), dbuf, h.size() * sizeof(u64), hipMemcpyDeviceToHost, b->stream);
+        (void)hipStreamSynchronize(b->stream);
+        for (size_t i = 0; i < dnames.size(); ++i) {
+            u64 hsh = 1469598103934665603ull;
+            for (size_t k = 0; k < dnames[i].second; ++k) hsh = (hsh ^ h[i * DW + k]) * 1099511628211ull;
+            std::fprintf(stderr, "boot-dbg %-14s %016llx [%llu %llu %llu %llu]\n", dnames[i].first.c_str(),
+                         (unsigned long long)hsh, (unsigned long long)h[i * DW], (unsigned long long)h[i * DW + 1],
+                         (unsigned long long)h[i * DW + 2], (unsigned long long)h[i * DW + 3]);
+        }
+    };
     // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
     ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch), "alloc");
     ok(flags_s.alloc(B * sizeof(int), o->stream, o->pool, o->debug_scratch), "alloc");
@@ -3128,14 +3212,18 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64* coef = coef_s.as<u64>();
     int* flags = flags_s.as<int>();
     u64* small = coef + B * 2 * n;
+    snap("ct", ct, B * 2 * n);
     ok(dev_copy(coef, ct, B * 2 * n * sizeof(u64), o->stream), "copy");
     launch_fill_u32(reinterpret_cast<uint32_t*>(flags), 0, (long)B, o->stream);   // (see dev_copy)
     ok(hipGetLastError(), "flags fill");
+    snap("coef", coef, B * 2 * n);
     if (rc == 0) rc = exacto_rns_inv_dev(o, coef, B * 2);
+    snap("coef_inv", coef, B * 2 * n);
     if (rc == 0) {
         launch_modswitch(coef, small, flags, (long)B, n, o->primes[0], q_prime, b->plain, o->stream);
         ok(hipGetLastError(), "modswitch launch");
     }
+    snap("small", small, B * 2 * n);
     std::vector<int> hflags(B);
     if (rc == 0) ok(hipMemcpyAsync(hflags.data(), flags, B * sizeof(int), hipMemcpyDeviceToHost, o->stream), "flags");
     if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
@@ -3144,12 +3232,22 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
     u64* c0pt = c0pt_s.as<u64>();
     u64* c1pt = c0pt + B * n;
+    snap("small_again", small, B * 2 * n);
+    xsnap("small", small);
+    xsnap("c0pt_before", c0pt);
     if (rc == 0) {
         launch_rows(c0pt, n, small, 2 * n, n, (long)B, b->stream);
         launch_rows(c1pt, n, small + n, 2 * n, n, (long)B, b->stream);
         ok(hipGetLastError(), "copy c0/c1");
     }
+    snap("c0pt_copied", c0pt, B * n);
+    xsnap("c0pt_after", c0pt);
     if (rc == 0) rc = lift_plain(b, c1pt, (long)B, false);
+    snap("c0pt_lift1", c0pt, B * n);
+    if (dbg)
+        std::fprintf(stderr, "boot-dbg ptrs coef=%p small=%p flags=%p c0pt=%p out=%p pl_buf=%p o.pool=%p b.pool=%p\n",
+                     (void*)coef, (void*)small, (void*)flags, (void*)c0pt, (void*)out, (void*)b->pl_buf, (void*)o->pool,
+                     (void*)b->pool);
     if (rc == 0) {
         launch_plain_apply(PLAIN_MUL, bsk, 0, out, (long)B, 2, b->pl_buf, Lbn, n, b->L, b->d_primes, b->stream);
         ok(hipGetLastError(), "plain_mul launch");
@@ -3160,6 +3258,8 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
                            b->stream);
         ok(hipGetLastError(), "plain_add launch");
     }
+    snap("c0pt", c0pt, B * n);
+    snap("phase_out", out, B * 2 * Lbn);
     // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
     const size_t ctw = 2 * Lbn;
     if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
@@ -3169,8 +3269,10 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         u64* oi = out + i * ctw;
         ok(dev_copy(phase, oi, ctw * sizeof(u64), b->stream), "copy");
         if (rc) break;
+        snap("phase" + std::to_string(i), phase, ctw);
         if (!hflags[i]) {  // bfv_host.rs:180-186
             rc = exacto_eval_poly_dev(b, phase, rpoly, m, oi, 1);
+            snap("result" + std::to_string(i), oi, ctw);
             continue;
         }
         if (!slots) {  // once per call, on the first item that takes the ring path
@@ -3183,7 +3285,14 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         if (rc == 0) rc = exacto_eval_poly_dev(b, slots, rpoly, m, rounded, n);
         if (rc == 0) rc = exacto_slots_to_coeffs_dev(b, rounded, n, 2, oi);
     }
-    return drain.finish(rc);
+    rc = drain.finish(rc);
+    if (dbg) {
+        std::fprintf(stderr, "boot-dbg flags [%d] B=%zu m=%zu rpoly0..2=%llu %llu %llu\n", B ? hflags[0] : -1, B, m,
+                     (unsigned long long)rpoly[0], (unsigned long long)(m > 1 ? rpoly[1] : 0),
+                     (unsigned long long)(m > 2 ? rpoly[2] : 0));
+        dump();
+    }
+    return rc;
 }
 
 extern "C" int exacto_bootstrap_key_material(exacto_ctx* o, exacto_ctx* b, const uint64_t* sk, uint64_t* boot_sk,

@@ -178,6 +178,7 @@ void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items
 // dst[r][k] = src ? src[r][k] : 0 over rows x len with the given row strides (u64 elements)
 void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, long len, long rows, hipStream_t s);
 void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s);
+void launch_xcd_probe(const u64* src, u64* dst, long words, uint32_t* xcc, int blocks, hipStream_t s);
 void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s);
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,

@@ -1187,6 +1187,20 @@ rows_kernel(u64* __restrict__ dst, long dst_stride, const u64* __restrict__ src,
     }
 }
 
+// Diagnostic (EXACTO_DEBUG_BOOT): every block copies the same `words` words into its
+// own slot of dst and records the XCD it ran on, so a stale per-XCD L2 line shows as one slot
+// differing from the others.
+__global__ void __launch_bounds__(64) xcd_probe_kernel(const u64* src, u64* dst, long words, uint32_t* xcc) {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    for (long i = threadIdx.x; i < words; i += 64) dst[blockIdx.x * words + i] = src[i];
+    if (threadIdx.x == 0) xcc[blockIdx.x] = x;
+}
+
+void launch_xcd_probe(const u64* src, u64* dst, long words, uint32_t* xcc, int blocks, hipStream_t s) {
+    hipLaunchKernelGGL(xcd_probe_kernel, dim3(blocks), dim3(64), 0, s, src, dst, words, xcc);
+}
+
 void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, long len, long rows, hipStream_t s) {
     const long total = len * rows;
     if (total <= 0) return;

@@ -453,7 +453,9 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // are the generated statements of ntt_asm.inc (InvRoundAsm): bounds tracked per value at
 // generation time (inputs < 4q), special-prime reductions, n^-1 folded into the last stage.  Same
 // convention, twiddle layout and LDS exchanges as inv_rounds.
-template <int LOGN, int R>
+// GEN: the generic-prime statements (InvRoundGenAsm: any prime below 2^60, conditional-subtraction
+// reductions; the HPS auxiliary primes), same layout and bounds contract.
+template <int LOGN, int R, bool GEN = false>
 __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -469,8 +471,9 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
         lds_barrier();
         lds_load_x<LO>(lds, x, t2);
     }
-    InvRoundAsm<LOGN, R>::run(x, tw, K);
-    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
+    if constexpr (GEN) InvRoundGenAsm<LOGN, R>::run(x, tw, K);
+    else InvRoundAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1, GEN>(x, lds, tid, tab, K);
 }
 
 // The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread): each
@@ -637,6 +640,28 @@ __device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
 #define EXACTO_PROBE_SLEEPS_TENSOR 14   // a third of a cfg3 tensor block's ~21 us lifetime
 #endif
 
+// Inverse NTT, n = 4096 / 8192, every prime of the batch below 2^60 but not of the 2^60 - d form
+// (HPS auxiliary primes): ntt_inv_kernel with the generated generic-prime rounds (InvRoundGenAsm).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
+ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int LAST_LO = LOGN - 4;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    u64 x[16];
+    load_rows16<N>(x, src, tid);
+    inv_rounds_asm<LOGN, 0, true>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+}
+
 // Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds, exchanges and
 // coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic
@@ -797,7 +822,9 @@ __device__ __forceinline__ void tensor_unit(int rem, int L, int p2only, int& t, 
 // products and the stores), 3 = the product kernel with its first generation staggered.  (Round 4
 // also measured the next generation's operands prefetched into the L2 by scalar loads before or
 // after the transform: 296 -> 357 us, removed.)
-template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0>
+// GEN (n = 4096 / 8192, every prime below 2^60 but not all 2^60 - d: HPS): lazy Barrett products,
+// then the generated generic-prime inverse rounds (InvRoundGenAsm) instead of the C++ ones.
+template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
@@ -900,9 +927,9 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     }
     if constexpr (PROBE == 2) {
         // no transform: the products are stored as they are
-    } else if constexpr (ASM) {
+    } else if constexpr (ASM || GEN) {
         const AsmK AK = make_asmk_inv(P);
-        inv_rounds_asm<LOGN, 0>(x, lds, tid, tw_table(P.tw_inv), AK);
+        inv_rounds_asm<LOGN, 0, GEN>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
@@ -1214,6 +1241,12 @@ static bool tensor_pin_at(int logn) {
     return on < 0 ? logn == 13 : on && (logn == 12 || logn == 13);
 }
 
+// EXACTO_NTT_GEN=0: the C++ generic-prime inverse rounds instead of the generated ones (A/B switch)
+static bool ntt_gen_on() {
+    static const int on = env_switch("EXACTO_NTT_GEN", 1);
+    return on != 0;
+}
+
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0) {
@@ -1231,6 +1264,13 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
                                T, L, K, primes, remap, p2only);
+            return;
+        }
+    }
+    if constexpr (LOGN == 12 || LOGN == 13) {
+        if (lazy && !p2only && ntt_gen_on()) {   // every prime below 2^60: the generated generic-prime rounds
+            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0, s,
+                               op, extP, T, L, K, primes, remap);
             return;
         }
     }
@@ -1281,6 +1321,11 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
     if (asm_inv && inverse && (logn == 12 || logn == 13)) {
         if (logn == 12) hipLaunchKernelGGL((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
         else hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        return;
+    }
+    if (inverse && lazy && (logn == 12 || logn == 13) && ntt_gen_on()) {   // every prime below 2^60: generic asm rounds
+        if (logn == 12) hipLaunchKernelGGL((ntt_inv_gen_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else hipLaunchKernelGGL((ntt_inv_gen_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     switch (logn) {

@@ -52,3 +52,18 @@ def test_cpp_api_reproduces_golden_vectors(gpu_available, tmp_path):
     r = subprocess.run([binary, str(tmp_path), *names], capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_api_with_many_live_contexts(gpu_available, tmp_path):
+    """with one scratch pool per context, keeping every destroyed context alive
+    (EXACTO_LEAK_CTX=1, a dozen contexts and their pools) made the bootstrap read zeros in 13 of 20
+    runs of this suite; the library's one pool per device gives the golden results every time."""
+    binary = BIN if os.path.exists(BIN) else compile_test_api(str(tmp_path / "test_api"))
+    names = _write_fixtures(str(tmp_path))
+    env = dict(os.environ, EXACTO_LEAK_CTX="1")
+    env.pop("EXACTO_SCRATCH_POOL", None)
+    for rep in range(3):
+        r = subprocess.run([binary, str(tmp_path), *names], capture_output=True, text=True, timeout=600,
+                           env=env)
+        assert r.returncode == 0 and "ALL OK" in r.stdout, f"repetition {rep}\n" + r.stdout + r.stderr

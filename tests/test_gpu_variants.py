@@ -7,8 +7,8 @@ digests are compared with the default's.  The default selection itself is pinned
 the rest of the suite (test_gpu_golden.py digests, test_gpu_published.py, test_gpu_ntt.py,
 test_gpu_psum.py); bit-exact, integer work.
 
-Not listed (no effect on results): EXACTO_SCRATCH_POOL / EXACTO_DEBUG_SCRATCH / EXACTO_DEBUG_FILL
-(allocation diagnostics, tools/diag.sh), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
+Not listed (no effect on results): EXACTO_SCRATCH_POOL / EXACTO_DEBUG_SCRATCH / EXACTO_DEBUG_FILL /
+EXACTO_LEAK_CTX (allocation diagnostics, tools/diag.sh), EXACTO_DEBUG_BOOT (bootstrap snapshots), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
 EXACTO_PROF_RAW (profiling arithmetic), EXACTO_RCCL_LIB (library path).
 """
 
@@ -28,6 +28,7 @@ VARIANTS = {
     "tensor_pin_none": ({"EXACTO_TENSOR_PIN": "0"}, ["cfg5"]),
     "ntt_asm_off": ({"EXACTO_NTT_ASM": "0"}, ["cfg3", "cfg5", "hps"]),
     "ntt_asm_inv_off": ({"EXACTO_NTT_ASM_INV": "0"}, ["cfg3", "cfg5", "hps"]),
+    "ntt_gen_off": ({"EXACTO_NTT_GEN": "0"}, ["hps"]),
     "one_lane": ({"EXACTO_DUAL_STREAM": "0"}, ["cfg3", "cfg5"]),
     "three_lanes": ({"EXACTO_LANES": "3"}, ["cfg3"]),
     "share_ext_off": ({"EXACTO_SHARE_EXT": "0"}, ["cfg4", "cfg5", "hps"]),
@@ -75,7 +76,7 @@ def test_every_library_switch_is_covered():
             with open(os.path.join(src, f)) as fh:
                 found |= set(re.findall(r'(?:getenv|env_switch)\("(EXACTO_[A-Z0-9_]+)"', fh.read()))
     neutral = {"EXACTO_SCRATCH_POOL", "EXACTO_DEBUG_SCRATCH", "EXACTO_DEBUG_FILL", "EXACTO_DBFV_GROUP_MB",
-               "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB"}
+               "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB", "EXACTO_DEBUG_BOOT", "EXACTO_LEAK_CTX"}
     assert found - neutral == set(SWITCHES), found ^ (set(SWITCHES) | neutral)
 
 

@@ -199,6 +199,19 @@ def reduce_seq(st, dst, src, src_hi, t, u):
     ]
 
 
+def halve_seq(st, dst, src, m, t, c):
+    """dst = src - m q if src >= m q else src (pairs; any prime q < 2^60, no special form): the
+    generic reduction step of InvRound(generic=True).  t: temp pair; c: this stream's carry pair.
+    The subtraction's high word takes m q's high half from a VGPR (one SGPR read per VALU)."""
+    sl, sh = lo(src), hi(src)
+    return [
+        Ins(f"v_sub_co_u32_e64 {lo(t)}, {c}, {sl}, {st.cql(m)}", wr=[c]),
+        Ins(f"v_subb_co_u32_e64 {hi(t)}, {c}, {sh}, {st.cqh(m)}, {c}", rd=[c], wr=[c]),
+        Ins(f"v_cndmask_b32_e64 {lo(dst)}, {lo(t)}, {sl}, {c}", rd=[c]),
+        Ins(f"v_cndmask_b32_e64 {hi(dst)}, {hi(t)}, {sh}, {c}", rd=[c]),
+    ]
+
+
 def canon_seq(st, dst, r, S, M):
     """dst = r mod q for r < 2q: s = r - q, out = s + (q & sign(s)).  S, M: temp pairs."""
     return [
@@ -406,9 +419,13 @@ class InvRound(Statement):
     """One inverse round (Gentleman-Sande, stage bits BLO..BHI ascending) as one asm statement.
     bound_in: every input value < bound_in * q."""
 
-    def __init__(self, logn, r, bound_in, approx=True):
+    def __init__(self, logn, r, bound_in, approx=True, generic=False):
         super().__init__()
         self.logn, self.r, self.approx = logn, r, approx
+        # generic: any prime q < 2^60 (the HPS auxiliary primes): a sum that would pass 16q first
+        # halves its larger operand's bound by one conditional subtraction of (bound / 2) q
+        # (halve_seq, 4 VALU) instead of the special-prime fold to < 2q (reduce_seq)
+        self.generic = generic
         self.tb = 3 if approx else 2             # Shoup output bound (units of q)
         self.lo = min(4 * r, logn - 4)
         self.blo = 4 * r
@@ -490,10 +507,21 @@ class InvRound(Statement):
                     c = sp(C[j])
                     s = []
                     # keep the pair sum and the difference below 16q
-                    for _ in range(2):
+                    for _ in range(8 if self.generic else 2):
                         if bnd[k0] + bnd[k1] <= 16:
                             break
                         kr = k0 if bnd[k0] >= bnd[k1] else k1
+                        if self.generic:
+                            half = 1
+                            while 2 * half < bnd[kr]:
+                                half *= 2            # bnd[kr] in (half, 2 half]: subtract half q
+                            if loc[kr] is None:
+                                dst = alloc()
+                                s += [Ins(f"v_lshl_add_u64 {dst}, %[x{kr}], 0, 0")]
+                                loc[kr] = dst
+                            s += halve_seq(self, loc[kr], loc[kr], half, t["B"], c)
+                            bnd[kr] = half
+                            continue
                         if loc[kr] is None:
                             dst = alloc()
                             s += reduce_seq(self, dst, val64(kr), self.xh(kr), lo(t["B"]), hi(t["B"]))
@@ -561,8 +589,10 @@ class InvRound(Statement):
 
     def emit(self):
         seq = self.gen()
-        return emit_statement(f"InvRoundAsm<{self.logn}, {self.r}>", self, seq, self.vmax,
-                              f"round {self.r} of the {1 << self.logn}-point inverse NTT: stage bits "
+        struct = "InvRoundGenAsm" if self.generic else "InvRoundAsm"
+        return emit_statement(f"{struct}<{self.logn}, {self.r}>", self, seq, self.vmax,
+                              f"round {self.r} of the {1 << self.logn}-point inverse NTT"
+                              f"{' for any prime below 2^60' if self.generic else ''}: stage bits "
                               f"{self.blo}..{self.bhi}, inputs < {self.bound_in}q, outputs < "
                               f"{self.bound_out}q",
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
@@ -646,11 +676,11 @@ def inv_rounds_pinned(logn, approx=True):
     return out
 
 
-def inv_rounds(logn, approx=True):
+def inv_rounds(logn, approx=True, generic=False):
     """The inverse rounds of one transform, each starting at the previous round's output bound."""
     out, b = [], INV_BOUND_IN
     for r in range((logn + 3) // 4):
-        rd = InvRound(logn, r, b, approx)
+        rd = InvRound(logn, r, b, approx, generic)
         rd.gen()
         out.append(rd)
         b = rd.bound_out
@@ -768,6 +798,7 @@ __device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
 
 template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
+template <int LOGN, int R> struct InvRoundGenAsm;   // any prime below 2^60 (HPS auxiliary primes)
 template <int W> struct MulNear60Asm;
 template <int W> struct MulNear60PinAsm;   // temps below the pinned homes (kernels with EXACTO_PIN_DECL)
 template <int W> struct MulNear60PinVAsm;  // ... as asm volatile (ordered with fences and other statements)
@@ -786,6 +817,9 @@ def main():
             parts.append("\n")
         for rd in inv_rounds(logn, approx):
             parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
+            parts.append("\n")
+        for rd in inv_rounds(logn, approx, generic=True):
+            parts.append(InvRound(logn, rd.r, rd.bound_in, approx, generic=True).emit())
             parts.append("\n")
         for r in range((logn + 3) // 4):
             parts.append(Round(logn, r, approx, True, pinned=True).emit())
