@@ -1684,7 +1684,7 @@ static int host_call(exacto_ctx* c, const std::vector<std::pair<const void*, siz
     HIP_TRY(hipMemcpyAsync(host_out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     static const bool dbg = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
-    if (dbg && out_bytes <= 64 * 8) {   // (the bootstrap diagnostic: what the host received)
+    if (dbg && host_out && out_bytes >= 8 && out_bytes <= 64 * 8) {   // (the bootstrap diagnostic: what the host received)
         u64 hsh = 1469598103934665603ull;
         const u64* ho = static_cast<const u64*>(host_out);
         for (size_t k = 0; k < out_bytes / 8; ++k) hsh = (hsh ^ ho[k]) * 1099511628211ull;
@@ -3113,6 +3113,64 @@ extern "C" int exacto_bootstrap_key_material_dev(exacto_ctx* o, exacto_ctx* b, c
     return rc;
 }
 
+// EXACTO_DEBUG_BOOT=1: the diagnostic of DESIGN.md §3's intermittent bootstrap result.  snap()
+// copies the first words of an intermediate into a debug buffer on the stream as the call runs;
+// xsnap() reads a block from 16 workgroups spread over the XCDs, each recording its XCD; dump()
+// prints both to stderr after the call's final synchronisation.  Off: every call is a no-op.
+struct BootDebug {
+    static constexpr int DW = 64, DN = 16, XB = 16, XN = 4;
+    hipStream_t s;
+    bool on;
+    u64* dbuf = nullptr;
+    u64* xbuf = nullptr;
+    uint32_t* xcc = nullptr;
+    std::vector<std::pair<std::string, size_t>> names;
+    std::vector<std::string> xnames;
+    explicit BootDebug(hipStream_t st) : s(st) {
+        static const bool env = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
+        on = env && hipMalloc((void**)&dbuf, DN * DW * sizeof(u64)) == hipSuccess &&
+             hipMalloc((void**)&xbuf, XN * XB * 4 * sizeof(u64)) == hipSuccess &&
+             hipMalloc((void**)&xcc, XN * XB * sizeof(uint32_t)) == hipSuccess;
+    }
+    ~BootDebug() {
+        if (dbuf || xbuf || xcc) (void)hipStreamSynchronize(s);
+        free_dev(dbuf); free_dev(xbuf); free_dev(xcc);
+    }
+    void snap(const std::string& name, const u64* p, size_t words) {
+        if (!on || names.size() >= (size_t)DN) return;
+        const size_t w = std::min<size_t>(words, DW);
+        launch_copy_u64(dbuf + names.size() * DW, p, (long)w, s);
+        names.emplace_back(name, w);
+    }
+    void xsnap(const std::string& name, const u64* p) {
+        if (!on || xnames.size() >= (size_t)XN) return;
+        launch_xcd_probe(p, xbuf + xnames.size() * XB * 4, 4, xcc + xnames.size() * XB, XB, s);
+        xnames.push_back(name);
+    }
+    void dump() {
+        if (!on) return;
+        std::vector<u64> h(DN * DW), hx(XN * XB * 4);
+        std::vector<uint32_t> hc(XN * XB);
+        (void)hipMemcpyAsync(h.data(), dbuf, h.size() * sizeof(u64), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(hx.data(), xbuf, hx.size() * sizeof(u64), hipMemcpyDeviceToHost, s);
+        (void)hipMemcpyAsync(hc.data(), xcc, hc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        for (size_t i = 0; i < xnames.size(); ++i) {
+            std::string line = "boot-dbg xcd " + xnames[i] + ":";
+            for (int k = 0; k < XB; ++k)
+                line += " x" + std::to_string(hc[i * XB + k]) + "=" + std::to_string(hx[(i * XB + k) * 4]);
+            std::fprintf(stderr, "%s\n", line.c_str());
+        }
+        for (size_t i = 0; i < names.size(); ++i) {
+            u64 hsh = 1469598103934665603ull;   // FNV-1a of the snapshot
+            for (size_t k = 0; k < names[i].second; ++k) hsh = (hsh ^ h[i * DW + k]) * 1099511628211ull;
+            std::fprintf(stderr, "boot-dbg %-14s %016llx [%llu %llu %llu %llu]\n", names[i].first.c_str(),
+                         (unsigned long long)hsh, (unsigned long long)h[i * DW], (unsigned long long)h[i * DW + 1],
+                         (unsigned long long)h[i * DW + 2], (unsigned long long)h[i * DW + 3]);
+        }
+    }
+};
+
 // bfv_bootstrap (bfv_host.rs:131-205) on B ciphertexts of the original scheme (ct [B][2][1][n] on
 // o) -> out [B][2][Lb][n] on b.  bsk [2][Lb][n] is the encryption of s under b; the boot
 // relinearisation key must be resident in b; (elements, gks) are the trace keys as in
@@ -3152,59 +3210,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     auto ok = [&](hipError_t e, const char* what) {
         if (rc == 0 && e != hipSuccess) rc = fail(EXACTO_ERR_HIP, std::string("HIP error: ") + what);
     };
-    // EXACTO_DEBUG_BOOT=1 (diagnostic of DESIGN.md §3's intermittent result): snapshots of every
-    // intermediate (first 64 words) copied on the stream as the call runs, printed to stderr at the end
-    static const bool dbg = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
-    static u64* dbuf = nullptr;
-    constexpr int DW = 64, DN = 16;
-    std::vector<std::pair<std::string, size_t>> dnames;
-    if (dbg && !dbuf) (void)hipMalloc((void**)&dbuf, DN * DW * sizeof(u64));
-    auto snap = [&](const std::string& name, const u64* p, size_t words) {
-        if (!dbg || !dbuf || dnames.size() >= (size_t)DN) return;
-        const size_t w = std::min<size_t>(words, DW);
-        launch_copy_u64(dbuf + dnames.size() * DW, p, (long)w, b->stream);
-        dnames.emplace_back(name, w);
-    };
-    // multi-XCD snapshots: 16 blocks read the same words (first 4 each) and report their XCD
-    static u64* xbuf = nullptr;
-    static uint32_t* xcc = nullptr;
-    constexpr int XB = 16, XN = 4;
-    std::vector<std::string> xnames;
-    if (dbg && !xbuf) {
-        (void)hipMalloc((void**)&xbuf, XN * XB * 4 * sizeof(u64));
-        (void)hipMalloc((void**)&xcc, XN * XB * sizeof(uint32_t));
-    }
-    auto xsnap = [&](const std::string& name, const u64* p) {
-        if (!dbg || !xbuf || xnames.size() >= (size_t)XN) return;
-        launch_xcd_probe(p, xbuf + xnames.size() * XB * 4, 4, xcc + xnames.size() * XB, XB, b->stream);
-        xnames.push_back(name);
-    };
-    auto dump = [&]() {
-        if (dbg && !xnames.empty()) {
-            std::vector<u64> hx(XN * XB * 4);
-            std::vector<uint32_t> hc(XN * XB);
-            (void)hipMemcpyAsync(hx.data(), xbuf, hx.size() * sizeof(u64), hipMemcpyDeviceToHost, b->stream);
-            (void)hipMemcpyAsync(hc.data(), xcc, hc.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, b->stream);
-            (void)hipStreamSynchronize(b->stream);
-            for (size_t i = 0; i < xnames.size(); ++i) {
-                std::string line = "boot-dbg xcd " + xnames[i] + ":";
-                for (int k = 0; k < XB; ++k)
-                    line += " x" + std::to_string(hc[i * XB + k]) + "=" + std::to_string(hx[(i * XB + k) * 4]);
-                std::fprintf(stderr, "%s\n", line.c_str());
-            }
-        }
-        if (!dbg || dnames.empty()) return;
-        std::vector<u64> h(DN * DW);
-        (void)hipMemcpyAsync(h.data(), dbuf, h.size() * sizeof(u64), hipMemcpyDeviceToHost, b->stream);
-        (void)hipStreamSynchronize(b->stream);
-        for (size_t i = 0; i < dnames.size(); ++i) {
-            u64 hsh = 1469598103934665603ull;
-            for (size_t k = 0; k < dnames[i].second; ++k) hsh = (hsh ^ h[i * DW + k]) * 1099511628211ull;
-            std::fprintf(stderr, "boot-dbg %-14s %016llx [%llu %llu %llu %llu]\n", dnames[i].first.c_str(),
-                         (unsigned long long)hsh, (unsigned long long)h[i * DW], (unsigned long long)h[i * DW + 1],
-                         (unsigned long long)h[i * DW + 2], (unsigned long long)h[i * DW + 3]);
-        }
-    };
+    BootDebug dbg(b->stream);
     // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
     ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch), "alloc");
     ok(flags_s.alloc(B * sizeof(int), o->stream, o->pool, o->debug_scratch), "alloc");
@@ -3212,18 +3218,18 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64* coef = coef_s.as<u64>();
     int* flags = flags_s.as<int>();
     u64* small = coef + B * 2 * n;
-    snap("ct", ct, B * 2 * n);
+    dbg.snap("ct", ct, B * 2 * n);
     ok(dev_copy(coef, ct, B * 2 * n * sizeof(u64), o->stream), "copy");
     launch_fill_u32(reinterpret_cast<uint32_t*>(flags), 0, (long)B, o->stream);   // (see dev_copy)
     ok(hipGetLastError(), "flags fill");
-    snap("coef", coef, B * 2 * n);
+    dbg.snap("coef", coef, B * 2 * n);
     if (rc == 0) rc = exacto_rns_inv_dev(o, coef, B * 2);
-    snap("coef_inv", coef, B * 2 * n);
+    dbg.snap("coef_inv", coef, B * 2 * n);
     if (rc == 0) {
         launch_modswitch(coef, small, flags, (long)B, n, o->primes[0], q_prime, b->plain, o->stream);
         ok(hipGetLastError(), "modswitch launch");
     }
-    snap("small", small, B * 2 * n);
+    dbg.snap("small", small, B * 2 * n);
     std::vector<int> hflags(B);
     if (rc == 0) ok(hipMemcpyAsync(hflags.data(), flags, B * sizeof(int), hipMemcpyDeviceToHost, o->stream), "flags");
     if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
@@ -3232,22 +3238,18 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
     u64* c0pt = c0pt_s.as<u64>();
     u64* c1pt = c0pt + B * n;
-    snap("small_again", small, B * 2 * n);
-    xsnap("small", small);
-    xsnap("c0pt_before", c0pt);
+    dbg.snap("small_again", small, B * 2 * n);
+    dbg.xsnap("small", small);
+    dbg.xsnap("c0pt_before", c0pt);
     if (rc == 0) {
         launch_rows(c0pt, n, small, 2 * n, n, (long)B, b->stream);
         launch_rows(c1pt, n, small + n, 2 * n, n, (long)B, b->stream);
         ok(hipGetLastError(), "copy c0/c1");
     }
-    snap("c0pt_copied", c0pt, B * n);
-    xsnap("c0pt_after", c0pt);
+    dbg.snap("c0pt_copied", c0pt, B * n);
+    dbg.xsnap("c0pt_after", c0pt);
     if (rc == 0) rc = lift_plain(b, c1pt, (long)B, false);
-    snap("c0pt_lift1", c0pt, B * n);
-    if (dbg)
-        std::fprintf(stderr, "boot-dbg ptrs coef=%p small=%p flags=%p c0pt=%p out=%p pl_buf=%p o.pool=%p b.pool=%p\n",
-                     (void*)coef, (void*)small, (void*)flags, (void*)c0pt, (void*)out, (void*)b->pl_buf, (void*)o->pool,
-                     (void*)b->pool);
+    dbg.snap("c0pt_lift1", c0pt, B * n);
     if (rc == 0) {
         launch_plain_apply(PLAIN_MUL, bsk, 0, out, (long)B, 2, b->pl_buf, Lbn, n, b->L, b->d_primes, b->stream);
         ok(hipGetLastError(), "plain_mul launch");
@@ -3258,8 +3260,8 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
                            b->stream);
         ok(hipGetLastError(), "plain_add launch");
     }
-    snap("c0pt", c0pt, B * n);
-    snap("phase_out", out, B * 2 * Lbn);
+    dbg.snap("c0pt", c0pt, B * n);
+    dbg.snap("phase_out", out, B * 2 * Lbn);
     // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
     const size_t ctw = 2 * Lbn;
     if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
@@ -3269,10 +3271,10 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         u64* oi = out + i * ctw;
         ok(dev_copy(phase, oi, ctw * sizeof(u64), b->stream), "copy");
         if (rc) break;
-        snap("phase" + std::to_string(i), phase, ctw);
+        dbg.snap("phase" + std::to_string(i), phase, ctw);
         if (!hflags[i]) {  // bfv_host.rs:180-186
             rc = exacto_eval_poly_dev(b, phase, rpoly, m, oi, 1);
-            snap("result" + std::to_string(i), oi, ctw);
+            dbg.snap("result" + std::to_string(i), oi, ctw);
             continue;
         }
         if (!slots) {  // once per call, on the first item that takes the ring path
@@ -3286,12 +3288,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         if (rc == 0) rc = exacto_slots_to_coeffs_dev(b, rounded, n, 2, oi);
     }
     rc = drain.finish(rc);
-    if (dbg) {
-        std::fprintf(stderr, "boot-dbg flags [%d] B=%zu m=%zu rpoly0..2=%llu %llu %llu\n", B ? hflags[0] : -1, B, m,
-                     (unsigned long long)rpoly[0], (unsigned long long)(m > 1 ? rpoly[1] : 0),
-                     (unsigned long long)(m > 2 ? rpoly[2] : 0));
-        dump();
-    }
+    dbg.dump();
     return rc;
 }
 

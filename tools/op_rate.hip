@@ -43,13 +43,30 @@ typedef uint32_t u32;
     X(26, "v_lshl_or_b32", asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a[i]) : "v"(b)))         \
     X(27, "v_sub_u32", asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))                    \
     X(28, "v_max_u32", asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))                    \
-    X(29, "v_min_u32", asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))
+    X(29, "v_min_u32", asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b)))                    \
+    X(30, "v_mul_u32_u24", asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b)))            \
+    X(31, "v_fma_f64", asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(w[i]) : "v"((u64)b)))           \
+    X(32, "v_mul_f64", asm volatile("v_mul_f64 %0, %0, %1" : "+v"(w[i]) : "v"((u64)b)))               \
+    X(33, "v_cvt_f64_u32", asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(w[i]) : "v"(a[i])))             \
+    X(34, "v_cvt_u32_f64", asm volatile("v_cvt_u32_f64 %0, %1" : "=v"(a[i]) : "v"(w[i])))             \
+    X(35, "v_fma_f32", asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(b)))                \
+    X(36, "v_pk_fma_f32", asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(w[i]) : "v"((u64)b)))     \
+    X(37, "v_mul_lo_u16", asm volatile("v_mul_lo_u16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))             \
+    X(38, "v_pk_mul_lo_u16", asm volatile("v_pk_mul_lo_u16 %0, %0, %1" : "+v"(a[i]) : "v"(b)))        \
+    X(39, "v_dot2_u32_u16", asm volatile("v_dot2_u32_u16 %0, %0, %1, %0" : "+v"(a[i]) : "v"(b)))      \
+    X(40, "PAIR cmp+cndmask vcc", asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(b) : "vcc")) \
+    X(41, "PAIR cmp+cndmask s", asm volatile("v_cmp_gt_u32_e64 s[40:41], %0, %1\n\tv_cndmask_b32_e64 %0, %0, %1, s[40:41]" : "+v"(a[i]) : "v"(b) : "s40", "s41")) \
+    X(42, "PAIR sub+min", asm volatile("v_sub_u32 %0, %0, %1\n\tv_min_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b))) \
+    X(43, "v_cndmask_b32 vcc (set)", asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(b)))     \
+    X(44, "PAIR sub_co+subb vcc", asm volatile("v_sub_co_u32 %0, vcc, %0, %1\n\tv_subb_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a[i]) : "v"(b) : "vcc")) \
+    X(45, "PAIR sub_co+subb s", asm volatile("v_sub_co_u32_e64 %0, s[40:41], %0, %1\n\tv_subb_co_u32_e64 %0, s[40:41], %0, %1, s[40:41]" : "+v"(a[i]) : "v"(b) : "s40", "s41"))
 
 template <int OP>
 __global__ void __launch_bounds__(256) k(u32* out, u32 seed) {
     u32 a[8], b = seed + threadIdx.x;
     u64 w[8];
     for (int i = 0; i < 8; ++i) { a[i] = seed * (i + 3) + threadIdx.x; w[i] = a[i]; }
+    if (OP == 43) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a[0]), "v"(b) : "vcc");
     for (int it = 0; it < ITERS; ++it) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
