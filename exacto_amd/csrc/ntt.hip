@@ -627,11 +627,14 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // Probe mode 3 (tools/ntt_probe.hip): the first generation of resident blocks (`slots`, one per CU
 // per step of blockIdx / 256) start staggered by `ph` of PHASES block lifetimes, so that loads and
 // arithmetic of co-resident blocks stop running in phase; later blocks inherit their slot's offset.
+// exacto_probe_sleeps >= 0 (set by the probe tool) overrides the compiled sleeps per phase.
+__device__ int exacto_probe_sleeps = -1;
 template <int PHASES>
 __device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
     if ((int)blockIdx.x >= slots) return;
     const int ph = (int)(blockIdx.x / 256) % PHASES;
-    for (int i = 0; i < ph * sleeps_per_phase; ++i) __builtin_amdgcn_s_sleep(16);   // ~1024 cycles each
+    const int sp = exacto_probe_sleeps >= 0 ? exacto_probe_sleeps : sleeps_per_phase;
+    for (int i = 0; i < ph * sp; ++i) __builtin_amdgcn_s_sleep(16);   // ~1024 cycles each
 }
 #ifndef EXACTO_PROBE_SLEEPS_FWD
 #define EXACTO_PROBE_SLEEPS_FWD 11      // a quarter of a 4096-point forward block's ~21 us lifetime
@@ -681,7 +684,10 @@ ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
     const u64 q = P.q;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
-    if constexpr (PROBE == 3) probe_stagger<4>(1024, EXACTO_PROBE_SLEEPS_FWD);
+    if constexpr (PROBE == 3) {
+        if constexpr (LOGN == 12) probe_stagger<4>(1024, EXACTO_PROBE_SLEEPS_FWD);
+        else probe_stagger<2>(512, EXACTO_PROBE_SLEEPS_FWD);   // n = 8192: two blocks per CU
+    }
     EXACTO_PIN_DECL
     if constexpr (PROBE == 1) {
         const u64 h = ((u64)p << 20) ^ (u64)tid;

@@ -112,6 +112,37 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 3>), dim3(tblocks), dim3(256), 0, 0, op, E, Tt, 3, 4, d_pc, 1, 0);
     });
     const double fbytes = 16.0 * N * polys, tbytes = 7.0 * 8 * N * items * NP;
+    // n = 8192 forward (cfg5's launches hold 512-640 polynomials against 512 resident blocks): full,
+    // compute only, memory only, and the second block of each CU started late by a swept delay
+    constexpr int N13 = 1 << 13;
+    std::vector<TwPair> tw13(N13);
+    for (auto& t : tw13) {
+        t.w = rng() % q;
+        t.ws = shoup_c(t.w, q);
+    }
+    TwPair* d_tw13 = nullptr;
+    CK(hipMalloc(&d_tw13, N13 * sizeof(TwPair)));
+    CK(hipMemcpy(d_tw13, tw13.data(), N13 * sizeof(TwPair), hipMemcpyHostToDevice));
+    for (auto& P : pc) P.tw_fwd = P.tw_inv = d_tw13;
+    CK(hipMemcpy(d_pc, pc.data(), NP * sizeof(PrimeConst), hipMemcpyHostToDevice));
+    std::printf("{\"n8192\": [");
+    for (long p13 : {512L, 576L, 1024L}) {
+        nb.src_item_stride = N13; nb.dst_item_stride = N13;
+        const double a = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 0>), dim3(p13), dim3(512), 0, 0, nb, d_pc); });
+        const double c = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 1>), dim3(p13), dim3(512), 0, 0, nb, d_pc); });
+        const double m = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 2>), dim3(p13), dim3(512), 0, 0, nb, d_pc); });
+        std::printf("%s{\"polys\": %ld, \"full_us\": %.2f, \"frac\": %.3f, \"compute_only_us\": %.2f, \"memory_only_us\": %.2f, \"stagger\": {",
+                    p13 == 512 ? "" : ", ", p13, a, 16.0 * N13 * p13 / (a * 1e3) / 8000.0, c, m);
+        for (int sl : {0, 2, 4, 6, 8, 12, 16}) {
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(exacto_probe_sleeps), &sl, sizeof(int)));
+            const double t = timed([&] { hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 3>), dim3(p13), dim3(512), 0, 0, nb, d_pc); });
+            std::printf("%s\"%d\": %.2f", sl ? ", " : "", sl, t);
+        }
+        std::printf("}}");
+        const int off = -1;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(exacto_probe_sleeps), &off, sizeof(int)));
+    }
+    std::printf("]}\n");
     std::printf("{\"fwd_pin_polys\": %ld, \"fwd_full_us\": %.2f, \"fwd_compute_only_us\": %.2f, \"fwd_memory_only_us\": %.2f, "
                 "\"fwd_staggered_us\": %.2f, \"fwd_full_GBs\": %.1f, \"fwd_compute_over_full\": %.3f, "
                 "\"tensor12_blocks\": %ld, \"tensor_full_us\": %.2f, \"tensor_compute_only_us\": %.2f, "
