@@ -294,7 +294,8 @@ __device__ __forceinline__ void lds_load_x(const u64* lds, u64 (&x)[16], int tid
     for (int k = 0; k < 16; ++k) x[k] = *reinterpret_cast<const u64*>(lb + (b ^ (swz(k << LO) << 3)));
 }
 
-template <int LOGN, int R>
+// GEN: the generic-prime statements (FwdRoundGenAsm: any prime below 2^60; the HPS primes).
+template <int LOGN, int R, bool GEN = false>
 __device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
@@ -310,8 +311,9 @@ __device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
         lds_barrier();
         lds_load_x<LO>(lds, x, t2);
     }
-    FwdRoundAsm<LOGN, R>::run(x, tw, K);
-    if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1>(x, lds, tid, tab, K);
+    if constexpr (GEN) FwdRoundGenAsm<LOGN, R>::run(x, tw, K);
+    else FwdRoundAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1, GEN>(x, lds, tid, tab, K);
 }
 
 // ---------------------------------------------------------------- inverse
@@ -643,7 +645,34 @@ __device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
 #define EXACTO_PROBE_SLEEPS_TENSOR 14   // a third of a cfg3 tensor block's ~21 us lifetime
 #endif
 
-// Inverse NTT, n = 4096 / 8192, every prime of the batch below 2^60 but not of the 2^60 - d form
+// Forward NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not all of the
+// 2^60 - d form (the HPS primes): ntt_fwd_kernel's loads, the generated generic-prime rounds
+// (FwdRoundGenAsm, canonical outputs) and coalesced stores (element tid + k T through LDS).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
+ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+    constexpr int N = 1 << LOGN;
+    constexpr int T = N / 16;
+    __shared__ u64 lds[N];
+    const int tid = threadIdx.x;
+    const int p = blockIdx.x;
+    const int item = p / nb.ppi, sub = p - item * nb.ppi;
+    const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
+    const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
+                     (long)sub * N;
+    u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
+    u64 x[16];
+    load_coeffs<N>(x, nb, src, item, sub, P.q, tid);
+    fwd_rounds_asm<LOGN, 0, true>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
+    lds_barrier();
+    lds_store_x<0>(lds, x, tid);
+    lds_barrier();
+    lds_load_x<LOGN - 4>(lds, x, tid);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+}
+
+// Inverse NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not of the 2^60 - d form
 // (HPS auxiliary primes): ntt_inv_kernel with the generated generic-prime rounds (InvRoundGenAsm).
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
@@ -1273,7 +1302,7 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
             return;
         }
     }
-    if constexpr (LOGN == 12 || LOGN == 13) {
+    if constexpr (LOGN == 10 || LOGN == 12 || LOGN == 13) {
         if (lazy && !p2only && ntt_gen_on()) {   // every prime below 2^60: the generated generic-prime rounds
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0, s,
                                op, extP, T, L, K, primes, remap);
@@ -1329,9 +1358,17 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
         else hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
-    if (inverse && lazy && (logn == 12 || logn == 13) && ntt_gen_on()) {   // every prime below 2^60: generic asm rounds
-        if (logn == 12) hipLaunchKernelGGL((ntt_inv_gen_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_inv_gen_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+    if (lazy && (logn == 10 || logn == 12 || logn == 13) && ntt_gen_on()) {   // every prime below 2^60: generic asm rounds
+        const dim3 th(1u << (logn - 4));
+        if (inverse) {
+            if (logn == 10) hipLaunchKernelGGL((ntt_inv_gen_kernel<10>), dim3(count), th, 0, s, nb, primes);
+            else if (logn == 12) hipLaunchKernelGGL((ntt_inv_gen_kernel<12>), dim3(count), th, 0, s, nb, primes);
+            else hipLaunchKernelGGL((ntt_inv_gen_kernel<13>), dim3(count), th, 0, s, nb, primes);
+        } else {
+            if (logn == 10) hipLaunchKernelGGL((ntt_fwd_gen_kernel<10>), dim3(count), th, 0, s, nb, primes);
+            else if (logn == 12) hipLaunchKernelGGL((ntt_fwd_gen_kernel<12>), dim3(count), th, 0, s, nb, primes);
+            else hipLaunchKernelGGL((ntt_fwd_gen_kernel<13>), dim3(count), th, 0, s, nb, primes);
+        }
         return;
     }
     switch (logn) {

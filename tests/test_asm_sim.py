@@ -28,6 +28,18 @@ def test_rounds_match_exact_arithmetic():
                     asm_sim.check_inv_round_pinned(logn, r, q, rng, approx)
 
 
+def test_generic_rounds_match_exact_arithmetic():
+    # FwdRoundGenAsm / InvRoundGenAsm (any q < 2^60) at every size they are emitted for, over the
+    # HPS primes of the published configurations and the ends of the range
+    rng = random.Random(13)
+    for logn in gen_ntt_asm.GEN_LOGN:
+        for r in range((logn + 3) // 4):
+            for i in range(2 * len(asm_sim.GENERIC_PRIMES)):
+                q = asm_sim.GENERIC_PRIMES[i % len(asm_sim.GENERIC_PRIMES)]
+                asm_sim.check_round(logn, r, q, rng, True, generic=True)
+                asm_sim.check_inv_round(logn, r, q, rng, True, generic=True)
+
+
 def test_tensor_products_match_exact_arithmetic():
     # MulNear60Asm: the 120-bit product folded twice through 2^60 == d, for every BASELINE prime
     # (the fifth entry of PRIMES has d = 2^32 - 3, outside the d < 2^24 this sequence needs)

@@ -102,6 +102,8 @@ class Lane:
             r = self.rd32(ops[2]) - self.rd32(ops[3]) - self.s[ops[4]]
             self.s[ops[1]] = 1 if r < 0 else 0
             self.wr32(ops[0], r)
+        elif mnem == "v_cmp_le_u64_e64":
+            self.s[ops[0]] = 1 if self.rd64(ops[1]) <= self.rd64(ops[2]) else 0
         elif mnem == "v_lshl_add_u64":
             self.wr64(ops[0], (self.rd64(ops[1]) << int(ops[2])) + self.rd64(ops[3]))
         elif mnem == "v_lshrrev_b32":
@@ -152,6 +154,10 @@ def _named(rd, x, tw, q, logn):
         if m:
             named[key] = [int(m.group(1)) * q, 64]
             continue
+        m = re.fullmatch(r"nmq(\d+)", key)
+        if m:
+            named[key] = [((1 << 64) - int(m.group(1)) * q) & M64, 64]
+            continue
         m = re.fullmatch(r"q(\d+)([lh])", key)
         if m:
             cq = int(m.group(1)) * q
@@ -170,8 +176,8 @@ def _inputs(rng, bound_in):
     return x
 
 
-def check_round(logn, r, q, rng, approx=True):
-    rd = G.Round(logn, r, approx)
+def check_round(logn, r, q, rng, approx=True, generic=False):
+    rd = G.Round(logn, r, approx, generic=generic)
     seq = rd.gen()
     first = r == 0
     bound_in = q if first else 16 * q
@@ -196,9 +202,9 @@ def check_round(logn, r, q, rng, approx=True):
             assert got[k] < rd.bound_out * q, ("bound", logn, r, k, got[k] / q)
 
 
-def check_inv_round(logn, r, q, rng, approx=True):
-    rd = G.inv_rounds(logn, approx)[r]
-    rd = G.InvRound(logn, r, rd.bound_in, approx)
+def check_inv_round(logn, r, q, rng, approx=True, generic=False):
+    rd = G.inv_rounds(logn, approx, generic)[r]
+    rd = G.InvRound(logn, r, rd.bound_in, approx, generic)
     seq = rd.gen()
     x = _inputs(rng, rd.bound_in * q)
     tw = [rng.randrange(q) for _ in range(15)]
@@ -295,6 +301,10 @@ def check_mulpair(w, q, rng):
 
 PRIMES = [1152921504606830593, 1152921504606748673, 1152921504606683137, 1152921504606601217,
           (1 << 60) - (1 << 32) + 3]  # the last: d = 2^32 - 3, the edge of the path (primality irrelevant here)
+# the generic rounds: the HPS primes of compact_bfv (q, aux) and u64_dbfv (aux), odd values near both
+# ends of (2^30, 2^60), and the special primes (any prime below 2^60 is in their domain)
+GENERIC_PRIMES = [1099509805057, 562949953443841, 18014398509998081, 36028797018972161,
+                  (1 << 60) - 1, (1 << 59) + 12345, (1 << 30) + 3] + PRIMES[:2]
 
 
 def main():
@@ -308,6 +318,12 @@ def main():
                     check_inv_round(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
                     check_round_pinned(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
                     check_inv_round_pinned(logn, r, PRIMES[i % len(PRIMES)], rng, approx)
+    for logn in G.GEN_LOGN:
+        for r in range((logn + 3) // 4):
+            for i in range(trials):
+                q = GENERIC_PRIMES[i % len(GENERIC_PRIMES)]
+                check_round(logn, r, q, rng, True, generic=True)
+                check_inv_round(logn, r, q, rng, True, generic=True)
     for i in range(trials):
         for w in (1, 2):
             check_mulpair(w, PRIMES[i % 4], rng)

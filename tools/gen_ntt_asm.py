@@ -37,6 +37,11 @@ bounded by X's bound + cq per stage), so the round ends below 2q + 4cq <= 14q < 
 Final forward round: the reduction above, then r - q, selected by the sign of r - q (and-mask + add).
 Final inverse stage: n^-1 folded in (x0 = (U+V)*n^-1, x1 = D*psi_inv_rev[1]*n^-1), exact Shoup,
 then the same canonical reduction.
+Generic rounds (FwdRoundGenAsm / InvRoundGenAsm, any q < 2^60: the HPS primes of compact_bfv and
+u64_dbfv): the Shoup chain is the same (it only uses 2^64 - q); every reduction is instead a chain
+of conditional subtractions of (bound/2) q, each c = (m q <= x) by one 64-bit compare, x + (2^64 -
+m q) by one 64-bit add and two selects, in that order so the mask is read 2 instructions after its
+write (no s_nop).  Forward: round start 8q, 4q, 2q; final chain down to q.
 
 Register model: one asm statement per round.  The 16 values enter and leave through "+v" u64
 operands tied to x[k]; the first stage also takes u32 halves of its inputs.  Tied operands are
@@ -59,7 +64,9 @@ VBASE = int(os.environ.get("EXACTO_ASM_VBASE", "104"))   # first physical VGPR o
 W = int(os.environ.get("EXACTO_ASM_STREAMS", "2"))       # butterflies interleaved per group
 SGPR_C = [80, 82, 84, 88, 90, 92][:max(W, 2)]            # carry pair of each stream
 SGPR_SD = 86                  # sink for the carry-out of v_mad_u64_u32 where it is not used
+SGPR_RED = [80, 82, 84, 88]   # carry pairs of the generic rounds' four reduction streams
 INV_BOUND_IN = 4              # inverse round 0 input bound (the fused tensor's c1 < 4q)
+GEN_LOGN = (10, 12, 13)       # transform sizes with generic-prime rounds (cfg1: n = 1024; u64_dbfv: 4096)
 
 
 def v(i):
@@ -144,6 +151,7 @@ class Statement:
     def nq(self): return self._in("nq", "s", "K.nq")
 
     def mq(self, m): return self._in(f"mq{m}", "s", f"K.q * {m}u")
+    def nmq(self, m): return self._in(f"nmq{m}", "s", f"(u64)0 - K.q * {m}u")
     def cql(self, c): return self._in(f"q{c}l", "s", f"(uint32_t)(K.q * {c}u)")
     def cqh(self, c): return self._in(f"q{c}h", "v", f"(uint32_t)((K.q * {c}u) >> 32)")
 
@@ -199,17 +207,32 @@ def reduce_seq(st, dst, src, src_hi, t, u):
     ]
 
 
-def halve_seq(st, dst, src, m, t, c):
+def halve_seq(st, dst, src, m, t, c, halves=None):
     """dst = src - m q if src >= m q else src (pairs; any prime q < 2^60, no special form): the
-    generic reduction step of InvRound(generic=True).  t: temp pair; c: this stream's carry pair.
-    The subtraction's high word takes m q's high half from a VGPR (one SGPR read per VALU)."""
-    sl, sh = lo(src), hi(src)
+    generic reduction step of InvRound / Round(generic=True).  t: temp pair; c: this stream's mask
+    pair; halves: the source's (low, high) 32-bit operands for the selects when src is a tied 64-bit
+    operand.  The compare goes first, so its mask is read by the selects 2 instructions later and the
+    step needs no s_nop even in a single stream: c = (m q <= src), t = src + (2^64 - m q), select."""
+    sl, sh = halves if halves else (lo(src), hi(src))
     return [
-        Ins(f"v_sub_co_u32_e64 {lo(t)}, {c}, {sl}, {st.cql(m)}", wr=[c]),
-        Ins(f"v_subb_co_u32_e64 {hi(t)}, {c}, {sh}, {st.cqh(m)}, {c}", rd=[c], wr=[c]),
-        Ins(f"v_cndmask_b32_e64 {lo(dst)}, {lo(t)}, {sl}, {c}", rd=[c]),
-        Ins(f"v_cndmask_b32_e64 {hi(dst)}, {hi(t)}, {sh}, {c}", rd=[c]),
+        Ins(f"v_cmp_le_u64_e64 {c}, {st.mq(m)}, {src}", wr=[c]),
+        Ins(f"v_lshl_add_u64 {t}, {src}, 0, {st.nmq(m)}"),
+        Ins(f"v_cndmask_b32_e64 {lo(dst)}, {sl}, {lo(t)}, {c}", rd=[c]),
+        Ins(f"v_cndmask_b32_e64 {hi(dst)}, {sh}, {hi(t)}, {c}", rd=[c]),
     ]
+
+
+def halve_chain(bound):
+    """The conditional subtractions that take a value below bound * q to [0, q): (bound / 2) q,
+    then (bound / 4) q, ... q, each halving the bound."""
+    out, b = [], bound
+    while b > 1:
+        half = 1
+        while 2 * half < b:
+            half *= 2
+        out.append(half)
+        b = half
+    return out
 
 
 def canon_seq(st, dst, r, S, M):
@@ -227,7 +250,7 @@ def emit_statement(struct, st, seq, vmax, comment, run_args):
     seq = pad_hazards(seq)
     body = "\\n\\t".join(i.text for i in seq)
     clob = [f'"v{i}"' for i in range(VBASE, vmax)]
-    clob += [f'"s{i}"' for p in SGPR_C + [SGPR_SD] for i in (p, p + 1)]
+    clob += [f'"s{i}"' for p in sorted(set(SGPR_C + SGPR_RED + [SGPR_SD])) for i in (p, p + 1)]
     clob.append('"memory"')   # keeps the next round's twiddle loads below the statement
     outs = ", ".join(f'[x{k}] "+v"(x[{k}])' for k in range(16))
     ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in st.ins)
@@ -259,7 +282,7 @@ def emit_pinned(name, st, seq, vmax, comment):
     body = "\\n\\t".join(i.text for i in seq)
     base = PIN_BASE + 32
     clob = [f'"v{i}"' for i in range(base, vmax)]
-    clob += [f'"s{i}"' for p in SGPR_C + [SGPR_SD] for i in (p, p + 1)]
+    clob += [f'"s{i}"' for p in sorted(set(SGPR_C + SGPR_RED + [SGPR_SD])) for i in (p, p + 1)]
     clob.append('"memory"')
     outs = ", ".join(f'"+v"(xl{k}), "+v"(xh{k})' for k in range(16))
     ins = ", ".join(f'[{k}] "{c}"({e})' for k, c, e in st.ins)
@@ -274,9 +297,13 @@ def emit_pinned(name, st, seq, vmax, comment):
 class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
-    def __init__(self, logn, r, approx=True, addx=True, pinned=False):
+    def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False):
         super().__init__()
         self.logn, self.r, self.approx, self.addx, self.pinned = logn, r, approx, addx, pinned
+        # generic: any prime q < 2^60 (the HPS primes): the round-start reduction of X from < 16q to
+        # < 2q is three conditional subtractions (8q, 4q, 2q; halve_seq) instead of the special-prime
+        # fold, and the final canonical reduction a chain of them down to q
+        self.generic = generic
         self.c = 3 if approx else 2            # Shoup output bound (units of q)
         self.lo = max(logn - 4 * (r + 1), 0)
         self.bhi = logn - 1 - 4 * r
@@ -285,7 +312,8 @@ class Round(Statement):
         nst = self.bhi - self.lo + 1
         # bound of the round's outputs (units of q): X < 1 (round 0, canonical input) or < 2
         # (reduced at round start), plus c per stage
-        self.bound_out = 1 if self.last else (1 if r == 0 else 2) + self.c * nst
+        self.bound_last = (1 if r == 0 else 2) + self.c * nst   # before a final reduction
+        self.bound_out = 1 if self.last else self.bound_last
 
     def tw(self, slot, part):
         c = "s" if self.uniform_tw else "v"
@@ -331,14 +359,24 @@ class Round(Statement):
         xop = {k: (vp(P[k]) if self.pinned else f"%[x{k}]") for k in range(16)}
         in_p = {k: self.pinned for k in range(16)}
 
+        # the generic reductions run as four streams (carry pairs SGPR_RED, temp pairs B and E of
+        # the two butterfly temp sets, free outside the butterflies) so that no carry read waits
+        red_t = [vp(temps[0]["B"]), vp(temps[1]["B"]), vp(temps[0]["E"]), vp(temps[1]["E"])]
         if self.r > 0:   # round-start reduction of the first stage's X values into P
             red = [k for k in range(16) if not (k >> first_lb) & 1]
-            streams = [[] for _ in range(len(temps))]
+            streams = [[] for _ in range(4 if self.generic else len(temps))]
             for i, k in enumerate(red):
-                j = i % len(temps)
-                t = temps[j]
+                j = i % len(streams)
+                t = temps[j % len(temps)]
                 src_hi = v(P[k] + 1) if self.pinned else self.xh(k)
-                streams[j] += reduce_seq(self, vp(P[k]), xop[k], src_hi, v(t["B"]), v(t["B"] + 1))
+                if self.generic:
+                    srch = None if self.pinned else (self.xl(k), self.xh(k))
+                    for i2, m in enumerate((8, 4, 2)):
+                        first = i2 == 0 and not self.pinned
+                        streams[j] += halve_seq(self, vp(P[k]), xop[k] if first else vp(P[k]), m, red_t[j],
+                                                sp(SGPR_RED[j]), halves=srch if first else None)
+                else:
+                    streams[j] += reduce_seq(self, vp(P[k]), xop[k], src_hi, v(t["B"]), v(t["B"] + 1))
                 in_p[k] = True
             seq += interleave(streams)
 
@@ -393,11 +431,17 @@ class Round(Statement):
 
         if self.last:
             # canonical reduction of all 16 values (< 16q) into the tied operands
-            streams = [[] for _ in range(len(temps))]
+            streams = [[] for _ in range(4 if self.generic else len(temps))]
             for k in range(16):
-                j = k % len(temps)
-                t = temps[j]
+                j = k % len(streams)
+                t = temps[j % len(temps)]
                 R = vp(P[k])
+                if self.generic:
+                    for m in halve_chain(self.bound_last):
+                        streams[j] += halve_seq(self, R, R, m, red_t[j], sp(SGPR_RED[j]))
+                    if not self.pinned:
+                        streams[j].append(Ins(f"v_lshl_add_u64 {xop[k]}, {R}, 0, 0"))
+                    continue
                 streams[j] += reduce_seq(self, R, R, v(P[k] + 1), v(t["B"]), v(t["B"] + 1))
                 streams[j] += canon_seq(self, xop[k], R, vp(t["E"]), vp(t["F"]))
             seq += interleave(streams)
@@ -409,8 +453,10 @@ class Round(Statement):
             return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
                                f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes: "
                                f"stage bits {self.bhi}..{self.lo}")
-        return emit_statement(f"FwdRoundAsm<{self.logn}, {self.r}>", self, seq, self.vmax,
-                              f"round {self.r} of the {1 << self.logn}-point forward NTT: stage bits "
+        struct = "FwdRoundGenAsm" if self.generic else "FwdRoundAsm"
+        return emit_statement(f"{struct}<{self.logn}, {self.r}>", self, seq, self.vmax,
+                              f"round {self.r} of the {1 << self.logn}-point forward NTT"
+                              f"{' for any prime below 2^60' if self.generic else ''}: stage bits "
                               f"{self.bhi}..{self.lo}",
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
 
@@ -515,11 +561,13 @@ class InvRound(Statement):
                             half = 1
                             while 2 * half < bnd[kr]:
                                 half *= 2            # bnd[kr] in (half, 2 half]: subtract half q
-                            if loc[kr] is None:
+                            if loc[kr] is None:   # the first step reads the tied operand
                                 dst = alloc()
-                                s += [Ins(f"v_lshl_add_u64 {dst}, %[x{kr}], 0, 0")]
+                                s += halve_seq(self, dst, f"%[x{kr}]", half, t["B"], c,
+                                               halves=(self.xl(kr), self.xh(kr)))
                                 loc[kr] = dst
-                            s += halve_seq(self, loc[kr], loc[kr], half, t["B"], c)
+                            else:
+                                s += halve_seq(self, loc[kr], loc[kr], half, t["B"], c)
                             bnd[kr] = half
                             continue
                         if loc[kr] is None:
@@ -761,8 +809,8 @@ class MulPair(Statement):
 
 
 HEADER = """// GENERATED by tools/gen_ntt_asm.py -- do not edit.
-// Hand-scheduled forward / inverse NTT rounds for primes in (2^60 - 2^32, 2^60); see the
-// generator's docstring.  Included inside namespace exacto by ntt.hip.
+// Hand-scheduled forward / inverse NTT rounds for primes in (2^60 - 2^32, 2^60), and generic-prime
+// rounds for any q < 2^60; see the generator's docstring.  Included inside namespace exacto by ntt.hip.
 #pragma once
 
 // Emitted forms (measured, DESIGN.md §4): the approximate Shoup quotient (no low-low partial
@@ -798,7 +846,8 @@ __device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
 
 template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
-template <int LOGN, int R> struct InvRoundGenAsm;   // any prime below 2^60 (HPS auxiliary primes)
+template <int LOGN, int R> struct InvRoundGenAsm;   // any prime below 2^60 (HPS primes)
+template <int LOGN, int R> struct FwdRoundGenAsm;   // any prime below 2^60 (HPS primes)
 template <int W> struct MulNear60Asm;
 template <int W> struct MulNear60PinAsm;   // temps below the pinned homes (kernels with EXACTO_PIN_DECL)
 template <int W> struct MulNear60PinVAsm;  // ... as asm volatile (ordered with fences and other statements)
@@ -827,6 +876,14 @@ def main():
         for rd in inv_rounds_pinned(logn, approx):
             parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
+    for logn in GEN_LOGN:   # the generic-prime forward rounds (and n = 1024's inverse rounds)
+        for r in range((logn + 3) // 4):
+            parts.append(Round(logn, r, approx, addx, generic=True).emit())
+            parts.append("\n")
+        if logn not in (12, 13):
+            for rd in inv_rounds(logn, approx, generic=True):
+                parts.append(InvRound(logn, rd.r, rd.bound_in, approx, generic=True).emit())
+                parts.append("\n")
     with open(OUT, "w") as f:
         f.write("".join(parts).rstrip("\n") + "\n")
     print("wrote", OUT)
