@@ -139,21 +139,32 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     logn = n.bit_length() - 1
     on = lambda k: env.get(k, "1") != "0"
     _, moduli, aux, *_ = CONFIGS[cfg]
+    gen = logn in (10, 12, 13) and on("EXACTO_NTT_GEN")   # generated generic-prime rounds
     if aux:   # HPS: generic kernels for the primes outside (2^60 - 2^32, 2^60)
         primes = list(moduli) + list(aux)
-        gfwd, ginv = f"ntt_fwd_kernel<{logn}, true>", f"ntt_inv_kernel<{logn}, true>"
+        lazy = max(primes) < (1 << 60)
+        if gen and lazy:
+            gfwd, ginv = f"ntt_fwd_gen_kernel<{logn}>", f"ntt_inv_gen_kernel<{logn}>"
+        else:
+            gfwd, ginv = f"ntt_fwd_kernel<{logn}, true>", f"ntt_inv_kernel<{logn}, true>"
         near_q = logn in (12, 13) and _near60(moduli[0]) and on("EXACTO_NTT_ASM")
         fwd = f"ntt_fwd_pin_kernel<{logn}> + {gfwd}" if near_q else gfwd
         inv = f"ntt_inv_pin_kernel<{logn}> + {ginv}" if near_q else ginv
-        tensor = f"ntt_inv_tensor_kernel<{logn}, {'true' if max(primes) < (1 << 60) else 'false'}, false>"
+        tensor = (f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true>" if gen and lazy else
+                  f"ntt_inv_tensor_kernel<{logn}, {'true' if lazy else 'false'}, false>")
         return {0: fwd, 1: inv, 2: tensor, 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel",
                 14: "hps_extend_kernel", 15: "relin_mac_lds_kernel", 16: "hps_scale_kernel<true, *>"}
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    fwd = f"ntt_fwd_pin_kernel<{logn}>" if asm else f"ntt_fwd_kernel<{logn}, true>"
-    inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else f"ntt_inv_kernel<{logn}, true>"
+    gfwd = f"ntt_fwd_gen_kernel<{logn}>" if gen else f"ntt_fwd_kernel<{logn}, true>"
+    ginv = f"ntt_inv_gen_kernel<{logn}>" if gen else f"ntt_inv_kernel<{logn}, true>"
+    fwd = f"ntt_fwd_pin_kernel<{logn}>" if asm else gfwd
+    inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else ginv
     tp = env.get("EXACTO_TENSOR_PIN", "")
     pin = asm and on("EXACTO_NTT_ASM_INV") and (tp != "0" if tp else logn == 13)
-    tensor = f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor_kernel<{logn}, true, true>"
+    if asm and on("EXACTO_NTT_ASM_INV"):
+        tensor = f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor_kernel<{logn}, true, true>"
+    else:
+        tensor = f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true>" if gen else f"ntt_inv_tensor_kernel<{logn}, true, false>"
     polymul = f"ntt_polymul_kernel<{logn}>"
     return {0: fwd, 1: inv, 2: tensor, 3: polymul, 4: f"exact_lift_sp_kernel<{L}>",
             5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
