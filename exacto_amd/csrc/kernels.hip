@@ -908,6 +908,15 @@ __device__ __forceinline__ u64 hps_round_mod(u64 a, u64 q, u64 p, u64 pc) {
     return (neg && e) ? q - e : e;
 }
 
+// hps_round_mod on a value already centred: |a_c| and its sign
+__device__ __forceinline__ u64 hps_round_mag(u64 mag, bool neg, u64 q, u64 p, u64 pc) {
+    u64 e = mulhi64(mag, pc);
+    u64 r = p * mag + (q >> 1) - e * q;                   // exact: the true value is in [0, 3q)
+    if (r >= q) { ++e; r -= q; }
+    if (r >= q) ++e;
+    return (neg && e) ? q - e : e;
+}
+
 __device__ __forceinline__ u64 hps_ext_fast(u64 a, u64 q, const PrimeConst& P) {
     // eval.rs:307-313 with reduce64 instead of the % of a runtime divisor
     if (a > q / 2) {
@@ -929,11 +938,14 @@ __device__ __forceinline__ u64 hps_ext(u64 a, u64 q, u64 pj) {
 // Scaled component c of one item, coefficient j (eval.rs:257-413).  The third component's balanced
 // gadget digits go to D as residues mod q ([item][g][n]) or, with DT = int16_t / int8_t, to D16 as
 // signed digits (gadget base <= 2^16 / 2^8; dBFV sums them per output limb before one key switch).
-template <bool FAST, typename DT>
+// KK (FAST only): the number of auxiliary primes, 1 or 2, as a compile-time constant (0: K at run
+// time, the literal path).
+template <bool FAST, typename DT, int KK = 0>
 __global__ void __launch_bounds__(TPB)
 hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                 u64* __restrict__ D, DT* __restrict__ D16, int guse, int n, int K,
+                 u64* __restrict__ D, DT* __restrict__ D16, int guse, int n, int K_,
                  const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    const int K = KK ? KK : K_;
     ROW_SETUP(n)
     const long item = row / 3;
     const int comp = (int)(row - item * 3);
@@ -945,13 +957,21 @@ hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, 
     u64 result;
     if (FAST) {
         const PrimeConst& Pq = primes[0];
-        const u64 rq = hps_round_mod(a, q, p, C->hps_pc);
+        // a centred once: |a_c| feeds the rounding and the extension to every auxiliary prime
+        const bool aneg = a > (q >> 1);
+        const u64 amag = aneg ? q - a : a;
+        const u64 rq = hps_round_mag(amag, aneg, q, p, C->hps_pc);
+        // a_c mod p_j (eval.rs:307-313): |a_c| < q/2 needs no reduction when q <= p_j (block-uniform)
+        auto ext = [&](const PrimeConst& P) {
+            const u64 m = q <= P.q ? amag : reduce64(amag, P.q, P.mu64);
+            return (aneg && m) ? P.q - m : m;
+        };
         u64 mq;   // m mod q, Euclidean
         if (K == 1) {
             // eval.rs:301-332
             const PrimeConst& P1 = primes[1];
             const u64 bp = P1.q;
-            const u64 diff = sub_mod(Tin[n], hps_ext_fast(a, q, P1), bp);
+            const u64 diff = sub_mod(Tin[n], ext(P1), bp);
             const u64 m_raw = shoup_mul_red(diff, C->hps_qinv[0], C->hps_qinv_s[0], bp);
             const bool mneg = m_raw > bp / 2;
             const u64 mag = mneg ? bp - m_raw : m_raw;
@@ -963,10 +983,8 @@ hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, 
             // t0 p1 + t1 p0 < 2P decides how many P to subtract (k = 0, 1, 2: the Euclidean residue,
             // then the centring), and m mod q = t0 (p1 mod q) + t1 (p0 mod q) - k (P mod q).
             const u64 p0 = primes[1].q, p1 = primes[2].q;
-            const u64 t0 = shoup_mul_red(sub_mod(Tin[n], hps_ext_fast(a, q, primes[1]), p0), C->hps_t_w[0],
-                                         C->hps_t_ws[0], p0);
-            const u64 t1 = shoup_mul_red(sub_mod(Tin[2L * n], hps_ext_fast(a, q, primes[2]), p1), C->hps_t_w[1],
-                                         C->hps_t_ws[1], p1);
+            const u64 t0 = shoup_mul_red(sub_mod(Tin[n], ext(primes[1]), p0), C->hps_t_w[0], C->hps_t_ws[0], p0);
+            const u64 t1 = shoup_mul_red(sub_mod(Tin[2L * n], ext(primes[2]), p1), C->hps_t_w[1], C->hps_t_ws[1], p1);
             const u128 bigp = ((u128)C->hps_P[1] << 64) | C->hps_P[0];
             const u128 halfp = ((u128)C->hps_halfP[1] << 64) | C->hps_halfP[0];
             u128 mc = (u128)t0 * p1 + (u128)t1 * p0;           // < 2 P
@@ -1032,12 +1050,14 @@ void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, 
                       hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-#define HPS_(F, DT) hipLaunchKernelGGL((hps_scale_kernel<F, DT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, \
-                                       ncomp_r, D, (DT*)D16, guse, n, K, ct, primes)
-    if (fast) {
-        if (d8) HPS_(true, int8_t); else HPS_(true, int16_t);
+#define HPS_(F, DT, KK) hipLaunchKernelGGL((hps_scale_kernel<F, DT, KK>), dim3(blocks), dim3(TPB), 0, s, T, R, \
+                                           r_stride, ncomp_r, D, (DT*)D16, guse, n, K, ct, primes)
+    if (fast && K == 1) {
+        if (d8) HPS_(true, int8_t, 1); else HPS_(true, int16_t, 1);
+    } else if (fast && K == 2) {
+        if (d8) HPS_(true, int8_t, 2); else HPS_(true, int16_t, 2);
     } else {
-        if (d8) HPS_(false, int8_t); else HPS_(false, int16_t);
+        if (d8) HPS_(false, int8_t, 0); else HPS_(false, int16_t, 0);
     }
 #undef HPS_
 }
