@@ -106,6 +106,8 @@ def parse(argv=None):
     ap.add_argument("--reps", type=int, default=0, help="batches per step (0 = from --min-time)")
     ap.add_argument("--dry", action="store_true", help="no HIP calls: CPU/gloo stand-in of the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the batch-1 latency block (PMC passes: only full-batch dispatches)")
     ap.add_argument("--cpu-sample", type=int, default=0, help="units timed for the CPU baseline (0 = auto)")
     return ap.parse_args(argv)
 
@@ -614,7 +616,7 @@ def main():
         roofline, ntt, kernels = roofline_block(ctx, lambda: one(0), args.config, n, L, S)
 
     latency = None
-    if one_single is not None and not args.dry and world == 1:
+    if one_single is not None and not args.dry and world == 1 and not args.no_latency:
         latency = latency_block(one_single, sync)
         if args.config in PUBLISHED:
             pub = PUBLISHED[args.config]

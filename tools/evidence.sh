@@ -23,7 +23,7 @@ B="python3 $R/bench.py --config $CFG --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/prof_dual -o run --output-format csv -- $B > $E/prof_dual.log 2>&1
 EXACTO_DUAL_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/prof_single -o run --output-format csv -- $B > $E/prof_single.log 2>&1
 python3 $R/tools/trace_steady.py $(ls $E/prof_single/*kernel_trace.csv $E/prof_single/*/*kernel_trace.csv 2>/dev/null | head -1) > $E/steady.json
-P="python3 $R/bench.py --config $CFG --no-cpu-baseline --steps 2 --warmup 1 --reps 1 $*"
+P="python3 $R/bench.py --config $CFG --no-cpu-baseline --no-latency --steps 2 --warmup 1 --reps 1 $*"
 C="python3 $R/tools/ntt_bench.py --polys 16384 --reps 2"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $E/cal_fetch -o run --output-format csv -- $C > $E/cal_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $E/cal_write -o run --output-format csv -- $C > $E/cal_write.log 2>&1

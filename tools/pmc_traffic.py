@@ -56,10 +56,16 @@ if cf:
                           "write_factor_measured": known / (1024 * med(wk)) if wk else None}
 fetch = per_dispatch(os.path.join(out, "fetch"), "FETCH_SIZE")
 write = per_dispatch(os.path.join(out, "write"), "WRITE_SIZE")
-# The passes run the bench command, whose latency block adds batch-1 calls (small grids) to the
-# batches the roofline is about: the averages are per grid size, and the kernel's top-level figures
-# are those of its LARGEST grid (a full batch, the launches bench.py times).
-res["note"] = "top-level figures per kernel: its dispatches of the largest grid size; by_grid: all sizes"
+# The passes run the bench command with --no-latency (tools/evidence.sh), so every dispatch belongs
+# to a full batch.  A full batch launches several sizes (e.g. a 7168-product chunk and a 1024-product
+# rest, or transforms of different polynomial counts) and bench.py's algorithmic bytes per launch
+# average over that mix: the top-level figures average every dispatch, weighted by dispatch;
+# "largest_grid" keeps the largest size alone.  (A run with the latency block also holds batch-1
+# dispatches: pass --min-grid-frac F to drop grids below F x the largest.)
+MIN_FRAC = float(sys.argv[sys.argv.index("--min-grid-frac") + 1]) if "--min-grid-frac" in sys.argv else 0.0
+res["note"] = ("top-level figures per kernel: averages over all its dispatches of a bench.py --no-latency run "
+               "(the launch mix bench.py averages its algorithmic bytes over); largest_grid: that size alone; "
+               "by_grid: every size")
 for name in sorted(set(fetch) | set(write)):
     fd, wd = fetch.get(name, {}), write.get(name, {})
     if not fd or not wd:
@@ -74,8 +80,14 @@ for name in sorted(set(fetch) | set(write)):
                         "traffic_bytes_avg": sum(rd) / len(rd) + sum(wr) / len(wr)}
     if not by:
         continue
-    top = dict(by[max(by)])
-    top["grid_threads"] = max(by)
+    big = max(by)
+    mix = [g for g in by if g >= MIN_FRAC * big]
+    nd = sum(by[g]["dispatches"] for g in mix)
+    top = {"dispatches": nd}
+    for key in ("read_bytes_avg", "write_bytes_avg", "traffic_bytes_avg"):
+        top[key] = sum(by[g][key] * by[g]["dispatches"] for g in mix) / nd
+    top["grid_threads_mix"] = sorted(mix)
+    top["largest_grid"] = dict(by[big], grid_threads=big)
     if len(by) > 1:
         top["by_grid"] = {str(g): v for g, v in by.items()}
     res["kernels"][name] = top

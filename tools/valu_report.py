@@ -31,12 +31,18 @@ for d in sys.argv[2:]:
             vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
             names[k] = r["Kernel_Name"].split("(")[0].replace("void ", "")
             grids[k] = int(r.get("Grid_Size") or 0)
-# the bench command's latency block adds batch-1 dispatches (small grids): keep each kernel's
-# dispatches of its largest grid size (the full batches the roofline is about)
+# the passes run bench.py --no-latency (tools/evidence.sh, tools/r4_pmc.sh): every dispatch is part
+# of a full batch, and the averages are over all of them (the launch mix bench.py's own per-launch
+# averages cover).  --min-grid-frac F drops grids below F x the kernel's largest (a run that still
+# has the batch-1 latency block).
+MIN_FRAC = float(sys.argv[sys.argv.index("--min-grid-frac") + 1]) if "--min-grid-frac" in sys.argv else 0.0
+if "--min-grid-frac" in sys.argv:
+    i = sys.argv.index("--min-grid-frac")
+    del sys.argv[i:i + 2]
 top = {}
 for k, nm in names.items():
     top[nm] = max(top.get(nm, 0), grids[k])
-vals = {k: v for k, v in vals.items() if grids[k] == top[names[k]]}
+vals = {k: v for k, v in vals.items() if grids[k] >= MIN_FRAC * top[names[k]]}
 # the passes are separate runs of the same program: dispatch ids line up per kernel name in order
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for k, v in sorted(vals.items()):
