@@ -145,20 +145,25 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     if aux:   # HPS: generic kernels for the primes outside (2^60 - 2^32, 2^60)
         primes = list(moduli) + list(aux)
         lazy = max(primes) < (1 << 60)
+        # the smaller-prime instances (ntt.hip gen_qb): compact_bfv's primes below 2^50 at n = 1024,
+        # u64_dbfv's auxiliary primes below 2^56 at n = 4096 (the transform batches hold only those)
+        qb = {10: 50, 12: 56}.get(logn, 60) if on("EXACTO_NTT_GENQ") else 60
+        qsmall = qb if max(aux) < (1 << qb) else 60
         if gen and lazy:
-            gfwd, ginv = f"ntt_fwd_gen_kernel<{logn}>", f"ntt_inv_gen_kernel<{logn}>"
+            gfwd, ginv = f"ntt_fwd_gen_kernel<{logn}, {qsmall}>", f"ntt_inv_gen_kernel<{logn}, {qsmall}>"
         else:
             gfwd, ginv = f"ntt_fwd_kernel<{logn}, true>", f"ntt_inv_kernel<{logn}, true>"
         near_q = logn in (12, 13) and _near60(moduli[0]) and on("EXACTO_NTT_ASM")
         fwd = f"ntt_fwd_pin_kernel<{logn}> + {gfwd}" if near_q else gfwd
         inv = f"ntt_inv_pin_kernel<{logn}> + {ginv}" if near_q else ginv
-        tensor = (f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true>" if gen and lazy else
+        tq = qb if max(primes) < (1 << qb) else 60
+        tensor = (f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true, {tq}>" if gen and lazy else
                   f"ntt_inv_tensor_kernel<{logn}, {'true' if lazy else 'false'}, false>")
         return {0: fwd, 1: inv, 2: tensor, 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel",
                 14: "hps_extend_kernel", 15: "relin_mac_lds_kernel", 16: "hps_scale_kernel<true, *>"}
     asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    gfwd = f"ntt_fwd_gen_kernel<{logn}>" if gen else f"ntt_fwd_kernel<{logn}, true>"
-    ginv = f"ntt_inv_gen_kernel<{logn}>" if gen else f"ntt_inv_kernel<{logn}, true>"
+    gfwd = f"ntt_fwd_gen_kernel<{logn}, 60>" if gen else f"ntt_fwd_kernel<{logn}, true>"
+    ginv = f"ntt_inv_gen_kernel<{logn}, 60>" if gen else f"ntt_inv_kernel<{logn}, true>"
     fwd = f"ntt_fwd_pin_kernel<{logn}>" if asm else gfwd
     inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else ginv
     tp = env.get("EXACTO_TENSOR_PIN", "")
@@ -166,7 +171,7 @@ def kernel_names(n, L, S, cfg, env=os.environ):
     if asm and on("EXACTO_NTT_ASM_INV"):
         tensor = f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor_kernel<{logn}, true, true>"
     else:
-        tensor = f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true>" if gen else f"ntt_inv_tensor_kernel<{logn}, true, false>"
+        tensor = f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true, 60>" if gen else f"ntt_inv_tensor_kernel<{logn}, true, false>"
     polymul = f"ntt_polymul_kernel<{logn}>"
     return {0: fwd, 1: inv, 2: tensor, 3: polymul, 4: f"exact_lift_sp_kernel<{L}>",
             5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",

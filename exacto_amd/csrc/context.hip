@@ -1047,11 +1047,13 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     // algorithmic bytes: one read of the source (int16 digits: 2 B per coefficient) + one 8 B write
     ProfScope ps(c, inverse ? PK_INV : PK_FWD, (u64)count, ((nb.src16 ? 2.0 : 8.0) + 8.0) * c->n * (double)count);
     bool lazy = true, near60 = c->ntt_asm;
+    int qbits = 0;   // bit length of the batch's largest prime
     for (int t = nb.prime_base; t < nb.prime_base + nb.period; ++t) {
         lazy &= c->primes[t] < (1ull << 60);
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 32);
+        qbits = std::max(qbits, 64 - __builtin_clzll(c->primes[t]));
     }
-    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, near60 && c->ntt_asm_inv);
+    launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, near60 && c->ntt_asm_inv, qbits);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1059,7 +1061,9 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
 static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only = false) {
     const int NP = c->L + c->K;
     bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
+    int qbits = 0;
     for (int t = 0; t < NP; ++t) {
+        qbits = std::max(qbits, 64 - __builtin_clzll(c->primes[t]));
         lazy &= c->primes[t] < (1ull << 60);
         // the fused product (mulmod_near60) needs d = 2^60 - q < 2^24; the asm rounds d < 2^32
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
@@ -1069,7 +1073,8 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
     const double pb = 8.0 * c->n;
     const double per_item = p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP;
     ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), per_item * cnt);
-    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only);
+    launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
+                      qbits);
     CHECK_LAUNCH();
     return 0;
 }

@@ -75,8 +75,9 @@ struct CrtTables {
 // lazy: every prime of the batch is < 2^60 (forward NTT skips per-butterfly reductions)
 // asm_fwd / asm_inv: every prime of the batch is in (2^60 - 2^32, 2^60): the forward / inverse
 // transforms at n = 4096 / 8192 run the pinned-home kernels over the generated rounds (ntt_asm.inc)
+// qbits: bit length of the batch's largest prime (the generic kernels' smaller-prime forms)
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd = false, bool asm_inv = false);
+                hipStream_t s, bool asm_fwd = false, bool asm_inv = false, int qbits = 64);
 
 void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
                              hipStream_t s);
@@ -145,7 +146,8 @@ void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period,
 // p2only: every component of the ciphertext primes, the third only of the auxiliary primes (dBFV
 // psum; asm_inv and n = 4096 / 8192 only)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false);
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false,
+                       int qbits = 64);
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);

@@ -294,8 +294,8 @@ __device__ __forceinline__ void lds_load_x(const u64* lds, u64 (&x)[16], int tid
     for (int k = 0; k < 16; ++k) x[k] = *reinterpret_cast<const u64*>(lb + (b ^ (swz(k << LO) << 3)));
 }
 
-// GEN: the generic-prime statements (FwdRoundGenAsm: any prime below 2^60; the HPS primes).
-template <int LOGN, int R, bool GEN = false>
+// GEN: the generic-prime statements (FwdRoundGenAsm: any prime below 2^QB; the HPS primes).
+template <int LOGN, int R, bool GEN = false, int QB = 60>
 __device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
@@ -311,9 +311,9 @@ __device__ __forceinline__ void fwd_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
         lds_barrier();
         lds_load_x<LO>(lds, x, t2);
     }
-    if constexpr (GEN) FwdRoundGenAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (GEN) FwdRoundGenAsm<LOGN, R, QB>::run(x, tw, K);
     else FwdRoundAsm<LOGN, R>::run(x, tw, K);
-    if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1, GEN>(x, lds, tid, tab, K);
+    if constexpr (LO > 0) fwd_rounds_asm<LOGN, R + 1, GEN, QB>(x, lds, tid, tab, K);
 }
 
 // ---------------------------------------------------------------- inverse
@@ -457,7 +457,7 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // convention, twiddle layout and LDS exchanges as inv_rounds.
 // GEN: the generic-prime statements (InvRoundGenAsm: any prime below 2^60, conditional-subtraction
 // reductions; the HPS auxiliary primes), same layout and bounds contract.
-template <int LOGN, int R, bool GEN = false>
+template <int LOGN, int R, bool GEN = false, int QB = 60>
 __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -473,10 +473,16 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
         lds_barrier();
         lds_load_x<LO>(lds, x, t2);
     }
-    if constexpr (GEN) InvRoundGenAsm<LOGN, R>::run(x, tw, K);
+    if constexpr (GEN) InvRoundGenAsm<LOGN, R, QB>::run(x, tw, K);
     else InvRoundAsm<LOGN, R>::run(x, tw, K);
-    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1, GEN>(x, lds, tid, tab, K);
+    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1, GEN, QB>(x, lds, tid, tab, K);
 }
+
+// The smaller-prime forms of the generic rounds (tools/gen_ntt_asm.py GEN_QBITS): a batch whose
+// primes are all below 2^gen_qb<LOGN>() takes rounds with fewer reductions (the values' headroom
+// below 2^64 is larger); the host picks the kernel instance (launch_ntt / launch_inv_tensor: qbits).
+template <int LOGN>
+constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
 
 // The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread): each
 // thread loads its 16 consecutive words (8 x 16 B).  (Coalesced 8-B loads transposed through LDS
@@ -648,7 +654,7 @@ __device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
 // Forward NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not all of the
 // 2^60 - d form (the HPS primes): ntt_fwd_kernel's loads, the generated generic-prime rounds
 // (FwdRoundGenAsm, canonical outputs) and coalesced stores (element tid + k T through LDS).
-template <int LOGN>
+template <int LOGN, int QB = 60>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
 ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
@@ -663,7 +669,7 @@ ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     u64 x[16];
     load_coeffs<N>(x, nb, src, item, sub, P.q, tid);
-    fwd_rounds_asm<LOGN, 0, true>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
+    fwd_rounds_asm<LOGN, 0, true, QB>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
     lds_barrier();
     lds_store_x<0>(lds, x, tid);
     lds_barrier();
@@ -674,7 +680,7 @@ ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 
 // Inverse NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not of the 2^60 - d form
 // (HPS auxiliary primes): ntt_inv_kernel with the generated generic-prime rounds (InvRoundGenAsm).
-template <int LOGN>
+template <int LOGN, int QB = 60>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
 ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
@@ -689,7 +695,7 @@ ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     u64 x[16];
     load_rows16<N>(x, src, tid);
-    inv_rounds_asm<LOGN, 0, true>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
+    inv_rounds_asm<LOGN, 0, true, QB>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
@@ -859,7 +865,7 @@ __device__ __forceinline__ void tensor_unit(int rem, int L, int p2only, int& t, 
 // after the transform: 296 -> 357 us, removed.)
 // GEN (n = 4096 / 8192, every prime below 2^60 but not all 2^60 - d: HPS): lazy Barrett products,
 // then the generated generic-prime inverse rounds (InvRoundGenAsm) instead of the C++ ones.
-template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false>
+template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false, int QB = 60>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
@@ -964,7 +970,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         // no transform: the products are stored as they are
     } else if constexpr (ASM || GEN) {
         const AsmK AK = make_asmk_inv(P);
-        inv_rounds_asm<LOGN, 0, GEN>(x, lds, tid, tw_table(P.tw_inv), AK);
+        inv_rounds_asm<LOGN, 0, GEN, QB>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
@@ -1276,15 +1282,23 @@ static bool tensor_pin_at(int logn) {
     return on < 0 ? logn == 13 : on && (logn == 12 || logn == 13);
 }
 
-// EXACTO_NTT_GEN=0: the C++ generic-prime inverse rounds instead of the generated ones (A/B switch)
+// EXACTO_NTT_GEN=0: the C++ generic-prime inverse rounds instead of the generated ones (A/B switch).
 static bool ntt_gen_on() {
     static const int on = env_switch("EXACTO_NTT_GEN", 1);
     return on != 0;
 }
 
+// the smaller-prime generic rounds apply: every prime of the batch below 2^gen_qb<LOGN>().
+// EXACTO_NTT_GENQ=0: never (A/B switch)
+template <int LOGN>
+static bool gen_small(int qbits) {
+    static const int on = env_switch("EXACTO_NTT_GENQ", 1);
+    return on && gen_qb<LOGN>() < 60 && qbits <= gen_qb<LOGN>();
+}
+
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -1304,8 +1318,12 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
     }
     if constexpr (LOGN == 10 || LOGN == 12 || LOGN == 13) {
         if (lazy && !p2only && ntt_gen_on()) {   // every prime below 2^60: the generated generic-prime rounds
-            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0, s,
-                               op, extP, T, L, K, primes, remap);
+            if (gen_small<LOGN>(qbits))
+                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true, gen_qb<LOGN>()>), dim3(blocks),
+                                   dim3(threads), 0, s, op, extP, T, L, K, primes, remap);
+            else
+                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0,
+                                   s, op, extP, T, L, K, primes, remap);
             return;
         }
     }
@@ -1318,7 +1336,7 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
@@ -1333,17 +1351,17 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 7: launch_it<7>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 8: launch_it<8>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s); break;
+        case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s, false, 0, qbits); break;
         case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv); break;
-        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }
 }
 
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
-                hipStream_t s, bool asm_fwd, bool asm_inv) {
+                hipStream_t s, bool asm_fwd, bool asm_inv, int qbits) {
     if (count <= 0) return;
     // n = 4096 / 8192, every prime of the batch in (2^60 - 2^32, 2^60): the pinned-home kernels (the
     // non-pinned asm kernels and the persistent LDS-DMA forward kernel measured slower and were removed,
@@ -1360,15 +1378,17 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
     }
     if (lazy && (logn == 10 || logn == 12 || logn == 13) && ntt_gen_on()) {   // every prime below 2^60: generic asm rounds
         const dim3 th(1u << (logn - 4));
+#define GEN_NTT_(K_, LG_, QB_) hipLaunchKernelGGL((K_<LG_, QB_>), dim3(count), th, 0, s, nb, primes)
         if (inverse) {
-            if (logn == 10) hipLaunchKernelGGL((ntt_inv_gen_kernel<10>), dim3(count), th, 0, s, nb, primes);
-            else if (logn == 12) hipLaunchKernelGGL((ntt_inv_gen_kernel<12>), dim3(count), th, 0, s, nb, primes);
-            else hipLaunchKernelGGL((ntt_inv_gen_kernel<13>), dim3(count), th, 0, s, nb, primes);
+            if (logn == 10) { if (gen_small<10>(qbits)) GEN_NTT_(ntt_inv_gen_kernel, 10, 50); else GEN_NTT_(ntt_inv_gen_kernel, 10, 60); }
+            else if (logn == 12) { if (gen_small<12>(qbits)) GEN_NTT_(ntt_inv_gen_kernel, 12, 56); else GEN_NTT_(ntt_inv_gen_kernel, 12, 60); }
+            else GEN_NTT_(ntt_inv_gen_kernel, 13, 60);
         } else {
-            if (logn == 10) hipLaunchKernelGGL((ntt_fwd_gen_kernel<10>), dim3(count), th, 0, s, nb, primes);
-            else if (logn == 12) hipLaunchKernelGGL((ntt_fwd_gen_kernel<12>), dim3(count), th, 0, s, nb, primes);
-            else hipLaunchKernelGGL((ntt_fwd_gen_kernel<13>), dim3(count), th, 0, s, nb, primes);
+            if (logn == 10) { if (gen_small<10>(qbits)) GEN_NTT_(ntt_fwd_gen_kernel, 10, 50); else GEN_NTT_(ntt_fwd_gen_kernel, 10, 60); }
+            else if (logn == 12) { if (gen_small<12>(qbits)) GEN_NTT_(ntt_fwd_gen_kernel, 12, 56); else GEN_NTT_(ntt_fwd_gen_kernel, 12, 60); }
+            else GEN_NTT_(ntt_fwd_gen_kernel, 13, 60);
         }
+#undef GEN_NTT_
         return;
     }
     switch (logn) {

@@ -40,6 +40,19 @@ def test_generic_rounds_match_exact_arithmetic():
                 asm_sim.check_inv_round(logn, r, q, rng, True, generic=True)
 
 
+def test_small_prime_generic_rounds_match_exact_arithmetic():
+    # FwdRoundGenAsm / InvRoundGenAsm<LOGN, R, QB < 60>: fewer reductions for q < 2^QB, at the
+    # bounds the transform's earlier rounds leave (fwd_rounds / inv_rounds chain them)
+    rng = random.Random(17)
+    for logn, qbs in gen_ntt_asm.GEN_QBITS.items():
+        for qb in qbs:
+            qs = asm_sim.generic_primes(qb)
+            for r in range((logn + 3) // 4):
+                for i in range(3 * len(qs)):
+                    asm_sim.check_round(logn, r, qs[i % len(qs)], rng, True, True, qb)
+                    asm_sim.check_inv_round(logn, r, qs[i % len(qs)], rng, True, True, qb)
+
+
 def test_tensor_products_match_exact_arithmetic():
     # MulNear60Asm: the 120-bit product folded twice through 2^60 == d, for every BASELINE prime
     # (the fifth entry of PRIMES has d = 2^32 - 3, outside the d < 2^24 this sequence needs)

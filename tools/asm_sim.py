@@ -176,11 +176,13 @@ def _inputs(rng, bound_in):
     return x
 
 
-def check_round(logn, r, q, rng, approx=True, generic=False):
-    rd = G.Round(logn, r, approx, generic=generic)
+def check_round(logn, r, q, rng, approx=True, generic=False, qbits=60):
+    if qbits < 60:
+        rd = G.fwd_rounds(logn, approx, True, generic, qbits)[r]
+    else:
+        rd = G.Round(logn, r, approx, generic=generic)
     seq = rd.gen()
-    first = r == 0
-    bound_in = q if first else 16 * q
+    bound_in = rd.bound_in * q
     x = _inputs(rng, bound_in)
     tw = [rng.randrange(q) for _ in range(15)]
     named, _, _ = _named(rd, x, tw, q, logn)
@@ -202,9 +204,9 @@ def check_round(logn, r, q, rng, approx=True, generic=False):
             assert got[k] < rd.bound_out * q, ("bound", logn, r, k, got[k] / q)
 
 
-def check_inv_round(logn, r, q, rng, approx=True, generic=False):
-    rd = G.inv_rounds(logn, approx, generic)[r]
-    rd = G.InvRound(logn, r, rd.bound_in, approx, generic)
+def check_inv_round(logn, r, q, rng, approx=True, generic=False, qbits=60):
+    rd = G.inv_rounds(logn, approx, generic, qbits)[r]
+    rd = G.InvRound(logn, r, rd.bound_in, approx, generic, qbits)
     seq = rd.gen()
     x = _inputs(rng, rd.bound_in * q)
     tw = [rng.randrange(q) for _ in range(15)]
@@ -307,6 +309,11 @@ GENERIC_PRIMES = [1099509805057, 562949953443841, 18014398509998081, 36028797018
                   (1 << 60) - 1, (1 << 59) + 12345, (1 << 30) + 3] + PRIMES[:2]
 
 
+def generic_primes(qbits):
+    """The generic test primes below 2^qbits, and odd values at the top of that range."""
+    return [q for q in GENERIC_PRIMES if q < (1 << qbits)] + [(1 << qbits) - 1, (1 << qbits) - 12345]
+
+
 def main():
     trials = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     rng = random.Random(1)
@@ -324,6 +331,12 @@ def main():
                 q = GENERIC_PRIMES[i % len(GENERIC_PRIMES)]
                 check_round(logn, r, q, rng, True, generic=True)
                 check_inv_round(logn, r, q, rng, True, generic=True)
+        for qb in G.GEN_QBITS.get(logn, ()):
+            qs = generic_primes(qb)
+            for r in range((logn + 3) // 4):
+                for i in range(trials):
+                    check_round(logn, r, qs[i % len(qs)], rng, True, True, qb)
+                    check_inv_round(logn, r, qs[i % len(qs)], rng, True, True, qb)
     for i in range(trials):
         for w in (1, 2):
             check_mulpair(w, PRIMES[i % 4], rng)

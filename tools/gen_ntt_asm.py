@@ -67,6 +67,9 @@ SGPR_SD = 86                  # sink for the carry-out of v_mad_u64_u32 where it
 SGPR_RED = [80, 82, 84, 88]   # carry pairs of the generic rounds' four reduction streams
 INV_BOUND_IN = 4              # inverse round 0 input bound (the fused tensor's c1 < 4q)
 GEN_LOGN = (10, 12, 13)       # transform sizes with generic-prime rounds (cfg1: n = 1024; u64_dbfv: 4096)
+# smaller-prime forms per size (q < 2^qbits): compact_bfv's q and p (2^40, 2^49) at n = 1024,
+# u64_dbfv's auxiliary primes (2^54, 2^55) at n = 4096
+GEN_QBITS = {10: (50,), 12: (56,)}
 
 
 def v(i):
@@ -297,22 +300,34 @@ def emit_pinned(name, st, seq, vmax, comment):
 class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
-    def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False):
+    def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False, qbits=60, bound_in=None):
         super().__init__()
         self.logn, self.r, self.approx, self.addx, self.pinned = logn, r, approx, addx, pinned
         # generic: any prime q < 2^60 (the HPS primes): the round-start reduction of X from < 16q to
         # < 2q is three conditional subtractions (8q, 4q, 2q; halve_seq) instead of the special-prime
-        # fold, and the final canonical reduction a chain of them down to q
-        self.generic = generic
+        # fold, and the final canonical reduction a chain of them down to q.
+        # qbits < 60 (generic only, q < 2^qbits): values may grow to 2^64 / 2^qbits q before a
+        # reduction, so the round-start reduction is left out while the round's outputs stay below
+        # that (bound_in: the inputs' bound in units of q, from fwd_rounds)
+        self.generic, self.qbits = generic, qbits
+        self.cap = 16 if qbits >= 60 else (1 << (64 - qbits))
         self.c = 3 if approx else 2            # Shoup output bound (units of q)
         self.lo = max(logn - 4 * (r + 1), 0)
         self.bhi = logn - 1 - 4 * r
         self.last = self.lo == 0
         self.uniform_tw = self.lo + 4 >= logn     # thigh == 0: twiddles are block-uniform (SGPR)
         nst = self.bhi - self.lo + 1
-        # bound of the round's outputs (units of q): X < 1 (round 0, canonical input) or < 2
-        # (reduced at round start), plus c per stage
-        self.bound_last = (1 if r == 0 else 2) + self.c * nst   # before a final reduction
+        self.bound_in = bound_in if bound_in is not None else (1 if r == 0 else 16)
+        # X's bound at the round start: canonical in round 0; reduced to < 2q unless the round's
+        # outputs stay below cap q unreduced
+        if r == 0:
+            self.xbound, self.reduce_x = 1, False
+        elif qbits < 60 and self.bound_in + self.c * nst <= self.cap:
+            self.xbound, self.reduce_x = self.bound_in, False
+        else:
+            self.xbound, self.reduce_x = 2, True
+        # bound of the round's outputs (units of q): X's bound plus c per stage
+        self.bound_last = self.xbound + self.c * nst   # before a final reduction
         self.bound_out = 1 if self.last else self.bound_last
 
     def tw(self, slot, part):
@@ -362,7 +377,7 @@ class Round(Statement):
         # the generic reductions run as four streams (carry pairs SGPR_RED, temp pairs B and E of
         # the two butterfly temp sets, free outside the butterflies) so that no carry read waits
         red_t = [vp(temps[0]["B"]), vp(temps[1]["B"]), vp(temps[0]["E"]), vp(temps[1]["E"])]
-        if self.r > 0:   # round-start reduction of the first stage's X values into P
+        if self.reduce_x:   # round-start reduction of the first stage's X values into P
             red = [k for k in range(16) if not (k >> first_lb) & 1]
             streams = [[] for _ in range(4 if self.generic else len(temps))]
             for i, k in enumerate(red):
@@ -371,7 +386,7 @@ class Round(Statement):
                 src_hi = v(P[k] + 1) if self.pinned else self.xh(k)
                 if self.generic:
                     srch = None if self.pinned else (self.xl(k), self.xh(k))
-                    for i2, m in enumerate((8, 4, 2)):
+                    for i2, m in enumerate(halve_chain(self.bound_in)[:-1]):   # down to < 2q
                         first = i2 == 0 and not self.pinned
                         streams[j] += halve_seq(self, vp(P[k]), xop[k] if first else vp(P[k]), m, red_t[j],
                                                 sp(SGPR_RED[j]), halves=srch if first else None)
@@ -453,11 +468,13 @@ class Round(Statement):
             return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
                                f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes: "
                                f"stage bits {self.bhi}..{self.lo}")
-        struct = "FwdRoundGenAsm" if self.generic else "FwdRoundAsm"
-        return emit_statement(f"{struct}<{self.logn}, {self.r}>", self, seq, self.vmax,
+        struct = f"FwdRoundGenAsm<{self.logn}, {self.r}, {self.qbits}>" if self.generic else \
+            f"FwdRoundAsm<{self.logn}, {self.r}>"
+        return emit_statement(struct, self, seq, self.vmax,
                               f"round {self.r} of the {1 << self.logn}-point forward NTT"
-                              f"{' for any prime below 2^60' if self.generic else ''}: stage bits "
-                              f"{self.bhi}..{self.lo}",
+                              f"{f' for any prime below 2^{self.qbits}' if self.generic else ''}: stage bits "
+                              f"{self.bhi}..{self.lo}, inputs < {self.bound_in}q, "
+                              f"{'round-start reduction' if self.reduce_x else 'no round-start reduction'}",
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
 
 
@@ -465,9 +482,12 @@ class InvRound(Statement):
     """One inverse round (Gentleman-Sande, stage bits BLO..BHI ascending) as one asm statement.
     bound_in: every input value < bound_in * q."""
 
-    def __init__(self, logn, r, bound_in, approx=True, generic=False):
+    def __init__(self, logn, r, bound_in, approx=True, generic=False, qbits=60):
         super().__init__()
         self.logn, self.r, self.approx = logn, r, approx
+        # qbits < 60 (generic, q < 2^qbits): sums may reach 2^64 / 2^qbits q before a halving
+        self.qbits = qbits
+        self.cap = 16 if qbits >= 60 else (1 << (64 - qbits))
         # generic: any prime q < 2^60 (the HPS auxiliary primes): a sum that would pass 16q first
         # halves its larger operand's bound by one conditional subtraction of (bound / 2) q
         # (halve_seq, 4 VALU) instead of the special-prime fold to < 2q (reduce_seq)
@@ -552,9 +572,9 @@ class InvRound(Statement):
                     t = temps[j]
                     c = sp(C[j])
                     s = []
-                    # keep the pair sum and the difference below 16q
+                    # keep the pair sum and the difference below cap q (16q: 2^64 at q < 2^60)
                     for _ in range(8 if self.generic else 2):
-                        if bnd[k0] + bnd[k1] <= 16:
+                        if bnd[k0] + bnd[k1] <= self.cap:
                             break
                         kr = k0 if bnd[k0] >= bnd[k1] else k1
                         if self.generic:
@@ -637,10 +657,11 @@ class InvRound(Statement):
 
     def emit(self):
         seq = self.gen()
-        struct = "InvRoundGenAsm" if self.generic else "InvRoundAsm"
-        return emit_statement(f"{struct}<{self.logn}, {self.r}>", self, seq, self.vmax,
+        struct = f"InvRoundGenAsm<{self.logn}, {self.r}, {self.qbits}>" if self.generic else \
+            f"InvRoundAsm<{self.logn}, {self.r}>"
+        return emit_statement(struct, self, seq, self.vmax,
                               f"round {self.r} of the {1 << self.logn}-point inverse NTT"
-                              f"{' for any prime below 2^60' if self.generic else ''}: stage bits "
+                              f"{f' for any prime below 2^{self.qbits}' if self.generic else ''}: stage bits "
                               f"{self.blo}..{self.bhi}, inputs < {self.bound_in}q, outputs < "
                               f"{self.bound_out}q",
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
@@ -724,12 +745,23 @@ def inv_rounds_pinned(logn, approx=True):
     return out
 
 
-def inv_rounds(logn, approx=True, generic=False):
+def inv_rounds(logn, approx=True, generic=False, qbits=60):
     """The inverse rounds of one transform, each starting at the previous round's output bound."""
     out, b = [], INV_BOUND_IN
     for r in range((logn + 3) // 4):
-        rd = InvRound(logn, r, b, approx, generic)
+        rd = InvRound(logn, r, b, approx, generic, qbits)
         rd.gen()
+        out.append(rd)
+        b = rd.bound_out
+    return out
+
+
+def fwd_rounds(logn, approx=True, addx=True, generic=False, qbits=60):
+    """The forward rounds of one transform; with qbits < 60 each starts at the previous round's
+    output bound (the 60-bit forms assume < 16q, their round-start reduction's input bound)."""
+    out, b = [], None
+    for r in range((logn + 3) // 4):
+        rd = Round(logn, r, approx, addx, generic=generic, qbits=qbits, bound_in=b if qbits < 60 else None)
         out.append(rd)
         b = rd.bound_out
     return out
@@ -846,8 +878,9 @@ __device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
 
 template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
-template <int LOGN, int R> struct InvRoundGenAsm;   // any prime below 2^60 (HPS primes)
-template <int LOGN, int R> struct FwdRoundGenAsm;   // any prime below 2^60 (HPS primes)
+// any prime below 2^QB (the HPS primes; QB < 60: fewer reductions, the values' headroom is larger)
+template <int LOGN, int R, int QB = 60> struct InvRoundGenAsm;
+template <int LOGN, int R, int QB = 60> struct FwdRoundGenAsm;
 template <int W> struct MulNear60Asm;
 template <int W> struct MulNear60PinAsm;   // temps below the pinned homes (kernels with EXACTO_PIN_DECL)
 template <int W> struct MulNear60PinVAsm;  // ... as asm volatile (ordered with fences and other statements)
@@ -877,12 +910,19 @@ def main():
             parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
     for logn in GEN_LOGN:   # the generic-prime forward rounds (and n = 1024's inverse rounds)
-        for r in range((logn + 3) // 4):
-            parts.append(Round(logn, r, approx, addx, generic=True).emit())
+        for rd in fwd_rounds(logn, approx, addx, generic=True):
+            parts.append(rd.emit())
             parts.append("\n")
         if logn not in (12, 13):
             for rd in inv_rounds(logn, approx, generic=True):
                 parts.append(InvRound(logn, rd.r, rd.bound_in, approx, generic=True).emit())
+                parts.append("\n")
+        for qb in GEN_QBITS.get(logn, ()):   # smaller primes: fewer reductions
+            for rd in fwd_rounds(logn, approx, addx, generic=True, qbits=qb):
+                parts.append(rd.emit())
+                parts.append("\n")
+            for rd in inv_rounds(logn, approx, generic=True, qbits=qb):
+                parts.append(InvRound(logn, rd.r, rd.bound_in, approx, generic=True, qbits=qb).emit())
                 parts.append("\n")
     with open(OUT, "w") as f:
         f.write("".join(parts).rstrip("\n") + "\n")
