@@ -165,6 +165,7 @@ def test_rns_mul_inv_fused_matches_composition(gpu_available, n, qs):
     da = torch.from_numpy(a.view(np.int64)).cuda()
     db = torch.from_numpy(b.view(np.int64)).cuda()
     ref = da.clone()
+    torch.cuda.synchronize()  # the context's stream does not wait for torch's (the clone)
     ctx.rns_mul_dev(ref, db, ref, B)
     ctx.rns_inv_dev(ref, B)
     out = torch.empty_like(da)
@@ -201,6 +202,7 @@ def test_rns_polymul_matches_composition(gpu_available, n, qs):
     da = torch.from_numpy(a.view(np.int64)).cuda()
     db = torch.from_numpy(b.view(np.int64)).cuda()
     ra, rb = da.clone(), db.clone()
+    torch.cuda.synchronize()  # the context's stream does not wait for torch's (the clones)
     ctx.rns_fwd_dev(ra, B)
     ctx.rns_fwd_dev(rb, B)
     ctx.rns_mul_dev(ra, rb, ra, B)
