@@ -341,7 +341,7 @@ __device__ __forceinline__ void load_round_tw_inv(TwPair (&tw)[15], int tid, TwT
 __device__ __forceinline__ void halve(u64& v, int& m, u64 q) {
     const u64 t = q * (u64)(m / 2);
     v = v >= t ? v - t : v;
-    m /= 2;
+    m = (m + 1) / 2;   // v < m q -> v < ceil(m / 2) q (every m the rounds halve is even)
 }
 
 template <int LOGN, int LO, int BLO, int BHI, bool LAZY>
