@@ -425,16 +425,14 @@ hps_extend_kernel(const u64* __restrict__ coefQ, u64* __restrict__ extP, int n, 
     ROW_SETUP(n)
     const u64 q = primes[0].q;
     const u64 c = coefQ[row * n + j];
+    // centred once, branch-free: |c_c| mod p_a, negated for negative c_c; no reduction at all where
+    // q <= p_a (block-uniform: compact_bfv's 40-bit q under its 49-bit p)
+    const bool neg = c > q / 2;
+    const u64 mag = neg ? q - c : c;
     for (int a = 0; a < K; ++a) {
         const PrimeConst& P = primes[1 + a];
-        u64 r;
-        if (c > q / 2) {
-            const u64 rem = reduce64(q - c, P.q, P.mu64);
-            r = rem == 0 ? 0 : P.q - rem;
-        } else {
-            r = reduce64(c, P.q, P.mu64);
-        }
-        extP[(row * K + a) * n + j] = r;
+        const u64 rem = q <= P.q ? mag : reduce64(mag, P.q, P.mu64);
+        extP[(row * K + a) * n + j] = (neg && rem) ? P.q - rem : rem;
     }
 }
 
