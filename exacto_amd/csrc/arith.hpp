@@ -41,7 +41,20 @@ struct PrimeConst {
     u64 last_w, last_ws;       // psi_inv_rev[1] * n^-1 (fused last inverse stage)
     const TwPair* tw_fwd;      // [n] psi^brv(i)
     const TwPair* tw_inv;      // [n] psi^-brv(i)
+    // Montgomery products (R = 2^64) in the generic-prime tensor: -q^-1 mod 2^64, and the last
+    // inverse stage's two constants times R mod q (they cancel the products' R^-1)
+    u64 qinv_neg;
+    u64 n_inv_r, n_inv_rs, last_wr, last_wrs;
 };
+
+// a b R^-1 mod q in [0, 2q) (R = 2^64) for a b < q 2^64 (a, b < q): Montgomery's REDC with
+// m = lo(a b) (-q^-1) mod 2^64; (a b + m q) / 2^64 = hi(a b) + hi(m q) + (lo(a b) != 0), since the
+// low words sum to 0 or 2^64 exactly.
+__device__ __forceinline__ u64 mont_mul_lazy(u64 a, u64 b, u64 q, u64 qinv_neg) {
+    const u64 lo = a * b, hi = __umul64hi(a, b);
+    const u64 m = lo * qinv_neg;
+    return hi + __umul64hi(m, q) + (lo != 0 ? 1 : 0);
+}
 
 // hi64(y * s) from 32-bit halves.  u = y1*s0 + hi(y0*s0) fits 64 bits; v = y0*s1 + u is
 // a 65-bit sum, and y*s = lo(y0*s0) + 2^32*v + 2^64*y1*s1, so hi64 = y1*s1 + (v >> 32).

@@ -438,6 +438,14 @@ static PrimeConst make_prime_const(u64 q, int n, int logn, TwPair* h_fwd, TwPair
     P.n_inv_s = shoup_h(P.n_inv, q);
     P.last_w = mulmod_h(h_inv[1].w, P.n_inv, q);
     P.last_ws = shoup_h(P.last_w, q);
+    u64 qi = q;                                   // q^-1 mod 2^64 by Newton (q odd): 6 doublings
+    for (int it = 0; it < 6; ++it) qi *= 2 - q * qi;
+    P.qinv_neg = (u64)0 - qi;
+    const u64 r = (u64)((((u128)1) << 64) % q);   // R = 2^64 mod q
+    P.n_inv_r = mulmod_h(P.n_inv, r, q);
+    P.n_inv_rs = shoup_h(P.n_inv_r, q);
+    P.last_wr = mulmod_h(P.last_w, r, q);
+    P.last_wrs = shoup_h(P.last_wr, q);
     return P;
 }
 

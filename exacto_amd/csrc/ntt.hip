@@ -911,8 +911,11 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     operands(item, t, A0, A1, B0, B1);
     // ASM: every prime is 2^60 - d with d < 2^24 (launch_inv_tensor's caller checks)
     const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
+    // GEN: Montgomery products a b R^-1 (< 2q, fewer instructions than Barrett's quotient); the
+    // generated inverse's last stage multiplies by R with its constants (make_asmk_inv_mont)
     auto mulr = [&](u64 a, u64 b) {
-        return ASM ? mulmod_near60(a, b, dq) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
+        return ASM ? mulmod_near60(a, b, dq)
+                   : GEN ? mont_mul_lazy(a, b, P.q, P.qinv_neg) : LAZY ? barrett_mul_lazy(a, b, P) : mul_mod(a, b, P);
     };
     auto load = [&](const u64* src, u64 (&v)[16]) {
         if constexpr (PROBE == 1) {
@@ -962,14 +965,15 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const u64 v = z[k] + mulr(x[k], y[k]);
-                x[k] = LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
+                // GEN: two Montgomery products < 2q each, already under the inverse's 4q
+                x[k] = GEN ? v : LAZY ? (v >= q2 ? v - q2 : v) : (v >= q ? v - q : v);
             }
         }
     }
     if constexpr (PROBE == 2) {
         // no transform: the products are stored as they are
     } else if constexpr (ASM || GEN) {
-        const AsmK AK = make_asmk_inv(P);
+        const AsmK AK = GEN ? make_asmk_inv_mont(P) : make_asmk_inv(P);
         inv_rounds_asm<LOGN, 0, GEN, QB>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);

@@ -876,6 +876,17 @@ __device__ __forceinline__ AsmK make_asmk_inv(const PrimeConst& P) {
     return K;
 }
 
+// ... with the last stage's constants times R = 2^64 mod q: the inverse of Montgomery products
+// (every input carries R^-1, which the last stage cancels)
+__device__ __forceinline__ AsmK make_asmk_inv_mont(const PrimeConst& P) {
+    AsmK K = make_asmk(P.q);
+    K.nil = (uint32_t)P.n_inv_r; K.nih = (uint32_t)(P.n_inv_r >> 32);
+    K.nsl = (uint32_t)P.n_inv_rs; K.nsh = (uint32_t)(P.n_inv_rs >> 32);
+    K.lwl = (uint32_t)P.last_wr; K.lwh = (uint32_t)(P.last_wr >> 32);
+    K.lsl = (uint32_t)P.last_wrs; K.lsh = (uint32_t)(P.last_wrs >> 32);
+    return K;
+}
+
 template <int LOGN, int R> struct FwdRoundAsm;
 template <int LOGN, int R> struct InvRoundAsm;
 // any prime below 2^QB (the HPS primes; QB < 60: fewer reductions, the values' headroom is larger)
