@@ -906,6 +906,26 @@ __device__ __forceinline__ u64 hps_round_mod(u64 a, u64 q, u64 p, u64 pc) {
     return (neg && e) ? q - e : e;
 }
 
+// gadget_digits for one ciphertext prime (HPS) and a power-of-two base 2^sh (1 <= sh <= 16), signed
+// digits only: the same digits (keyswitch.rs:24-44: truncating %, [-B/2, B/2) adjustment, final
+// carry dropped) from one word, branch-free.
+template <typename DT>
+__device__ __forceinline__ void gadget_digits_l1(u64 v, u64 q, int sh, int guse, DT* D16, int n) {
+    const bool neg = v > (q >> 1);
+    u64 M = neg ? q - v : v;                      // |centred value|
+    const u64 B = 1ull << sh, mask = B - 1, half = B >> 1;
+    for (int g = 0; g < guse; ++g) {
+        const u64 r = M & mask;
+        M >>= sh;
+        // value +M: r >= B/2 -> digit r - B and a carry; value -M: r > B/2 -> digit B - r and a carry
+        const bool carry = neg ? (r > half) : (r >= half);
+        const i64 mag = carry ? (i64)(B - r) : (i64)r;
+        const bool dneg = neg ? !carry : carry;
+        M += carry ? 1 : 0;
+        D16[(long)g * n] = (DT)(dneg ? -mag : mag);
+    }
+}
+
 // hps_round_mod on a value already centred: |a_c| and its sign
 __device__ __forceinline__ u64 hps_round_mag(u64 mag, bool neg, u64 q, u64 p, u64 pc) {
     u64 e = mulhi64(mag, pc);
@@ -1038,7 +1058,9 @@ hps_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, 
     if (comp == 2) {
         u64 res[EXACTO_MAX_L];
         res[0] = result;
-        if (D16) gadget_digits<false, 1, DT>(res, 1, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
+        if (D16 && C->gshift >= 1 && C->gshift <= 16)   // every HPS config: base 2^8 or 2^16
+            gadget_digits_l1<DT>(result, q, C->gshift, guse, D16 + item * (long)guse * n + j, n);
+        else if (D16) gadget_digits<false, 1, DT>(res, 1, C, primes, nullptr, n, guse, D16 + item * (long)guse * n + j);
         else if (D) gadget_digits<false, 1>(res, 1, C, primes, D + item * (long)guse * n + j, n, guse);
     }
 }
