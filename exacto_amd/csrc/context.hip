@@ -1081,15 +1081,8 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
     const double pb = 8.0 * c->n;
     const double per_item = p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP;
     ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), per_item * cnt);
-    int split = 0;   // ciphertext primes special, auxiliary primes generic: their bit length
-    if (lazy && !near60 && c->K > 0 && c->ntt_asm && c->ntt_asm_inv) {
-        bool qs = true;
-        for (int t = 0; t < c->L; ++t) qs &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
-        for (int t = c->L; t < NP && qs; ++t) split = std::max(split, 64 - __builtin_clzll(c->primes[t]));
-        if (!qs) split = 0;
-    }
     launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
-                      qbits, split);
+                      qbits);
     CHECK_LAUNCH();
     return 0;
 }

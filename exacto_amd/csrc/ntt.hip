@@ -869,9 +869,7 @@ template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                      const PrimeConst* __restrict__ primes, int remap, int p2only = 0, int t0 = 0, int tn = 0) {
-    // t0, tn > 0: this launch covers primes t0 .. t0 + tn - 1 of every item (a batch split by prime
-    // class, launch_it); the output layout is the whole batch's
+                      const PrimeConst* __restrict__ primes, int remap, int p2only = 0) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
@@ -884,7 +882,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     // with xcd_group_remap they run back to back on one XCD, so the second reads hit its L2
     // p2only (dBFV psum: the P residues of c0 / c1 summed by launch_dbfv_pairsum): 3L + K blocks per item, every
     // component of the ciphertext primes, the third only of the auxiliary primes
-    const int per = p2only ? 3 * L + K : 3 * (tn > 0 ? tn : NP);
+    const int per = p2only ? 3 * L + K : 3 * NP;
     // groups of 3 keep each (item, prime)'s components together only while every item's blocks are a
     // multiple of 3; p2only's 3L + K is not (cfg5: 17), so there a whole item is one group
     const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
@@ -892,7 +890,6 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     const int rem = (int)(p - item * per);
     int t, c;
     tensor_unit(rem, L, p2only, t, c);
-    t += t0;
     const PrimeConst& P = primes[t];
     // the four operand polynomials of (item, prime t)
     auto operands = [&](long it, int tt, const u64*& A0, const u64*& A1, const u64*& B0, const u64*& B1) {
@@ -1305,8 +1302,7 @@ static bool gen_small(int qbits) {
 
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64,
-                      int split = 0) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -1321,23 +1317,6 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
                                T, L, K, primes, remap, p2only);
-            return;
-        }
-    }
-    if constexpr (LOGN == 12 || LOGN == 13) {
-        // split by prime class (EXACTO_TENSOR_SPLIT=1): the L ciphertext primes (2^60 - d, d < 2^24)
-        // on the special-prime asm kernel, the K auxiliary primes (below 2^gen_qb) on the generic one
-        static const int split_on = env_switch("EXACTO_TENSOR_SPLIT", 0);
-        if (split_on && split && lazy && !p2only && ntt_gen_on()) {
-            const long items = blocks / (3 * (L + K));
-            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(items * 3 * L), dim3(threads), 0, s, op,
-                               extP, T, L, K, primes, remap, 0, 0, L);
-            if (gen_small<LOGN>(split))
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true, gen_qb<LOGN>()>),
-                                   dim3(items * 3 * K), dim3(threads), 0, s, op, extP, T, L, K, primes, remap, 0, L, K);
-            else
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(items * 3 * K),
-                                   dim3(threads), 0, s, op, extP, T, L, K, primes, remap, 0, L, K);
             return;
         }
     }
@@ -1361,7 +1340,7 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits, int split) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits) {
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
@@ -1378,8 +1357,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s, false, 0, qbits); break;
         case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, split); break;
-        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, split); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }

@@ -29,7 +29,6 @@ VARIANTS = {
     "ntt_asm_off": ({"EXACTO_NTT_ASM": "0"}, ["cfg3", "cfg5", "hps"]),
     "ntt_asm_inv_off": ({"EXACTO_NTT_ASM_INV": "0"}, ["cfg3", "cfg5", "hps"]),
     "ntt_gen_off": ({"EXACTO_NTT_GEN": "0"}, ["hps"]),
-    "tensor_split": ({"EXACTO_TENSOR_SPLIT": "1"}, ["hps"]),
     "ntt_genq_off": ({"EXACTO_NTT_GENQ": "0"}, ["hps"]),
     # no asm at all: the special primes then take the C++ rounds too (with NTT_ASM=0 alone they take
     # the generic-prime asm rounds)
