@@ -437,6 +437,11 @@ def main():
     # relinearisation key: made on rank 0 only, broadcast by the library's RCCL into every rank's
     # resident key (ncclBroadcast over xGMI)
     key_collective = None
+    comm, rccl_nranks = None, None
+    if distributed and not args.dry:
+        # the library's own RCCL communicator; ncclCommCount on the line shows RCCL spans every rank
+        comm = xdist.rccl_comm_for(ctx, local)
+        rccl_nranks = comm.count()
     if args.config != "cfg2":
         kgen = torch.Generator(device=device)
         kgen.manual_seed(0xE7AC7003)
@@ -451,7 +456,6 @@ def main():
                 sync()
                 ctx.load_relin_key_dev(rlk, G)
             if distributed:
-                comm = xdist.rccl_comm_for(ctx, local)
                 ctx.broadcast_relin_key(comm, 0, G)
                 key_collective = "exacto_ctx_broadcast_relin_key (ncclBroadcast, library RCCL communicator)"
             sync()
@@ -675,6 +679,7 @@ def main():
             "world_size": world,
             "backend": backend,
             "key_broadcast": key_collective,
+            "rccl_nranks": rccl_nranks,
             "timed_s": round(elapsed, 3),
             "roofline": roofline,
             "ntt": ntt,
@@ -692,6 +697,9 @@ def main():
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()
+        if comm is not None:
+            sync()
+            comm.close()
         dist.destroy_process_group()
 
 

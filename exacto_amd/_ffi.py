@@ -133,6 +133,7 @@ _SIGS = [
     ("exacto_rccl_unique_id", [_P], C.c_int),
     ("exacto_rccl_comm_init", [C.POINTER(_P), C.c_int, _P, C.c_int, C.c_int], C.c_int),
     ("exacto_rccl_comm_destroy", [_P], C.c_int),
+    ("exacto_rccl_comm_count", [_P, C.POINTER(C.c_int)], C.c_int),
     ("exacto_ctx_broadcast_relin_key", [_P, _P, C.c_int, _SZ], C.c_int),
     ("exacto_broadcast_galois_key", [_P, _P, C.c_int, _P, _SZ], C.c_int),
     ("exacto_rccl_allgather_u64", [_P, _P, _P, _P, _SZ], C.c_int),
@@ -236,6 +237,12 @@ class RcclComm:
     @property
     def handle(self):
         return self._h
+
+    def count(self) -> int:
+        """ncclCommCount of the library's communicator: the ranks RCCL itself spans."""
+        v = C.c_int(0)
+        check(self._lib.exacto_rccl_comm_count(self._h, C.byref(v)))
+        return v.value
 
     def close(self):
         if self._h:

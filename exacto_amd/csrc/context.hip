@@ -300,7 +300,9 @@ struct exacto_ctx {
     // of inverse-transforming its NTT-domain input (dbfv_mul_group, exacto_dbfv_mul_chain_dev)
     u64* chain_coef = nullptr;
     size_t chain_coef_bytes = 0;
-    u64* coef_out = nullptr;        // set by the chain: where this step's coefficient form goes
+    u64* coef_out = nullptr;        // where this step's coefficient form went (psum steps of a chain)
+    int coef_slot = -1;             // set by the chain: chain_coef half for this step's coefficient form
+    size_t coef_slot_words = 0;     // ... and the size of one half
     const u64* coef_in = nullptr;   // set by the chain: the coefficient form of this step's `a`
     bool coef_written = false;      // reported back: coef_out holds this step's results
     u64* dec_buf = nullptr;    // decryption phase [B][L][n]
@@ -1983,7 +1985,15 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     const bool psum = sum_ks && c->psum_env && m <= c->psum_max && op.ea != nullptr && near60 &&
                       (c->logn == 12 || c->logn == 13) && exact_scale_sp_ok(c->L, c->K, crt_mode(c));
     // chain (psum): the limbs are formed in the coefficient domain in coef_out and forward-transformed
-    // from there into out, so coef_out keeps them for the next step's extension
+    // from there into out, so coef_out keeps them for the next step's extension.  The buffer is grown
+    // only here, where psum is known to be on (HPS or non-psum chains never allocate it).
+    c->coef_out = nullptr;
+    if (psum && c->coef_slot >= 0) {
+        size_t ccap = c->chain_coef_bytes;
+        if (grow(&c->chain_coef, &ccap, 2 * c->coef_slot_words * sizeof(u64))) return EXACTO_ERR_HIP;
+        c->chain_coef_bytes = ccap;
+        c->coef_out = c->chain_coef + (size_t)c->coef_slot * c->coef_slot_words;
+    }
     u64* cf = psum && c->coef_out ? c->coef_out : out;
     c->coef_written = false;
     if (psum) {
@@ -2084,7 +2094,7 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     if (B <= Bg) return dbfv_mul_group(c, d, base, plain, a, b, out, B, b_extended, limbs);
     // several groups: no coefficient-form carry between chain steps (its buffers are whole-batch)
     c->coef_in = nullptr;
-    c->coef_out = nullptr;
+    c->coef_slot = -1;
     const size_t ctw = 2 * L * n;
     for (size_t g0 = 0; g0 < B; g0 += Bg) {
         const size_t cnt = std::min(Bg, B - g0);
@@ -2250,19 +2260,18 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     if (B == 0) return 0;
     // the coefficient form of each step's result (psum path, one item group) goes to chain_coef, and
     // the next step lifts it directly: one batched inverse NTT of its input less per step
+    // (dbfv_mul_group allocates chain_coef, two halves of `bytes`, only when the step runs psum)
     const bool carry = depth > 1 && c->share_ext && c->K > 0;
-    if (carry) {
-        size_t cap = c->chain_coef_bytes;
-        if (grow(&c->chain_coef, &cap, 2 * bytes)) return EXACTO_ERR_HIP;
-        c->chain_coef_bytes = cap;
-    }
     const uint64_t* src = x;
     const u64* src_coef = nullptr;
     int rc = 0;
     for (size_t k = 0; k < depth && rc == 0; ++k) {
         uint64_t* dst = (k + 1 == depth) ? out : c->chain_buf + (k % 2) * (bytes / sizeof(u64));
         c->coef_in = src_coef;
-        c->coef_out = carry && k + 1 < depth ? c->chain_coef + (k % 2) * (bytes / sizeof(u64)) : nullptr;
+        c->coef_slot = carry && k + 1 < depth ? (int)(k % 2) : -1;
+        c->coef_slot_words = bytes / sizeof(u64);
+        c->coef_out = nullptr;
+        c->coef_written = false;
         // y's extensions are computed by the first step and reused by the others
         rc = dbfv_mul_core(c, d, base, plain, src, y, dst, B, k > 0);
         src_coef = c->coef_out && c->coef_written ? c->coef_out : nullptr;
@@ -2270,6 +2279,7 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     }
     c->coef_in = nullptr;
     c->coef_out = nullptr;
+    c->coef_slot = -1;
     c->coef_written = false;
     return rc;
 }
@@ -3149,14 +3159,16 @@ struct BootDebug {
         if (dbuf || xbuf || xcc) (void)hipStreamSynchronize(s);
         free_dev(dbuf); free_dev(xbuf); free_dev(xcc);
     }
+    // null source (an earlier allocation failed; the call's rc carries the real error): skipped, so the
+    // diagnostic never faults the GPU and hides that error
     void snap(const std::string& name, const u64* p, size_t words) {
-        if (!on || names.size() >= (size_t)DN) return;
+        if (!on || !p || names.size() >= (size_t)DN) return;
         const size_t w = std::min<size_t>(words, DW);
         launch_copy_u64(dbuf + names.size() * DW, p, (long)w, s);
         names.emplace_back(name, w);
     }
     void xsnap(const std::string& name, const u64* p) {
-        if (!on || xnames.size() >= (size_t)XN) return;
+        if (!on || !p || xnames.size() >= (size_t)XN) return;
         launch_xcd_probe(p, xbuf + xnames.size() * XB * 4, 4, xcc + xnames.size() * XB, XB, s);
         xnames.push_back(name);
     }
@@ -3545,6 +3557,13 @@ extern "C" int exacto_rccl_comm_destroy(void* comm) {
     return 0;
 }
 
+extern "C" int exacto_rccl_comm_count(void* comm, int* nranks) {
+    if (!comm || !nranks) return invalid_param("null argument");
+    if (int e = rccl_ready()) return e;
+    RCCL_TRY(rccl().comm_count((ncclComm_t)comm, nranks));
+    return 0;
+}
+
 // In-place broadcast of `words` u64 at buf from root's buffer, enqueued on the context stream.
 // Checks the communicator and the root first; *my_rank (optional) receives this rank.
 static int rccl_check(void* comm, int root, int* my_rank) {
@@ -3564,19 +3583,69 @@ static int rccl_bcast(exacto_ctx* c, void* comm, int root, u64* buf, size_t word
     return 0;
 }
 
+// Agreement step of a collective call: every rank contributes {its num_keys, its own verdict} and
+// all-gathers everyone's, so that every rank takes the same decision (proceed or InvalidParam)
+// before any rank resizes its key or enqueues the key broadcast.  A mismatch therefore fails on all
+// ranks instead of leaving the others blocked in a broadcast the failing rank never joins.
+static int rccl_agree(exacto_ctx* c, void* comm, u64 mine, u64 ok, bool* agreed, std::string* why) {
+    *agreed = false;
+    int nr = 0;
+    RCCL_TRY(rccl().comm_count((ncclComm_t)comm, &nr));
+    u64* dev = nullptr;
+    HIP_TRY(hipMalloc((void**)&dev, sizeof(u64) * 2 * (nr + 1)));
+    std::vector<u64> host(2 * (size_t)(nr + 1));
+    host[0] = mine;
+    host[1] = ok;
+    int rc = 0;
+    if (hipMemcpyAsync(dev, host.data(), 2 * sizeof(u64), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        rc = fail(EXACTO_ERR_HIP, "HIP error: hipMemcpyAsync (agreement header)");
+    else {
+        const ncclResult_t r = rccl().all_gather(dev, dev + 2, 2, ncclUint64, (ncclComm_t)comm, c->stream);
+        if (r != ncclSuccess)
+            rc = fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(r) + " (ncclAllGather)");
+        else if (hipMemcpyAsync(host.data() + 2, dev + 2, 2 * sizeof(u64) * nr, hipMemcpyDeviceToHost, c->stream) !=
+                     hipSuccess ||
+                 hipStreamSynchronize(c->stream) != hipSuccess)
+            rc = fail(EXACTO_ERR_HIP, "HIP error: agreement header read-back");
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(dev);
+    if (rc) return rc;
+    for (int r = 0; r < nr; ++r) {
+        if (!host[2 + 2 * r + 1]) {
+            *why = "rank " + std::to_string(r) + " rejected the call";
+            return 0;
+        }
+        if (host[2 + 2 * r] != host[2]) {
+            *why = "ranks disagree on num_keys (rank 0: " + std::to_string(host[2]) + ", rank " + std::to_string(r) +
+                   ": " + std::to_string(host[2 + 2 * r]) + ")";
+            return 0;
+        }
+    }
+    *agreed = true;
+    return 0;
+}
+
 // Every check runs before the resident key is touched: a failed call (bad root, no RCCL, a root
-// without a loaded key of that size) leaves the context's key exactly as it was.  The root
-// broadcasts its resident key as loaded (never resized); a receiving rank's buffer is (re)sized and
-// marked loaded only once the broadcast into it has been enqueued.
+// without a loaded key of that size, ranks passing different num_keys) leaves every rank's key
+// exactly as it was and returns InvalidParam on every rank (rccl_agree).  The root broadcasts its
+// resident key as loaded (never resized); a receiving rank's buffer is (re)sized and marked loaded
+// only once the broadcast into it has been enqueued.
 extern "C" int exacto_ctx_broadcast_relin_key(exacto_ctx* c, void* comm, int root, size_t num_keys) {
     if (int e = check_ctx(c)) return e;
     int me = -1;
     if (int e = rccl_check(comm, root, &me)) return e;
     const size_t words = num_keys * 2 * c->L * (size_t)c->n;
+    const bool root_ok = c->rlk_loaded && c->rlk_keys == num_keys;
+    std::string why;
+    bool agreed = false;
+    if (int e = rccl_agree(c, comm, num_keys, me == root ? root_ok : 1, &agreed, &why)) return e;
+    if (!agreed) {
+        if (me == root && !root_ok)
+            why = "broadcast root has no resident relinearization key of " + std::to_string(num_keys) + " rows";
+        return invalid_param(why);
+    }
     if (me == root) {
-        if (!c->rlk_loaded || c->rlk_keys != num_keys)
-            return invalid_param("broadcast root has no resident relinearization key of " + std::to_string(num_keys) +
-                                 " rows");
         if (!words) return 0;
         RCCL_TRY(rccl().broadcast(c->d_rlk, c->d_rlk, words, ncclUint64, root, (ncclComm_t)comm, c->stream));
         return 0;

@@ -384,14 +384,19 @@ int exacto_bfv_bootstrap_dev(exacto_ctx* orig, exacto_ctx* boot, const uint64_t*
  * context's stream.
  *   exacto_rccl_unique_id      ncclGetUniqueId -> id[128] (rank 0; share it out of band)
  *   exacto_rccl_comm_init      ncclCommInitRank on `device`
+ *   exacto_rccl_comm_count     ncclCommCount: the ranks the communicator spans (bench lines record it)
  *   exacto_ctx_broadcast_relin_key   root's resident relinearisation key -> every rank's resident key
- *                              (in place; non-root ranks need no prior load), num_keys = [G] rows
+ *                              (in place; non-root ranks need no prior load), num_keys = [G] rows.
+ *                              Collective agreement first: every rank all-gathers {num_keys, verdict},
+ *                              so a root without a key of that size, or ranks passing different
+ *                              num_keys, fail with InvalidParam on EVERY rank, keys untouched
  *   exacto_broadcast_galois_key      a device Galois key buffer [num_keys][2][L][n], in place
  *   exacto_rccl_allgather_u64  recv = [nranks][count] u64 (never a reduction: residues are not summable
  *                              by RCCL) */
 int exacto_rccl_unique_id(uint8_t* id);
 int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id, int rank, int device);
 int exacto_rccl_comm_destroy(void* comm);
+int exacto_rccl_comm_count(void* comm, int* nranks);
 int exacto_ctx_broadcast_relin_key(exacto_ctx* ctx, void* comm, int root, size_t num_keys);
 int exacto_broadcast_galois_key(exacto_ctx* ctx, void* comm, int root, uint64_t* gk_dev, size_t num_keys);
 int exacto_rccl_allgather_u64(exacto_ctx* ctx, void* comm, const uint64_t* send, uint64_t* recv, size_t count);

@@ -264,7 +264,93 @@ def worst_digests(threads):
     return out
 
 
+# The bench's production shapes (bench.py DEFAULT_BATCH), so that the exact batch the bench times,
+# at the library's default chunking and pipeline lanes, is compared against the C restatement:
+#   cfg3    bfv_mul_and_relin, B = 1024 (two 512-product chunks on two lanes; eval.rs:73-147)
+#   cfg1    bfv_mul_and_relin on compact_bfv, B = 8192 (chunks of 7168 + 1024; eval.rs:157-332)
+#   u64dbfv dbfv_mul on u64_dbfv, B = 64 items (4096 HPS products, chunks of 1152; dbfv/eval.rs:82-149)
+#   cfg2    INTT(NTT(a) . NTT(b)) of B = 16384 coefficient-domain polys (ntt.rs:181-195)
+# Inputs are regenerated from the seed by the GPU test (numpy default_rng, tests/bridge.py); the
+# digests of row blocks name the failing rows when one differs.
+BENCH_DIGESTS = {
+    "cfg3_bench": {"config": "cfg3", "n": 4096, "batch": 1024, "seed": 3301, "block": 128},
+    "cfg1_bench": {"config": "cfg1", "n": 1024, "batch": 8192, "seed": 1101, "block": 1024},
+    "u64dbfv_bench": {"config": "u64dbfv", "n": 4096, "batch": 64, "seed": 6401, "block": 8},
+    "cfg2_bench": {"config": "cfg2", "n": 4096, "batch": 16384, "seed": 2201, "block": 2048},
+}
+BENCH_GEN = ("numpy.random.default_rng(seed); bfv: ct1, ct2 = uniform_residues((B, 2)), rlk = "
+             "uniform_residues((G, 2)); dbfv: a, b = uniform_residues((B, d, 2)), rlk; cfg2: a, b = "
+             "uniform_residues((B,))  (tests/bridge.py)")
+
+
+def bench_params(cfg, n):
+    if cfg == "cfg3":
+        return P.cfg3_params(n)
+    if cfg == "cfg1":
+        return P.compact_bfv()
+    if cfg == "u64dbfv":
+        return P.u64_dbfv()
+    if cfg == "cfg2":
+        return P.BfvParamsBuilder().ring_degree(n).plain_modulus(65537).ct_moduli([P.Q3[0]]).build()
+    raise ValueError(cfg)
+
+
+def bench_digest_inputs(spec):
+    """(params, x, y, rlk) of a BENCH_DIGESTS entry; x, y are ct1/ct2, a/b or the cfg2 operands."""
+    prm = bench_params(spec["config"], spec["n"])
+    bp = prm.bfv_params if spec["config"] == "u64dbfv" else prm
+    rng = np.random.default_rng(spec["seed"])
+    q, n, B = bp.ct_basis.moduli, bp.ring_degree, spec["batch"]
+    pre = {"cfg2": (B,), "u64dbfv": (B, prm.num_digits if spec["config"] == "u64dbfv" else 0, 2)}.get(
+        spec["config"], (B, 2))
+    x = uniform_residues(rng, pre, q, n)
+    y = uniform_residues(rng, pre, q, n)
+    rlk = None if spec["config"] == "cfg2" else uniform_residues(rng, (bp.gadget_digits, 2), q, n)
+    return prm, x, y, rlk
+
+
+def bench_output(spec, prm, x, y, rlk, threads):
+    from oracle import cref
+    if spec["config"] == "cfg2":
+        return cref.polymul(spec["n"], prm.ct_basis.moduli[0], x, y, threads=threads)
+    if spec["config"] == "u64dbfv":
+        return cref.dbfv_mul(prm, x, y, rlk, threads=threads)
+    return cref.bfv_mul_and_relin(prm, x, y, rlk, threads=threads)
+
+
+def input_digest(x, y, rlk):
+    parts = [x.ravel(), y.ravel()] + ([] if rlk is None else [rlk.ravel()])
+    return sha(np.concatenate(parts))
+
+
+def bench_digests(threads, names=None):
+    import time
+    out = {}
+    for name, spec in BENCH_DIGESTS.items():
+        if names and name not in names:
+            continue
+        t0 = time.time()
+        prm, x, y, rlk = bench_digest_inputs(spec)
+        r = bench_output(spec, prm, x, y, rlk, threads)
+        e = dict(spec, generator=BENCH_GEN)
+        e["sha256_inputs"] = input_digest(x, y, rlk)
+        e["sha256_out"] = sha(r)
+        blk = spec["block"]
+        e["sha256_out_blocks"] = [sha(r[i:i + blk]) for i in range(0, spec["batch"], blk)]
+        out[name] = e
+        print(name, e["sha256_out"], f"{time.time() - t0:.1f} s", flush=True)
+    return out
+
+
 def main():
+    if "--bench-digests" in sys.argv:   # minutes: cfg3's 1024 BigInt schoolbook tensors dominate
+        names = [a for a in sys.argv[1:] if not a.startswith("--")]
+        with open(os.path.join(HERE, "digests.json")) as f:
+            dg = json.load(f)
+        dg.update(bench_digests(threads=os.cpu_count() or 1, names=names))
+        with open(os.path.join(HERE, "digests.json"), "w") as f:
+            json.dump(dg, f, indent=1)
+        return
     if "--worst-digests" in sys.argv:
         with open(os.path.join(HERE, "digests.json")) as f:
             dg = json.load(f)

@@ -29,7 +29,10 @@ def test_compact_bfv_production_batch(gpu_available):
     prm = P.compact_bfv()
     q, n = prm.ct_basis.moduli, prm.ring_degree
     rng = np.random.default_rng(0xE7AC7001)
-    B = 1100                                  # 512 + 512 + 76: chunk and lane boundaries
+    # the library's default chunk at compact_bfv is 7168 products, so B = 1100 is ONE chunk split in
+    # halves over the two lanes; set_chunk(512) then makes it 512 + 512 + 76 (chunk and lane
+    # boundaries).  The bench's own B = 8192 (7168 + 1024) is test_gpu_bench_shapes.py's cfg1 case.
+    B = 1100
     ct1 = uniform_residues(rng, (B, 2), q, n)
     ct2 = uniform_residues(rng, (B, 2), q, n)
     rlk = uniform_residues(rng, (prm.gadget_digits, 2), q, n)
@@ -39,6 +42,8 @@ def test_compact_bfv_production_batch(gpu_available):
     got = ctx.bfv_mul_and_relin(ct1, ct2)
     want = cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=16)
     assert np.array_equal(got, want)
+    ctx.set_chunk(512)
+    assert np.array_equal(ctx.bfv_mul_and_relin(ct1, ct2), want)
     # one product alone (the published single-call case) is the same as inside the batch
     assert np.array_equal(ctx.bfv_mul_and_relin(ct1[777:778], ct2[777:778]), want[777:778])
 

@@ -84,5 +84,12 @@ def test_rccl_one_rank_broadcast_and_allgather(gpu_available):
         assert torch.equal(gk, g0) and torch.equal(recv, send)
         with pytest.raises(ExactoError):
             dst.broadcast_relin_key(comm, 1, dst.G)   # root out of range
+        # a root whose resident key has another row count: the agreement step (every rank all-gathers
+        # {num_keys, verdict} before any key is touched) rejects the call on every rank, key intact
+        with pytest.raises(ExactoError) as e:
+            dst.broadcast_relin_key(comm, 0, dst.G - 1)
+        assert e.value.variant == "InvalidParam" and "rank 0 rejected" not in str(e.value)
+        assert np.array_equal(dst.bfv_mul_and_relin(ct1, ct2), want)
+        assert comm.count() == 1
     finally:
         comm.close()
