@@ -34,7 +34,8 @@ class CtxInfo(C.Structure):
                 ("num_aux_moduli", C.c_size_t), ("num_internal_aux", C.c_size_t),
                 ("gadget_digits", C.c_size_t), ("gadget_base", C.c_uint64),
                 ("plain_modulus", C.c_uint64), ("mul_path", C.c_int), ("device", C.c_int),
-                ("ks32_primes", C.c_int), ("psum_max", C.c_int)]
+                ("ks32_primes", C.c_int), ("psum_max", C.c_int),
+                ("ks32_lazy", C.c_int)]
 
 
 _lib = None
@@ -300,6 +301,13 @@ class HipContext:
         self.psum_max = info.psum_max
         self.ct_moduli = [int(q) for q in ct_moduli]
         self.plain_modulus = int(info.plain_modulus)
+
+    @property
+    def ks32_lazy(self) -> bool:
+        """The resident relinearisation key runs in the lazy 31-bit basis (decided at its first use)."""
+        info = CtxInfo()
+        check(self._lib.exacto_ctx_get_info(self._h, C.byref(info)))
+        return bool(info.ks32_lazy)
 
     @classmethod
     def from_params(cls, params, device=0):

@@ -127,6 +127,16 @@ struct Big {
         for (size_t i = 0; i < w.size() && a; ++i) { u64 s = w[i] + a; a = s < a; w[i] = s; }
         if (a) w.push_back(a);
     }
+    void add(const Big& o) {
+        u64 carry = 0;
+        for (size_t i = 0; i < std::max(w.size(), o.w.size()) || carry; ++i) {
+            if (i == w.size()) w.push_back(0);
+            const u128 t = (u128)w[i] + (i < o.w.size() ? o.w[i] : 0) + carry;
+            w[i] = (u64)t;
+            carry = (u64)(t >> 64);
+        }
+        trim();
+    }
     void shr1() {
         for (size_t i = 0; i < w.size(); ++i) w[i] = (w[i] >> 1) | (i + 1 < w.size() ? w[i + 1] << 63 : 0);
         trim();
@@ -173,7 +183,9 @@ struct ProfRec {
 struct Ks32Basis {
     int S = 0;
     int sum_max = 0;              // dBFV key-switch sums the basis lifts exactly
-    bool long_runs = false;       // every prime below 2^32 / 3: 12 MAC products per reduction
+    int mac_form = 0;             // ks32_mac: 0 primes up to 2^31 (7 products per reduction),
+                                  // 1 below 2^32 / 3 (12), 2 below 2^30 (12, lazy transforms)
+    Big P;                        // product of the primes
     Prime32* d_p32 = nullptr;
     uint2* d_tw32 = nullptr;
     Ks32Tables* d_kst = nullptr;
@@ -220,8 +232,16 @@ struct exacto_ctx {
     bool ks32 = true;
     int S32 = 0;                 // 0: not eligible for these parameters
     int ks32_sum_max = 0;        // key-switch sums that may be added before one lift (prod p bound)
-    bool ks32_long_runs = false; // every 31-bit prime below 2^32 / 3: 12 MAC products per reduction
+    int ks32_mac_form = 0;       // ks32_mac's reduction form for the active basis (Ks32Basis::mac_form)
     Ks32Basis kw;                // wide basis (primes up to 2^31) for dBFV digit sums the primary cannot hold
+    // The primary basis is one of two, chosen per relinearisation key (ensure_rs):
+    //   kn: narrow primes below 2^32 / 3 bounding |sum_g d_g * r_g| by G n (B/2) (q/2) for ANY key;
+    //   kz: lazy primes below 2^30 (cheaper 32-bit butterflies, ks32_dev.hpp), used when the resident
+    //       key's own L1 norms bound the sum: |u_{c,l}| <= (B/2) sum_g ||r_{g,c,l}||_1 < prod p / 2
+    //       (a uniform key has ||r||_1 ~ n q / 4: half the generic bound).  EXACTO_KS32_LAZY=0: kn only.
+    // S32 / d_p32 / d_tw32 / d_kst / ks32_sum_max / ks32_mac_form describe the active one.
+    Ks32Basis kn, kz;
+    bool ks32_lazy_active = false;
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
@@ -465,22 +485,32 @@ static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
 // 2^30) with prod p > `bound`, its twiddles, constants and Garner tables on the device.  sum_max:
 // how many key-switch sums (dBFV products of one output limb) the basis lifts exactly when they
 // are added first.  S = 0 when no basis of at most EXACTO_KS32_MAXS primes exists.
-static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
+// fixedS > 0 (the lazy basis): exactly fixedS primes in (7 pmax / 8, pmax), no bound check here (the
+// bound is the resident key's, checked when the key is converted: ensure_rs; ks32.hip's red_s64_lz
+// needs p > 0.8 * 2^30).
+static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b,
+                                 int fixedS = 0) {
     b->S = 0;
     std::vector<u64> ps;
     Big P(1);
     const u64 step = 2 * (u64)c->n;
-    for (u64 p = (pmax - 1) / step * step + 1; p > (1ull << 30) && ps.size() < EXACTO_KS32_MAXS; p -= step) {
+    const u64 pmin = fixedS ? pmax - pmax / 8 : (1ull << 30);
+    for (u64 p = (pmax - 1) / step * step + 1; p > pmin && ps.size() < EXACTO_KS32_MAXS; p -= step) {
         if (!is_prime_h(p)) continue;
         ps.push_back(p);
         P.mul(p);
-        if (P.cmp(bound) > 0) break;
+        if (fixedS ? (int)ps.size() == fixedS : P.cmp(bound) > 0) break;
     }
-    if (P.cmp(bound) <= 0 || ps.size() < 2) return 0;
-    b->long_runs = true;
-    for (u64 p : ps) b->long_runs &= p < (1ull << 32) / 3;
-    b->sum_max = 1;
-    for (u64 m = 2; m <= 64; ++m) {
+    if (fixedS ? (int)ps.size() != fixedS : (P.cmp(bound) <= 0 || ps.size() < 2)) return 0;
+    bool lazy = true, narrow = true;
+    for (u64 p : ps) {
+        lazy &= p < (1ull << 30);
+        narrow &= p < (1ull << 32) / 3;
+    }
+    b->mac_form = lazy ? 2 : narrow ? 1 : 0;
+    b->P = P;
+    b->sum_max = fixedS ? 0 : 1;
+    for (u64 m = 2; m <= 64 && !fixedS; ++m) {
         Big bm((u64)c->G);
         bm.mul((u64)c->n);
         bm.mul(c->gbase / 2);
@@ -558,6 +588,17 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
     return 0;
 }
 
+// the active primary basis (run_mul, dbfv_mul_group, bfv_apply_automorphism read these fields)
+static void use_ks32_basis(exacto_ctx* c, const Ks32Basis& b) {
+    c->S32 = b.S;
+    c->d_p32 = b.d_p32;
+    c->d_tw32 = b.d_tw32;
+    c->d_kst = b.d_kst;
+    c->ks32_sum_max = b.sum_max;
+    c->ks32_mac_form = b.mac_form;
+    c->ks32_lazy_active = &b == &c->kz;
+}
+
 static void free_basis(Ks32Basis* b) {
     free_dev(b->d_p32); free_dev(b->d_tw32); free_dev(b->d_kst); free_dev(b->d_rs);
     *b = Ks32Basis{};
@@ -565,8 +606,8 @@ static void free_basis(Ks32Basis* b) {
 
 // build_ks32_basis_impl, releasing whatever it allocated when a later step fails (the basis is not
 // attached to the context yet, so exacto_ctx_destroy would not free it)
-static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b) {
-    const int e = build_ks32_basis_impl(c, pmax, qmax, bound, b);
+static int build_ks32_basis(exacto_ctx* c, u64 pmax, u64 qmax, const Big& bound, Ks32Basis* b, int fixedS = 0) {
+    const int e = build_ks32_basis_impl(c, pmax, qmax, bound, b, fixedS);
     if (e) free_basis(b);
     return e;
 }
@@ -612,12 +653,12 @@ static int setup_ks32(exacto_ctx* c) {
         }
     }
     if (prim.S == 0) return 0;
-    c->S32 = prim.S;
-    c->d_p32 = prim.d_p32;
-    c->d_tw32 = prim.d_tw32;
-    c->d_kst = prim.d_kst;
-    c->ks32_sum_max = prim.sum_max;
-    c->ks32_long_runs = prim.long_runs;
+    c->kn = prim;
+    // the lazy basis: as many primes below 2^30 as the primary has (the workspaces are sized by S)
+    const char* lz = getenv("EXACTO_KS32_LAZY");
+    if (!(lz && lz[0] == '0') && wide_mode != 2)
+        if (int e = build_ks32_basis(c, 1ull << 30, qmax, bound, &c->kz, prim.S)) return e;
+    use_ks32_basis(c, c->kn);
     return 0;
 }
 
@@ -942,7 +983,9 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->ext_a); free_dev(c->ext_b);
     free_dev((u64*)c->d_cdt); free_dev(c->d_gpow); free_dev(c->d_delta); free_dev(c->enc_buf); free_dev(c->gk_s); free_dev(c->d_gk_rs); free_dev(c->d_dall); free_dev(c->d_hdig); free_dev(c->d_dk); free_dev(c->d_dsk); free_dev(c->d_uk); free_dev(c->pl_buf);
     if (c->ws_D16) (void)hipFree(c->ws_D16);
-    free_dev(c->d_p32); free_dev(c->d_tw32); free_dev(c->d_kst); free_dev(c->d_rs);
+    free_dev(c->d_rs);   // the active basis' tables belong to kn / kz
+    free_dev(c->kn.d_p32); free_dev(c->kn.d_tw32); free_dev(c->kn.d_kst); free_dev(c->kn.d_rs);
+    free_dev(c->kz.d_p32); free_dev(c->kz.d_tw32); free_dev(c->kz.d_kst); free_dev(c->kz.d_rs);
     free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst); free_dev(c->kw.d_rs);
     free_dev(c->ws_DS); free_dev(c->ws_U);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -965,6 +1008,7 @@ extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
     info->device = c->device;
     info->ks32_primes = c->ks32 ? c->S32 : 0;
     info->psum_max = c->psum_env ? c->psum_max : 0;
+    info->ks32_lazy = c->ks32 && c->ks32_lazy_active ? 1 : 0;
     return 0;
 }
 
@@ -1230,9 +1274,57 @@ static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t
     return 0;
 }
 
-// The resident relinearisation key in ks32's basis (d_rs).  Once per key.
+// The primary basis for the resident key: the lazy one (kz) when the key's own norms bound the key
+// switch, |u_{c,l}| <= (B/2) sum_g ||r_{g,c,l}||_1 with ||r||_1 <= (sum floor(|r_j|/2^20) + n) 2^20
+// (ks32_key_norm_kernel), for every (c, l): prod p > 2 m bound for m = 1 (and sum_max = the largest
+// such m <= 64 for dBFV digit sums); otherwise the narrow one (kn), whose bound holds for any key.
+static int ks32_select_basis(exacto_ctx* c) {
+    use_ks32_basis(c, c->kn);
+    if (c->kz.S == 0 || c->rlk_keys == 0) return 0;
+    const long rows = (long)c->rlk_keys * 2 * c->L, CL = 2L * c->L;
+    Scratch ks, nr;
+    HIP_TRY(ks.alloc((size_t)rows * c->n * sizeof(u64), c->stream, c->pool, c->debug_scratch));
+    HIP_TRY(nr.alloc((size_t)rows * sizeof(u64), c->stream, c->pool, c->debug_scratch));
+    NttBatch nb{};
+    nb.src = c->d_rlk; nb.src_item_stride = CL * c->n;
+    nb.dst = ks.as<u64>(); nb.dst_item_stride = CL * c->n;
+    nb.ppi = (int)CL; nb.prime_base = 0; nb.period = c->L;
+    if (int e = run_ntt(c, nb, rows, true)) return e;
+    ks32_key_norms(ks.as<u64>(), nr.as<u64>(), rows, c->L, c->n, c->d_primes, c->stream);
+    CHECK_LAUNCH();
+    std::vector<u64> h((size_t)rows);
+    HIP_TRY(hipMemcpyAsync(h.data(), nr.as<u64>(), h.size() * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    Big worst(0);
+    for (long cl = 0; cl < CL; ++cl) {
+        Big acc(0);
+        for (size_t g = 0; g < c->rlk_keys; ++g) {
+            Big t(h[(size_t)g * CL + cl] + (u64)c->n);
+            t.mul(1ull << 20);
+            acc.add(t);
+        }
+        if (acc.cmp(worst) > 0) worst = acc;
+    }
+    worst.mul(c->gbase / 2);
+    int sm = 0;
+    for (u64 m = 1; m <= 64; ++m) {
+        Big bm = worst;
+        bm.mul(2 * m);
+        bm.add(1);
+        if (c->kz.P.cmp(bm) <= 0) break;
+        sm = (int)m;
+    }
+    if (sm >= 1) {
+        c->kz.sum_max = sm;
+        use_ks32_basis(c, c->kz);
+    }
+    return 0;
+}
+
+// The resident relinearisation key in ks32's basis (d_rs), the basis chosen for it first.  Once per key.
 static int ensure_rs(exacto_ctx* c) {
     if (c->rs_valid) return 0;
+    if (int e = ks32_select_basis(c)) return e;
     size_t cap = c->rs_cap;
     const int e = ks32_convert_key(c, c->d_rlk, c->rlk_keys, &c->d_rs, &cap);
     c->rs_cap = cap;
@@ -1409,7 +1501,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                 }
                 {   // per (item, prime, coefficient): G digit residues in, 2L sums out (the key slice from LDS)
                     ProfScope pm(c, PK_KS_MAC, (u64)cnt * c->S32, 4.0 * n * cnt * c->S32 * (guse + 2.0 * L));
-                    ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
+                    ks32_mac(c->ws_DS, c->d_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_mac_form, c->stream);
                 }
                 {   // per (item, component, limb): S 31-bit sums in, R in and out
                     ProfScope pc(c, PK_KS_CRT, (u64)cnt * 2 * L, (double)n * cnt * 2 * L * (4.0 * c->S32 + 16.0));
@@ -1932,6 +2024,9 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     // The primary 31-bit basis when it holds the sums, else the wide one (primes up to 2^31).
     const size_t gu = std::min<size_t>(c->G, c->rlk_keys);
     const int m = c->cached_sum_m;
+    // the primary basis (narrow or lazy) and its sum_max depend on the resident key: decide first
+    if (c->S32 > 0 && c->ks32 && c->rlk_loaded && gu > 0)
+        if (int e = ensure_rs(c)) return e;
     const bool on = c->S32 > 0 && c->ks32 && m > 0 && c->digit16 && c->gbase <= 65536 &&
                     c->rlk_loaded && gu > 0;
     const bool use_prim = on && m <= c->ks32_sum_max;
@@ -1940,7 +2035,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     const int S = use_wide ? c->kw.S : c->S32;
     const Prime32* p32 = use_wide ? c->kw.d_p32 : c->d_p32;
     const Ks32Tables* kst = use_wide ? c->kw.d_kst : c->d_kst;
-    const bool long_runs = use_wide ? c->kw.long_runs : c->ks32_long_runs;
+    const int mac_form = use_wide ? c->kw.mac_form : c->ks32_mac_form;
     const bool wide = (u64)m * (c->gbase / 2) > 32767;   // digit sums beyond int16
     const size_t Bd = B * dout, Sn = (size_t)S * c->n;
     // HPS (u64_dbfv): with the products' c0 / c1 kept in the coefficient domain, relinearize is linear
@@ -2033,7 +2128,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         {
             ProfScope pm(c, PK_KS_MAC, (u64)Bd * S, 4.0 * nn * Bd * S * (gu + 2.0 * c->L));
             ks32_mac(c->d_dsk, use_wide ? c->kw.d_rs : c->d_rs, c->d_uk, (int)Bd, (int)gu, c->L, S, c->n, p32,
-                     long_runs, c->stream);
+                     mac_form, c->stream);
         }
         {
             ProfScope pc(c, PK_KS_CRT, (u64)Bd * 2 * c->L, nn * Bd * 2 * c->L * (4.0 * S + 16.0));
@@ -2581,10 +2676,13 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
     const bool d16 = c->digit16 && c->gbase <= 65536;  // int16 digits, as in run_mul
     // ks32 key switch (as run_mul): the key converted to the 31-bit basis on every call (the
     // caller may pass a different key in the same buffer), G L (2L) 60-bit (32-bit) transforms
-    const bool k32 = d16 && c->ks32 && c->S32 > 0 && c->path == EXACTO_PATH_EXACT_RNS;
+    // The narrow basis (kn) always: its bound holds for any key, and this key's norms are not
+    // examined (the lazy basis is chosen per resident relinearisation key only).
+    const Ks32Basis& kb = c->kn;
+    const bool k32 = d16 && c->ks32 && kb.S > 0 && c->path == EXACTO_PATH_EXACT_RNS;
     if (k32) {
         size_t cap = c->gk_rs_cap;
-        const int e = ks32_convert_key(c, gk, (size_t)guse, &c->d_gk_rs, &cap);
+        const int e = ks32_convert_key(c, gk, (size_t)guse, &c->d_gk_rs, &cap, kb.S, kb.d_p32);
         c->gk_rs_cap = cap;
         if (e) return e;
     } else {
@@ -2621,9 +2719,9 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
             CHECK_LAUNCH();
             launch_rows(c->ws_T + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
             CHECK_LAUNCH();
-            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
-            ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, c->S32, n, c->d_p32, c->ks32_long_runs, c->stream);
-            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->stream);
+            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, kb.S, c->logn, kb.d_p32, c->stream);
+            ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, kb.S, n, kb.d_p32, kb.mac_form, c->stream);
+            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, kb.S, c->logn, kb.d_kst, kb.d_p32, c->d_primes, c->stream);
             CHECK_LAUNCH();
             NttBatch rb{};
             rb.src = c->ws_T; rb.src_item_stride = 2 * Ln;

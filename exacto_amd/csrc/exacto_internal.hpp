@@ -110,8 +110,9 @@ void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int 
 void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
               const PrimeConst* qprimes, hipStream_t st);
 // U [items][2L][S][n] = sum_g DS (.) RS
+void ks32_key_norms(const u64* K, u64* out, long rows, int L, int n, const PrimeConst* qprimes, hipStream_t st);
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
-              const Prime32* primes, bool long_runs, hipStream_t st);
+              const Prime32* primes, int mac_form, hipStream_t st);
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
               const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);

@@ -81,6 +81,30 @@ ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int
     fwd32_store<LOGN>(x, lds, tid, P, RS + (long)b * N);
 }
 
+// Per key row [rows][n] (coefficient domain, canonical mod q_{row's limb}): sum_j floor(|r_j| / 2^20)
+// of its balanced coefficients, so that (sum + n) 2^20 bounds the row's L1 norm (each term < 2^39,
+// the sum < 2^53: exact in u64).  One block per row; the lazy basis is chosen from these (ensure_rs).
+__global__ void __launch_bounds__(256)
+ks32_key_norm_kernel(const u64* __restrict__ K, u64* __restrict__ out, int L, int n,
+                     const PrimeConst* __restrict__ qprimes) {
+    __shared__ u64 part[256];
+    const uint32_t row = blockIdx.x;
+    const u64 q = qprimes[row % (uint32_t)L].q, half = q >> 1;
+    const u64* src = K + (long)row * n;
+    u64 acc = 0;
+    for (int j = threadIdx.x; j < n; j += 256) {
+        const u64 r = src[j];
+        acc += (r > half ? q - r : r) >> 20;
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[row] = part[0];
+}
+
 // Signed 64-bit x -> x mod p, canonical (p in (2^30, 2^31)): x = hi 2^32 + lo with hi signed;
 // (hi + 2^31) 2^32 by Shoup with 2^32 mod p, lo by two halvings, -2^63 by the constant k63.
 __device__ __forceinline__ uint32_t red_s64(long long x, const Prime32& P) {
@@ -94,6 +118,19 @@ __device__ __forceinline__ uint32_t red_s64(long long x, const Prime32& P) {
 // Signed 64-bit x (|x| < 2^63) -> a small non-negative value == x mod p, below 3p + 2^32 < 2^33.6:
 // (hi + 2^31) 2^32 by Shoup with 2^32 mod p, plus lo, plus (-2^63) mod p.  Carried between runs
 // of signed products (7 VALU instead of red_s64's full reduction).
+// Lazy basis (7/8 2^30 < p < 2^30): x mod p in [0, 2p), the lazy inverse transform's input range.
+// The low word goes below 2p by lo - floor(lo / 2^30) p (< 2^30 + 3 (2^30 - p) < 2p for p > 0.8 2^30),
+// so a + b + k63 < 4p < 2^32 needs one min-subtraction (13 VALU instead of red_s64's 17).
+__device__ __forceinline__ uint32_t red_s64_lz(long long x, const Prime32& P) {
+    const uint32_t p = P.p;
+    const uint32_t hu = (uint32_t)((unsigned long long)x >> 32) ^ 0x80000000u;
+    const uint32_t a = red32(shoup32(hu, P.c32, P.c32s, p), p);
+    const uint32_t lo = (uint32_t)x;
+    const uint32_t b = lo - (lo >> 30) * p;
+    const uint32_t s = a + b + P.k63;
+    return min(s, s - 2 * p);
+}
+
 __device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P) {
     const uint32_t hu = (uint32_t)((unsigned long long)x >> 32) ^ 0x80000000u;
     const uint32_t a = shoup32(hu, P.c32, P.c32s, P.p);
@@ -109,22 +146,26 @@ __device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P)
 constexpr int KS_LS = 64;
 // RUN: signed products summed between reductions: 12 for primes below 2^32 / 3 (products below
 // 2^58.9), 7 for primes up to 2^31 (products below 2^60; 7 * 2^60 + 2^33.6 < 2^63)
-template <int CLB, int NW, int RUN>
+// LZ: lazy basis (p < 2^30), sums written in [0, 2p) (red_s64_lz) for the lazy inverse transforms
+template <int CLB, int NW, int RUN, bool LZ = false>
 __global__ void __launch_bounds__(NW * 64)
 ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t* __restrict__ U,
                 int G, int CL, int S, int items, int n, const Prime32* __restrict__ primes) {
     extern __shared__ int kl[];                // [g][cl - cl0][lane]
     constexpr int IG = 4 * NW;                 // items per block
-    const int lane = threadIdx.x & (KS_LS - 1), wave = threadIdx.x / KS_LS;
+    const int lane = threadIdx.x & (KS_LS - 1);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / KS_LS);   // uniform: item math on the SALU
     const int nb = n / KS_LS;
     const int jb = blockIdx.x % nb;
     const int s = (blockIdx.x / nb) % S;
     const int cl0 = (blockIdx.x / (nb * S)) * CLB;
     const int j = jb * KS_LS + lane;
     const Prime32& P = primes[s];
-    for (int r = threadIdx.x; r < G * CLB * KS_LS; r += NW * 64) {
-        const int g = r / (CLB * KS_LS), c = (r / KS_LS) % CLB, t = r & (KS_LS - 1);
-        kl[r] = RS[(((long)g * CL + cl0 + c) * S + s) * n + jb * KS_LS + t];
+    // key slice rows rr = g CLB + c, one per wave at a time (rr wave-uniform: the row index math runs
+    // on the SALU; a flat index r / (CLB 64) per element cost ~20 VALU per word staged)
+    for (int rr = wave; rr < G * CLB; rr += NW) {
+        const int g = rr / CLB, c = rr - g * CLB;
+        kl[rr * KS_LS + lane] = RS[(((long)g * CL + cl0 + c) * S + s) * n + jb * KS_LS + lane];
     }
     __syncthreads();
     const int it_end = min(items, (int)(blockIdx.y + 1) * IG);
@@ -152,7 +193,8 @@ ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t
             }
         }
 #pragma unroll
-        for (int c = 0; c < CLB; ++c) U[(((long)it * CL + cl0 + c) * S + s) * n + j] = red_s64(acc[c], P);
+        for (int c = 0; c < CLB; ++c)
+            U[(((long)it * CL + cl0 + c) * S + s) * n + j] = LZ ? red_s64_lz(acc[c], P) : red_s64(acc[c], P);
     }
 }
 
@@ -172,6 +214,66 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     u64* dst = R + item * r_stride + (long)(b - (uint32_t)item * CL) * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[k * T + tid] = x[k];
+}
+
+// The same per (item, c, l) block with its S inverse transforms run side by side: S groups of n/16
+// threads (S waves-groups, 12 waves at n = 4096, S = 3), group s transforms row s in its own LDS
+// slice, leaves the coefficients there in natural order, and then every thread lifts coefficients
+// j = tid + S T m (coalesced R reads and stores).  The serial form above runs the S transforms one
+// after the other in 4 waves (the launch's 12 waves per SIMD then issue at 0.68); here a block has
+// S times the independent waves.  n <= 4096 (S n/16 <= 1024 threads).
+template <int LOGN, int S>
+__global__ void __launch_bounds__(S * (1 << LOGN) / 16)
+ks32_crt_par_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
+                    const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
+                    const PrimeConst* __restrict__ qprimes) {
+    constexpr int N = 1 << LOGN, T = N / 16, TT = S * T;
+    __shared__ uint32_t lds[S * N];
+    const int tid = threadIdx.x;
+    const int g = tid / T, lt = tid - g * T;        // group = prime s, thread within it
+    const uint32_t b = blockIdx.x;                  // (item, cl)
+    uint32_t* my = lds + g * N;
+    {
+        uint32_t v[16];
+        const uint4* src = reinterpret_cast<const uint4*>(U + ((long)b * S + g) * N + 16 * lt);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const uint4 w = src[h];
+            v[4 * h] = w.x; v[4 * h + 1] = w.y; v[4 * h + 2] = w.z; v[4 * h + 3] = w.w;
+        }
+        inv32_any<LOGN>(v, my, lt, primes[g]);
+        // element k T + lt is in v[k]; the last round's exchange reads are done before the slice
+        // is overwritten with the natural-order result
+        lds_sync();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) my[k * T + lt] = v[k];
+    }
+    lds_sync();
+    uint32_t pr[S], hp[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        pr[s] = primes[s].p;
+        hp[s] = KT->halfP[s];
+    }
+    const uint32_t CL = 2 * L;
+    const long item = b / CL;
+    const int cl = (int)(b - (uint32_t)item * CL);
+    const int l = cl % L;
+    const u64 q = qprimes[l].q;
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+    const u64 negP = KT->negP[l];
+    const u64* rs = R + item * r_stride + (long)cl * N;
+    u64* dst = R + item * r_stride + (long)cl * N;
+#pragma unroll
+    for (int m = 0; m < (N + TT - 1) / TT; ++m) {
+        const int j = tid + m * TT;
+        if (j < N) {
+            uint32_t vj[S];
+#pragma unroll
+            for (int s = 0; s < S; ++s) vj[s] = lds[s * N + j];
+            dst[j] = ks32_lift_one<S>(vj, rs[j], pr, hp, KT, q, dq, negP);
+        }
+    }
 }
 
 // dBFV: the gadget digits of the products of one output limb k summed before their transforms.
@@ -246,6 +348,21 @@ template <int LOGN>
 static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
                             const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
     const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
+    // side-by-side transforms (ks32_crt_par_kernel) where S n/16 threads fit one block;
+    // EXACTO_KS_CRT_PAR=0 keeps the serial form (A/B)
+    static const bool par = [] { const char* e = std::getenv("EXACTO_KS_CRT_PAR"); return !(e && e[0] == '0'); }();
+    if constexpr (LOGN <= 12) {
+        if (par && S == 3) {
+            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 3>), grid, dim3(3 * block.x), 0, st, U, R, r_stride, L, KT,
+                               primes, qprimes);
+            return;
+        }
+        if (par && S == 2) {
+            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 2>), grid, dim3(2 * block.x), 0, st, U, R, r_stride, L, KT,
+                               primes, qprimes);
+            return;
+        }
+    }
     if (S == 2)
         hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else if (S == 3)
@@ -288,8 +405,13 @@ void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, con
 #undef CALL
 }
 
+void ks32_key_norms(const u64* K, u64* out, long rows, int L, int n, const PrimeConst* qprimes, hipStream_t st) {
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(ks32_key_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, K, out, L, n, qprimes);
+}
+
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
-              const Prime32* primes, bool long_runs, hipStream_t st) {
+              const Prime32* primes, int mac_form, hipStream_t st) {
     if (items <= 0) return;
     const int CL = 2 * L;
     // (c, l) pairs per block: the largest divisor of 2L whose key slice (G * CLB * 64 words) fits
@@ -302,11 +424,14 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
     const dim3 grid((unsigned)((n / KS_LS) * S * (CL / CLB)), (unsigned)((items + 4 * NW - 1) / (4 * NW)));
     const int* ds = reinterpret_cast<const int*>(DS);
     const int* rs = reinterpret_cast<const int*>(RS);
-#define MAC_(C_, W_, R_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_, R_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
+// mac_form: 0 primes up to 2^31 (7 products per reduction), 1 below 2^32 / 3 (12), 2 below 2^30
+// (12, lazy output)
+#define MAC_(C_, W_, R_, Z_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_, R_, Z_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
 #define MAC(C_)                                                  \
     do {                                                         \
-        if (long_runs) { if (NW == 8) MAC_(C_, 8, 12); else MAC_(C_, 4, 12); } \
-        else { if (NW == 8) MAC_(C_, 8, 7); else MAC_(C_, 4, 7); }          \
+        if (mac_form == 2) { if (NW == 8) MAC_(C_, 8, 12, true); else MAC_(C_, 4, 12, true); } \
+        else if (mac_form == 1) { if (NW == 8) MAC_(C_, 8, 12, false); else MAC_(C_, 4, 12, false); } \
+        else { if (NW == 8) MAC_(C_, 8, 7, false); else MAC_(C_, 4, 7, false); }          \
     } while (0)
     switch (CLB) {
         case 8: MAC(8); break;

@@ -61,16 +61,28 @@ __device__ __forceinline__ u64 lo_only(uint32_t x) {
     return __builtin_bit_cast(u64, v);
 }
 
+// Prime ranges of a 31-bit basis, and the butterfly form each takes (block-uniform choice):
+//   F32_LAZY   p < 2^30 (4p < 2^32): Harvey's lazy butterflies, values in [0, 4p) forward and
+//              [0, 2p) inverse between stages, one conditional subtraction per butterfly;
+//   F32_NARROW p < 2^32 / 3: values in [0, 3p] forward, both inverse inputs reduced to [0, p);
+//   F32_WIDE   p < 2^31: values below 2p, every operand reduced to [0, p).
+enum { F32_WIDE = 0, F32_NARROW = 1, F32_LAZY = 2 };
+__device__ __forceinline__ int form32(uint32_t p) {
+    return p < (1u << 30) ? F32_LAZY : p <= 0x55555555u ? F32_NARROW : F32_WIDE;
+}
+
 // One round: stage bits BHI..LO of the 4-bit window at LO.
-// Narrow primes (3p < 2^32, every prime of the primary basis): values in [0, 3p] between stages.
-// X is brought to [0, p) (two min-subtractions), and X + T comes straight out of the Shoup chain:
-// qh = hi(Y ws), then lo32(qh (2^32 - p) + (Y w + X)) by two v_mad_u64_u32 = X + T with
-// T = Y w - qh p in [0, 2p), and the second output 2X + 2p - (X + T) = X + 2p - T: 3 multiplies and
-// 7 simple ops per butterfly instead of 3 + 9 (the ~12 % cut of the digit transforms' VALU).
+// Narrow primes (3p < 2^32): values in [0, 3p] between stages.  X is brought to [0, p) (two
+// min-subtractions), and X + T comes straight out of the Shoup chain: qh = hi(Y ws), then
+// lo32(qh (2^32 - p) + (Y w + X)) by two v_mad_u64_u32 = X + T with T = Y w - qh p in [0, 2p), and
+// the second output 2X + 2p - (X + T) = X + 2p - T: 3 multiplies and 7 simple ops per butterfly
+// instead of 3 + 9 (the ~12 % cut of the digit transforms' VALU).
+// Lazy primes (4p < 2^32): the same chain with values in [0, 4p) between stages, X brought to
+// [0, 2p) by ONE min-subtraction (X + T < 4p, X + 2p - T < 4p): 3 multiplies and 5 simple ops.
 // Wide primes (up to 2^31): values < 2p between stages, X and T reduced to [0, p) separately.
 // CANON: the round's inputs are canonical (round 0: the caller's values are in [0, p)), so the first
 // stage's X needs no reduction (8 butterflies x 4 VALU per thread less in the digit transforms).
-template <int LOGN, int LO, int BHI, bool NARROW, bool CANON = false>
+template <int LOGN, int LO, int BHI, int FORM, bool CANON = false>
 __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const uint2* __restrict__ tw, uint32_t p) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
@@ -85,13 +97,16 @@ __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const ui
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m, k1 = k0 + half;
-                if constexpr (NARROW) {
-                    // [0, 3p] -> [0, p); canonical already in the first stage of a CANON round
-                    const uint32_t X = (CANON && b == BHI) ? x[k0] : red32(min(x[k0], x[k0] - p2), p);
+                if constexpr (FORM != F32_WIDE) {
+                    // narrow: [0, 3p] -> [0, p); lazy: [0, 4p) -> [0, 2p); canonical already in the
+                    // first stage of a CANON round
+                    const uint32_t X = (CANON && b == BHI) ? x[k0]
+                                       : FORM == F32_LAZY ? min(x[k0], x[k0] - p2)
+                                                          : red32(min(x[k0], x[k0] - p2), p);
                     const uint32_t qh = __umulhi(x[k1], t.y);
                     const uint32_t o0 = (uint32_t)mad64(qh, np, mad64(x[k1], t.x, lo_only(X)));
-                    x[k0] = o0;                      // X + T < 3p
-                    x[k1] = 2 * X + p2 - o0;         // X + 2p - T in (0, 3p]
+                    x[k0] = o0;                      // X + T (< 3p narrow, < 4p lazy)
+                    x[k1] = 2 * X + p2 - o0;         // X + 2p - T (in (0, 3p] narrow, (0, 4p) lazy)
                 } else {
                     const uint32_t X = red32(x[k0], p);
                     const uint32_t T = red32(shoup32(x[k1], t.x, t.y, p), p);
@@ -103,7 +118,7 @@ __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const ui
     }
 }
 
-template <int LOGN, int R, bool NARROW>
+template <int LOGN, int R, int FORM>
 __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const uint2* tw, uint32_t p) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
@@ -114,13 +129,9 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
         lds_sync();
         lds32_load<LO>(lds, x, tid);
     }
-    fwd32_round<LOGN, LO, BHI, NARROW, R == 0>(x, tid, tw, p);   // round 0: canonical inputs (fwd32_store)
-    if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1, NARROW>(x, lds, tid, tw, p);
+    fwd32_round<LOGN, LO, BHI, FORM, R == 0>(x, tid, tw, p);   // round 0: canonical inputs (fwd32_store)
+    if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1, FORM>(x, lds, tid, tw, p);
 }
-
-// 3p < 2^32: the narrow rounds above apply (every prime of the primary basis; the wide basis has
-// primes up to 2^31)
-__device__ __forceinline__ bool narrow32(uint32_t p) { return p <= 0x55555555u; }
 
 // x (element tid + k T, canonical: round 0 relies on it) -> NTT, stored coalesced at dst (element tid + k T of the
 // bit-reversed-order evaluation array), as balanced residues in (-p/2, p/2] (int32 bits): the
@@ -130,12 +141,17 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     const uint32_t p = P.p, half = p >> 1;
-    if (narrow32(p)) {   // block-uniform
-        fwd32_rounds<LOGN, 0, true>(x, lds, tid, P.tw_fwd, p);
+    const int form = form32(p);   // block-uniform
+    if (form == F32_LAZY) {
+        fwd32_rounds<LOGN, 0, F32_LAZY>(x, lds, tid, P.tw_fwd, p);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = red32(min(x[k], x[k] - 2 * p), p);   // [0, 4p) -> [0, p)
+    } else if (form == F32_NARROW) {
+        fwd32_rounds<LOGN, 0, F32_NARROW>(x, lds, tid, P.tw_fwd, p);
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = red32(min(x[k], x[k] - 2 * p), p);   // [0, 3p] -> [0, p)
     } else {
-        fwd32_rounds<LOGN, 0, false>(x, lds, tid, P.tw_fwd, p);
+        fwd32_rounds<LOGN, 0, F32_WIDE>(x, lds, tid, P.tw_fwd, p);
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = red32(x[k], p);
     }
@@ -151,10 +167,14 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
 
 // ---------------------------------------------------------------- inverse (Gentleman-Sande)
 
-template <int LOGN, int LO, int BLO, int BHI>
+// Inputs below 2p.  Lazy primes (4p < 2^32): U + V < 4p is brought back below 2p by one
+// min-subtraction and U + 2p - V < 4p goes to the Shoup product as is (9 VALU per butterfly);
+// otherwise both inputs are first reduced to [0, p) (11 VALU).  Outputs below 2p, the last stage's
+// canonical.
+template <int LOGN, int LO, int BLO, int BHI, bool LAZY>
 __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Prime32& P) {
     constexpr int N = 1 << LOGN;
-    const uint32_t p = P.p;
+    const uint32_t p = P.p, p2 = 2 * p;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
 #pragma unroll
     for (int b = BLO; b <= BHI; ++b) {
@@ -167,20 +187,32 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m, k1 = k0 + half;
-                const uint32_t U = red32(x[k0], p), V = red32(x[k1], p);
-                if (b == LOGN - 1) {  // n^-1 folded in, canonical
-                    x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
-                    x[k1] = red32(shoup32(U + p - V, P.last_w, P.last_ws, p), p);
+                if constexpr (LAZY) {
+                    const uint32_t U = x[k0], V = x[k1];
+                    if (b == LOGN - 1) {  // n^-1 folded in, canonical
+                        x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
+                        x[k1] = red32(shoup32(U + p2 - V, P.last_w, P.last_ws, p), p);
+                    } else {
+                        const uint32_t sum = U + V;
+                        x[k0] = min(sum, sum - p2);
+                        x[k1] = shoup32(U + p2 - V, t.x, t.y, p);
+                    }
                 } else {
-                    x[k0] = U + V;
-                    x[k1] = shoup32(U + p - V, t.x, t.y, p);
+                    const uint32_t U = red32(x[k0], p), V = red32(x[k1], p);
+                    if (b == LOGN - 1) {  // n^-1 folded in, canonical
+                        x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
+                        x[k1] = red32(shoup32(U + p - V, P.last_w, P.last_ws, p), p);
+                    } else {
+                        x[k0] = U + V;
+                        x[k1] = shoup32(U + p - V, t.x, t.y, p);
+                    }
                 }
             }
         }
     }
 }
 
-template <int LOGN, int R>
+template <int LOGN, int R, bool LAZY>
 __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -192,8 +224,54 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
         lds_sync();
         lds32_load<LO>(lds, x, tid);
     }
-    inv32_round<LOGN, LO, BLO, BHI>(x, tid, P);
-    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1>(x, lds, tid, P);
+    inv32_round<LOGN, LO, BLO, BHI, LAZY>(x, tid, P);
+    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY>(x, lds, tid, P);
+}
+
+// inverse transform of x (inputs below 2p) in the form of the block's prime range
+template <int LOGN>
+__device__ __forceinline__ void inv32_any(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
+    if (form32(P.p) == F32_LAZY) inv32_rounds<LOGN, 0, true>(x, lds, tid, P);
+    else inv32_rounds<LOGN, 0, false>(x, lds, tid, P);
+}
+
+// One coefficient's centred Garner lift of its S residues v[s] (canonical mod p_s) evaluated mod
+// q_l = 2^60 - dq, plus r (canonical mod q_l): the result canonical.  The lift mod q is a Horner
+// evaluation x = a_0 + p_0 (a_1 + p_1 (a_2 + ...)) whose every step folds the 92-bit product through
+// 2^60 == d (5 instructions); the centring (x > floor(P/2)) is decided on the mixed-radix digits and
+// adds q - (P mod q).
+template <int S>
+__device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, const uint32_t (&pr)[S],
+                                             const uint32_t (&hp)[S], const Ks32Tables* __restrict__ KT, u64 q,
+                                             uint32_t dq, u64 negP) {
+    uint32_t a[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const uint32_t ps = pr[s];
+        uint32_t t = v[s];
+#pragma unroll
+        for (int kk = 0; kk < s; ++kk) {   // a_kk < p_kk < 2 p_s
+            t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
+            t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
+        }
+        a[s] = t;
+    }
+    bool gt = false, eq = true;
+#pragma unroll
+    for (int s = S - 1; s >= 0; --s) {
+        gt = gt || (eq && a[s] > hp[s]);
+        eq = eq && a[s] == hp[s];
+    }
+    u64 t = a[S - 1];
+#pragma unroll
+    for (int s = S - 2; s >= 0; --s) {
+        const u64 lo = (u64)(uint32_t)t * pr[s] + a[s];                      // < 2^63
+        const u64 hi = (u64)(uint32_t)(t >> 32) * pr[s] + (lo >> 32);         // x = hi 2^32 + lo.lo
+        const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
+        t = l60 + (hi >> 28) * dq;                                         // < 2^60 + 2^56
+    }
+    if (gt) t += negP;
+    return reduce_near60(t + r, q);                                        // t + r < 2^62
 }
 
 // Per (item, c, l) = block b: the S accumulated rows -> inverse NTT mod p_s -> centred Garner lift ->
@@ -220,7 +298,7 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
             const uint4 w = src[h];
             v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
         }
-        inv32_rounds<LOGN, 0>(v[s], lds, tid, primes[s]);
+        inv32_any<LOGN>(v[s], lds, tid, primes[s]);
     }
     uint32_t pr[S], hp[S];
 #pragma unroll
@@ -235,39 +313,10 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
     const u64* src = R + item * r_stride + (long)cl * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        // Garner over the p_s: a_s = (v_s - a_0 - a_1 p_0 - ...) / (p_0 ... p_{s-1}) mod p_s
-        uint32_t a[S];
+        uint32_t vk[S];
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const uint32_t ps = pr[s];
-            uint32_t t = v[s][k];
-#pragma unroll
-            for (int kk = 0; kk < s; ++kk) {   // a_kk < p_kk < 2 p_s
-                t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
-                t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
-            }
-            a[s] = t;
-        }
-        // centred: x > floor(P/2), on the mixed-radix digits, most significant first
-        bool gt = false, eq = true;
-#pragma unroll
-        for (int s = S - 1; s >= 0; --s) {
-            gt = gt || (eq && a[s] > hp[s]);
-            eq = eq && a[s] == hp[s];
-        }
-        const bool neg = gt;
-        // Horner mod q from the most significant digit; t < 2q between steps
-        u64 t = a[S - 1];
-#pragma unroll
-        for (int s = S - 2; s >= 0; --s) {
-            const u64 lo = (u64)(uint32_t)t * pr[s] + a[s];                      // < 2^63
-            const u64 hi = (u64)(uint32_t)(t >> 32) * pr[s] + (lo >> 32);         // x = hi 2^32 + lo.lo
-            const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
-            t = l60 + (hi >> 28) * dq;                                         // < 2^60 + 2^56
-        }
-        if (neg) t += negP;
-        t += src[k * T + tid];
-        x[k] = reduce_near60(t, q);                                                // t < 2^62
+        for (int s = 0; s < S; ++s) vk[s] = v[s][k];
+        x[k] = ks32_lift_one<S>(vk, src[k * T + tid], pr, hp, KT, q, dq, negP);
     }
 }
 

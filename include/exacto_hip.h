@@ -77,6 +77,8 @@ typedef struct exacto_ctx_info {
     int device;
     int ks32_primes;          /* primes of the 31-bit key-switch basis in use (0: limb-wise MAC) */
     int psum_max;             /* dbfv_mul: products per output limb scaled as one sum (0: per product) */
+    int ks32_lazy;            /* 1: the resident relinearisation key runs in the lazy 31-bit basis (primes
+                                 below 2^30, chosen from the key's own norms at its first use) */
 } exacto_ctx_info;
 
 /* ---- context: replaces BfvParamsBuilder::build + RnsBasis::new + make_plan ----

@@ -52,6 +52,25 @@ def test_worst_case_key_switch_cfg3(gpu_available):
     c1, c2 = pad(ct1, ct2, 200, q, n, 1)      # 200 products: two lanes of 100
     got = ctx.bfv_mul_and_relin(c1, c2)
     assert np.array_equal(got[:1], want)
+    # the sign-aligned key's L1 norms exceed the lazy basis' bound: the narrow basis runs it
+    assert not ctx.ks32_lazy
+
+
+def test_worst_case_digits_lazy_basis_cfg3(gpu_available):
+    """The same extreme digits (every one -B/2) with a uniform key: its norms (~n q / 4 per row) fit
+    the lazy basis (primes below 2^30), which then runs the key switch at its digit bound."""
+    prm = P.cfg3_params(4096)
+    q, n, G = prm.ct_basis.moduli, 4096, prm.gadget_digits
+    ct1, ct2, _, _ = W.digit_case_bfv(q, prm.plain_modulus, prm.gadget_base, G, n)
+    rlk = uniform_residues(np.random.default_rng(30), (G, 2), q, n)
+    want = cref.bfv_mul_and_relin(prm, ct1, ct2, rlk, threads=8)
+    ctx = HipContext.from_params(prm)
+    ctx.load_relin_key(rlk)
+    c1, c2 = pad(ct1, ct2, 200, q, n, 3)
+    got = ctx.bfv_mul_and_relin(c1, c2)
+    assert ctx.ks32_lazy
+    assert np.array_equal(got[:1], want)
+    assert np.array_equal(got[1:3], cref.bfv_mul_and_relin(prm, c1[1:3], c2[1:3], rlk, threads=8))
 
 
 @pytest.mark.parametrize("kind", ["digits", "tensor"])

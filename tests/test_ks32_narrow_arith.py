@@ -53,3 +53,90 @@ def test_narrow_butterfly_bounds_and_congruence():
             assert o0 < 3 * p and 0 < o1 <= 3 * p, (p, x0, x1, w, o0, o1)
             assert o0 % p == (x0 + x1 * w) % p
             assert o1 % p == (x0 - x1 * w) % p
+
+
+# ---- the lazy basis (every prime below 2^30, 4p < 2^32: F32_LAZY in ks32_dev.hpp) ----
+
+def _lazy_primes():
+    """The three largest primes p = 1 mod 2n below 2^30 for n = 1024 / 4096 / 8192 (the lazy bases
+    build_ks32_basis picks), and the smallest it may pick (just above 7/8 2^30)."""
+    out = []
+    for step in (2048, 8192, 16384):
+        p, got = (1 << 30) - step + 1, 0
+        while got < 3:
+            if all(p % d for d in range(3, int(p ** 0.5) + 1, 2)):
+                out.append(p)
+                got += 1
+            p -= step
+    p = (7 << 27) // 8192 * 8192 + 8192 + 1
+    while not all(p % d for d in range(3, int(p ** 0.5) + 1, 2)):
+        p += 8192
+    return out + [p]
+
+
+def _shoup(x, w, p):
+    ws = (w << 32) // p
+    return (x * w - ((x * ws) >> 32) * p) & M32
+
+
+def _lazy_fwd(x0, x1, w, p, canon=False):
+    X = x0 if canon else min(x0, (x0 - 2 * p) & M32)
+    qh = (x1 * ((w << 32) // p)) >> 32
+    o0 = (qh * ((-p) & M32) + x1 * w + X) & M32
+    o1 = (2 * X + 2 * p - o0) & M32
+    return X, o0, o1
+
+
+def _lazy_inv(u, v, w, p):
+    s = (u + v) & M32
+    return min(s, (s - 2 * p) & M32), _shoup((u + 2 * p - v) & M32, w, p)
+
+
+def _red_s64_lz(x, p):
+    """ks32.hip red_s64_lz: signed 64-bit x -> [0, 2p), x mod p."""
+    c32 = (1 << 32) % p
+    k63 = (-(1 << 63)) % p
+    xu = x & ((1 << 64) - 1)
+    hu = (xu >> 32) ^ 0x80000000
+    a = _shoup(hu, c32, p)
+    a = min(a, (a - p) & M32)
+    lo = xu & M32
+    b = (lo - (lo >> 30) * p) & M32
+    s = (a + b + k63) & M32
+    return min(s, (s - 2 * p) & M32)
+
+
+def test_lazy_butterflies_bounds_and_congruence():
+    rng = np.random.default_rng(30)
+    for p in _lazy_primes():
+        assert 4 * p <= M32
+        cases = [(4 * p - 1, M32, p - 1), (0, 0, 0), (2 * p, 4 * p - 1, 1), (2 * p - 1, 2 * p - 1, p - 1)]
+        cases += [(int(rng.integers(0, 4 * p)), int(rng.integers(0, 4 * p)), int(rng.integers(0, p)))
+                  for _ in range(3000)]
+        for x0, x1, w in cases:                      # forward: values in [0, 4p) between stages
+            X, o0, o1 = _lazy_fwd(x0, x1, w, p)
+            assert X < 2 * p and X % p == x0 % p
+            assert o0 < 4 * p and 0 < o1 < 4 * p, (p, x0, x1, w, o0, o1)
+            assert o0 % p == (x0 + x1 * w) % p and o1 % p == (x0 - x1 * w) % p
+        for x0, x1, w in cases[:1000]:               # first stage of round 0: canonical X
+            X, o0, o1 = _lazy_fwd(x0 % p, x1, w, p, canon=True)
+            assert o0 < 4 * p and 0 < o1 < 4 * p
+        for _, _, w in cases:                        # inverse: values in [0, 2p) between stages
+            u, v = int(rng.integers(0, 2 * p)), int(rng.integers(0, 2 * p))
+            o0, o1 = _lazy_inv(u, v, w, p)
+            assert o0 < 2 * p and o1 < 2 * p
+            assert o0 % p == (u + v) % p and o1 % p == ((u - v) * w) % p
+        for u, v in [(2 * p - 1, 0), (0, 2 * p - 1), (2 * p - 1, 2 * p - 1)]:
+            o0, o1 = _lazy_inv(u, v, p - 1, p)
+            assert o0 < 2 * p and o1 < 2 * p
+
+
+def test_lazy_mac_reduction():
+    """The MAC's lazy reduction of a signed 64-bit accumulator: [0, 2p), congruent (ks32.hip)."""
+    rng = np.random.default_rng(64)
+    for p in _lazy_primes():
+        xs = [0, 1, -1, (1 << 63) - 1, -(1 << 63), (1 << 62) + 12345, -(1 << 62) - 777]
+        xs += [int(v) for v in rng.integers(-(1 << 63), (1 << 63) - 1, size=2000, dtype=np.int64)]
+        for x in xs:
+            r = _red_s64_lz(x, p)
+            assert r < 2 * p and r % p == x % p, (p, x, r)
