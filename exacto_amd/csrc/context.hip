@@ -355,8 +355,32 @@ struct exacto_ctx {
     std::vector<ProfRec> recs;
 };
 
+// EXACTO_DEBUG_BOOT=1: every device allocation and release of the library is logged
+// to stderr with its pointer, size, pool and stream, and with the allocation range the runtime
+// reports for it (hipMemGetAddressRange), so that the failing bootstrap call's blocks can be checked
+// for overlap with any other live block.
+static bool dbg_alloc_on() {
+    static const bool on = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
+    return on;
+}
+static void dbg_alloc_log(const char* what, const void* p, size_t bytes, const void* pool, const void* stream,
+                          bool range) {
+    if (!dbg_alloc_on()) return;
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    if (range && p) {
+        if (hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)p) != hipSuccess) base = nullptr;
+        (void)hipGetLastError();   // a failed lookup must not reach the next CHECK_LAUNCH
+    }
+    std::fprintf(stderr, "alloc-dbg %s p=%p bytes=%zu pool=%p stream=%p range=%p+%zu\n", what, p, bytes, pool, stream,
+                 (void*)base, sz);
+}
+
 static void free_dev(void* p) {
-    if (p) (void)hipFree(p);
+    if (p) {
+        dbg_alloc_log("hipFree", p, 0, nullptr, nullptr, false);
+        (void)hipFree(p);
+    }
 }
 
 // Per-call scratch from the context's own stream-ordered pool (hipMallocFromPoolAsync / hipFreeAsync
@@ -372,13 +396,19 @@ struct Scratch {
     Scratch() = default;
     Scratch(const Scratch&) = delete;
     Scratch& operator=(const Scratch&) = delete;
+    hipMemPool_t from = nullptr;
     ~Scratch() {
-        if (p) (void)hipFreeAsync(p, s);
+        if (p) {
+            dbg_alloc_log("hipFreeAsync", p, 0, from, s, false);
+            (void)hipFreeAsync(p, s);
+        }
     }
     hipError_t alloc(size_t bytes, hipStream_t st, hipMemPool_t pool, bool debug) {
         s = st;
+        from = pool;
         hipError_t e = pool ? hipMallocFromPoolAsync(&p, std::max<size_t>(bytes, 8), pool, st)
                             : hipMallocAsync(&p, std::max<size_t>(bytes, 8), st);
+        if (e == hipSuccess) dbg_alloc_log(pool ? "hipMallocFromPoolAsync" : "hipMallocAsync", p, bytes, pool, st, true);
         if (e == hipSuccess && debug) e = hipMemsetAsync(p, 0xFF, std::max<size_t>(bytes, 8), st);
         return e;
     }
@@ -392,6 +422,7 @@ struct Scratch {
 static hipError_t dev_alloc(void** p, size_t bytes) {
     static const bool fill = [] { const char* e = getenv("EXACTO_DEBUG_FILL"); return e && e[0] == '1'; }();
     hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) dbg_alloc_log("hipMalloc", *p, bytes, nullptr, nullptr, true);
     if (e == hipSuccess && fill && bytes) {
         e = hipMemset(*p, 0xA5, bytes);
         if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -916,6 +947,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
             props.location.type = hipMemLocationTypeDevice;
             props.location.id = device;
             if (hipMemPoolCreate(p, &props) != hipSuccess) return (*p = nullptr, false);
+            dbg_alloc_log("hipMemPoolCreate", nullptr, 0, *p, nullptr, false);
             if (hipMemPoolSetAttribute(*p, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess) return true;
             (void)hipMemPoolDestroy(*p);
             return (*p = nullptr, false);
@@ -991,7 +1023,10 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->own_pool && c->pool) (void)hipMemPoolDestroy(c->pool);
+    if (c->own_pool && c->pool) {
+        dbg_alloc_log("hipMemPoolDestroy", nullptr, 0, c->pool, nullptr, false);
+        (void)hipMemPoolDestroy(c->pool);
+    }
     delete c;
 }
 
@@ -1257,8 +1292,8 @@ static int crt_mode(const exacto_ctx* c) {
 // (coefficient domain), balanced, reduced mod each p_s, forward NTT mod p_s -> dst [keys][2L][S][n]
 // (grown as needed).
 static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t** dst, size_t* cap, int S = 0,
-                            const Prime32* p32 = nullptr) {
-    if (!S) { S = c->S32; p32 = c->d_p32; }
+                            const Prime32* p32 = nullptr, int form = 0) {
+    if (!S) { S = c->S32; p32 = c->d_p32; form = c->ks32_mac_form; }
     const long rows = (long)keys * 2 * c->L;
     if (grow((u64**)dst, cap, std::max<size_t>((size_t)rows * S * c->n * sizeof(uint32_t), 8)))
         return EXACTO_ERR_HIP;
@@ -1269,7 +1304,7 @@ static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t
     nb.dst = ks.as<u64>(); nb.dst_item_stride = 2L * c->L * c->n;
     nb.ppi = 2 * c->L; nb.prime_base = 0; nb.period = c->L;
     if (int e = run_ntt(c, nb, rows, true)) return e;
-    ks32_key(ks.as<u64>(), *dst, rows, c->L, S, c->logn, p32, c->d_primes, c->stream);
+    ks32_key(ks.as<u64>(), *dst, rows, c->L, S, c->logn, p32, c->d_primes, form, c->stream);
     CHECK_LAUNCH();
     return 0;
 }
@@ -1337,7 +1372,7 @@ static int ensure_rs(exacto_ctx* c) {
 static int ensure_rs_wide(exacto_ctx* c) {
     if (c->kw.rs_valid) return 0;
     size_t cap = c->kw.rs_cap;
-    const int e = ks32_convert_key(c, c->d_rlk, c->rlk_keys, &c->kw.d_rs, &cap, c->kw.S, c->kw.d_p32);
+    const int e = ks32_convert_key(c, c->d_rlk, c->rlk_keys, &c->kw.d_rs, &cap, c->kw.S, c->kw.d_p32, c->kw.mac_form);
     c->kw.rs_cap = cap;
     if (e) return e;
     c->kw.rs_valid = true;
@@ -1497,7 +1532,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             if (!c->ks_defer) {   // (deferred: the caller sums the digits of products first, dbfv_mul_core)
                 {   // int16 digit in (2 B), 31-bit residue out (4 B) per coefficient and prime
                     ProfScope pd(c, PK_KS_DIGITS, (u64)cnt * guse * c->S32, 6.0 * n * cnt * guse * c->S32);
-                    ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->stream);
+                    ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, c->S32, c->logn, c->d_p32, c->ks32_mac_form, c->stream);
                 }
                 {   // per (item, prime, coefficient): G digit residues in, 2L sums out (the key slice from LDS)
                     ProfScope pm(c, PK_KS_MAC, (u64)cnt * c->S32, 4.0 * n * cnt * c->S32 * (guse + 2.0 * L));
@@ -1505,7 +1540,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                 }
                 {   // per (item, component, limb): S 31-bit sums in, R in and out
                     ProfScope pc(c, PK_KS_CRT, (u64)cnt * 2 * L, (double)n * cnt * 2 * L * (4.0 * c->S32 + 16.0));
-                    ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes,
+                    ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->ks32_mac_form,
                              c->stream);
                 }
                 CHECK_LAUNCH();
@@ -2122,8 +2157,8 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         }
         {
             ProfScope pn(c, PK_KS_DIGITS, (u64)Bd * gu * S, nn * Bd * gu * S * (ds + 4.0));
-            if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
-            else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, c->stream);
+            if (wide) ks32_digits32((const int32_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, mac_form, c->stream);
+            else ks32_digits((const int16_t*)c->d_dk, c->d_dsk, (int)Bd, (int)gu, S, c->logn, p32, mac_form, c->stream);
         }
         {
             ProfScope pm(c, PK_KS_MAC, (u64)Bd * S, 4.0 * nn * Bd * S * (gu + 2.0 * c->L));
@@ -2132,7 +2167,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         }
         {
             ProfScope pc(c, PK_KS_CRT, (u64)Bd * 2 * c->L, nn * Bd * 2 * c->L * (4.0 * S + 16.0));
-            ks32_crt(c->d_uk, cf, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, c->stream);
+            ks32_crt(c->d_uk, cf, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, mac_form, c->stream);
         }
         CHECK_LAUNCH();
     }
@@ -2682,7 +2717,7 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
     const bool k32 = d16 && c->ks32 && kb.S > 0 && c->path == EXACTO_PATH_EXACT_RNS;
     if (k32) {
         size_t cap = c->gk_rs_cap;
-        const int e = ks32_convert_key(c, gk, (size_t)guse, &c->d_gk_rs, &cap, kb.S, kb.d_p32);
+        const int e = ks32_convert_key(c, gk, (size_t)guse, &c->d_gk_rs, &cap, kb.S, kb.d_p32, kb.mac_form);
         c->gk_rs_cap = cap;
         if (e) return e;
     } else {
@@ -2719,9 +2754,9 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
             CHECK_LAUNCH();
             launch_rows(c->ws_T + Ln, 2 * Ln, nullptr, 0, Ln, cnt, c->stream);
             CHECK_LAUNCH();
-            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, kb.S, c->logn, kb.d_p32, c->stream);
+            ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, kb.S, c->logn, kb.d_p32, kb.mac_form, c->stream);
             ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, kb.S, n, kb.d_p32, kb.mac_form, c->stream);
-            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, kb.S, c->logn, kb.d_kst, kb.d_p32, c->d_primes, c->stream);
+            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, kb.S, c->logn, kb.d_kst, kb.d_p32, c->d_primes, kb.mac_form, c->stream);
             CHECK_LAUNCH();
             NttBatch rb{};
             rb.src = c->ws_T; rb.src_item_stride = 2 * Ln;
@@ -3361,6 +3396,9 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
     u64* c0pt = c0pt_s.as<u64>();
     u64* c1pt = c0pt + B * n;
+    // debug: the library's generic writers (rows / copy / fill kernels) report writes into c0pt and
+    // c1pt from here to the end of the call (the rows copies below are the expected ones, kind 0)
+    if (dbg.on && rc == 0) debug_watch_set(c0pt, c0pt + 2 * B * n, b->stream);
     dbg.snap("small_again", small, B * 2 * n);
     dbg.xsnap("small", small);
     dbg.xsnap("c0pt_before", c0pt);
@@ -3412,6 +3450,14 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     }
     rc = drain.finish(rc);
     dbg.dump();
+    if (dbg.on) {
+        std::fprintf(stderr, "boot-dbg watch c0pt=%p..%p hits=0x%x (bit k: 0 rows copy, 1 rows zero, 2 copy_u64, "
+                     "3 fill 0, 4 fill other)\n", (void*)c0pt, (void*)(c0pt + 2 * B * n), debug_watch_hits(b->stream));
+        debug_watch_set(nullptr, nullptr, b->stream);
+        std::fprintf(stderr, "boot-dbg ptrs coef=%p small=%p flags=%p c0pt=%p out=%p o.pool=%p b.pool=%p o.stream=%p "
+                     "b.stream=%p\n", (void*)coef, (void*)small, (void*)flags, (void*)c0pt, (void*)out, (void*)o->pool,
+                     (void*)b->pool, (void*)o->stream, (void*)b->stream);
+    }
     return rc;
 }
 

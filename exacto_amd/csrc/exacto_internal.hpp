@@ -102,20 +102,23 @@ struct Ks32Tables {
     u64 negP[EXACTO_MAX_L];                               // (q_l - P mod q_l) mod q_l
 };
 // int16 digits [items][G][n] -> DS [items][G][S][n], NTT mod p_s
+// form: the basis' butterfly form, 0 primes up to 2^31, 1 below 2^32 / 3, 2 below 2^30 (lazy)
+// (ks32_dev.hpp F32_*; Ks32Basis::mac_form)
 void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
-                 hipStream_t st);
+                 int form, hipStream_t st);
 void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
-                   hipStream_t st);
+                   int form, hipStream_t st);
 // key rows [rows][n] (coefficient domain, canonical mod q_{row % L}) -> RS [rows][S][n]
 void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
-              const PrimeConst* qprimes, hipStream_t st);
-// U [items][2L][S][n] = sum_g DS (.) RS
+              const PrimeConst* qprimes, int form, hipStream_t st);
+// per key row: sum_j floor(|balanced r_j| / 2^20) (the lazy basis' key-norm bound)
 void ks32_key_norms(const u64* K, u64* out, long rows, int L, int n, const PrimeConst* qprimes, hipStream_t st);
+// U [items][2L][S][n] = sum_g DS (.) RS
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
               const Prime32* primes, int mac_form, hipStream_t st);
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
-              const Prime32* primes, const PrimeConst* qprimes, hipStream_t st);
+              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st);
 
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item
@@ -183,6 +186,9 @@ void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, lon
 void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s);
 void launch_xcd_probe(const u64* src, u64* dst, long words, uint32_t* xcc, int blocks, hipStream_t s);
 void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s);
+// EXACTO_DEBUG_BOOT: watch a byte range for writes by rows / copy / fill (kernels.hip g_dbg_watch)
+void debug_watch_set(const void* lo, const void* hi, hipStream_t s);
+uint32_t debug_watch_hits(hipStream_t s);
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
                       hipStream_t s);

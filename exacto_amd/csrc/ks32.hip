@@ -30,7 +30,7 @@ namespace exacto {
 // ---------------------------------------------------------------- kernels
 
 // digits [item][g][n] (int16, or int32 for dBFV digit sums beyond int16) -> DS [item][g][s][n]
-template <int LOGN, typename DT>
+template <int LOGN, typename DT, int FORM>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
 ks32_digit_ntt_kernel(const DT* __restrict__ D16, uint32_t* __restrict__ DS, int G, int S,
                       const Prime32* __restrict__ primes) {
@@ -48,11 +48,11 @@ ks32_digit_ntt_kernel(const DT* __restrict__ D16, uint32_t* __restrict__ DS, int
         const int d = src[tid + k * T];
         x[k] = d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
     }
-    fwd32_store<LOGN>(x, lds, tid, P, DS + (long)b * N);
+    fwd32_store<LOGN, FORM>(x, lds, tid, P, DS + (long)b * N);
 }
 
 // key rows [rows][n] canonical mod q_{row's limb} (u64) -> RS [rows][S][n]: balanced, mod p_s, NTT
-template <int LOGN>
+template <int LOGN, int FORM>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
 ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int S,
                 const Prime32* __restrict__ primes, const PrimeConst* __restrict__ qprimes) {
@@ -78,7 +78,7 @@ ks32_key_kernel(const u64* __restrict__ K, uint32_t* __restrict__ RS, int L, int
             x[k] = (uint32_t)(r % P.p);
         }
     }
-    fwd32_store<LOGN>(x, lds, tid, P, RS + (long)b * N);
+    fwd32_store<LOGN, FORM>(x, lds, tid, P, RS + (long)b * N);
 }
 
 // Per key row [rows][n] (coefficient domain, canonical mod q_{row's limb}): sum_j floor(|r_j| / 2^20)
@@ -198,7 +198,7 @@ ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t
     }
 }
 
-template <int LOGN, int S>
+template <int LOGN, int S, bool LAZY>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
 ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
                 const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
@@ -208,7 +208,7 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;             // (item, cl)
     u64 x[16];
-    ks32_crt_values<LOGN, S>(x, U, R, r_stride, L, b, lds, tid, KT, primes, qprimes);
+    ks32_crt_values<LOGN, S, LAZY>(x, U, R, r_stride, L, b, lds, tid, KT, primes, qprimes);
     const uint32_t CL = 2 * L;
     const long item = b / CL;
     u64* dst = R + item * r_stride + (long)(b - (uint32_t)item * CL) * N;
@@ -222,7 +222,7 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
 // j = tid + S T m (coalesced R reads and stores).  The serial form above runs the S transforms one
 // after the other in 4 waves (the launch's 12 waves per SIMD then issue at 0.68); here a block has
 // S times the independent waves.  n <= 4096 (S n/16 <= 1024 threads).
-template <int LOGN, int S>
+template <int LOGN, int S, bool LAZY>
 __global__ void __launch_bounds__(S * (1 << LOGN) / 16)
 ks32_crt_par_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
                     const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
@@ -241,7 +241,7 @@ ks32_crt_par_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_
             const uint4 w = src[h];
             v[4 * h] = w.x; v[4 * h + 1] = w.y; v[4 * h + 2] = w.z; v[4 * h + 3] = w.w;
         }
-        inv32_any<LOGN>(v, my, lt, primes[g]);
+        inv32_rounds<LOGN, 0, LAZY>(v, my, lt, primes[g]);
         // element k T + lt is in v[k]; the last round's exchange reads are done before the slice
         // is overwritten with the natural-order result
         lds_sync();
@@ -325,26 +325,42 @@ ks32_digit_sum_kernel(const IT* __restrict__ D, int npairs, const int* __restric
 
 // ---------------------------------------------------------------- launchers
 
+// form: the basis' butterfly form (F32_WIDE / F32_NARROW / F32_LAZY = Ks32Basis::mac_form), a
+// template parameter of every kernel (a runtime branch kept the union of both forms' registers)
+#define FORM_SWITCH(form, CALL)                          \
+    switch (form) {                                      \
+        case F32_LAZY: CALL(F32_LAZY); break;            \
+        case F32_NARROW: CALL(F32_NARROW); break;        \
+        default: CALL(F32_WIDE); break;                  \
+    }
+
 template <int LOGN>
 static void ks32_launch_digits(const void* D, bool wide, uint32_t* DS, int items, int G, int S, const Prime32* primes,
-                               hipStream_t st) {
+                               int form, hipStream_t st) {
     const dim3 grid((unsigned)((long)items * G * S)), block((1 << LOGN) / 16);
-    if (wide)
-        hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int32_t>), grid, block, 0, st, (const int32_t*)D, DS, G, S,
-                           primes);
-    else
-        hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int16_t>), grid, block, 0, st, (const int16_t*)D, DS, G, S,
-                           primes);
+#define DIG_(F_)                                                                                                \
+    do {                                                                                                        \
+        if (wide)                                                                                               \
+            hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int32_t, F_>), grid, block, 0, st, (const int32_t*)D, \
+                               DS, G, S, primes);                                                               \
+        else                                                                                                    \
+            hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int16_t, F_>), grid, block, 0, st, (const int16_t*)D, \
+                               DS, G, S, primes);                                                               \
+    } while (0)
+    FORM_SWITCH(form, DIG_)
+#undef DIG_
 }
 
 template <int LOGN>
 static void ks32_launch_key(const u64* K, uint32_t* RS, long rows, int L, int S, const Prime32* primes,
-                            const PrimeConst* qprimes, hipStream_t st) {
-    hipLaunchKernelGGL((ks32_key_kernel<LOGN>), dim3((unsigned)(rows * S)), dim3((1 << LOGN) / 16), 0, st, K, RS, L,
-                       S, primes, qprimes);
+                            const PrimeConst* qprimes, int form, hipStream_t st) {
+#define KEY_(F_) hipLaunchKernelGGL((ks32_key_kernel<LOGN, F_>), dim3((unsigned)(rows * S)), dim3((1 << LOGN) / 16), 0, \
+                                    st, K, RS, L, S, primes, qprimes)
+    FORM_SWITCH(form, KEY_)
+#undef KEY_
 }
 
-template <int LOGN>
+template <int LOGN, bool LAZY>
 static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
                             const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
     const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
@@ -353,22 +369,22 @@ static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items,
     static const bool par = [] { const char* e = std::getenv("EXACTO_KS_CRT_PAR"); return !(e && e[0] == '0'); }();
     if constexpr (LOGN <= 12) {
         if (par && S == 3) {
-            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 3>), grid, dim3(3 * block.x), 0, st, U, R, r_stride, L, KT,
-                               primes, qprimes);
+            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 3, LAZY>), grid, dim3(3 * block.x), 0, st, U, R, r_stride, L,
+                               KT, primes, qprimes);
             return;
         }
         if (par && S == 2) {
-            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 2>), grid, dim3(2 * block.x), 0, st, U, R, r_stride, L, KT,
-                               primes, qprimes);
+            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 2, LAZY>), grid, dim3(2 * block.x), 0, st, U, R, r_stride, L,
+                               KT, primes, qprimes);
             return;
         }
     }
     if (S == 2)
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else if (S == 3)
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 3>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 3, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 4>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 4, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
 }
 
 #define KS32_SWITCH(logn, CALL)                  \
@@ -381,26 +397,26 @@ static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items,
         default: break;                          \
     }
 
-void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+void ks32_digits(const int16_t* D16, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes, int form,
                  hipStream_t st) {
     if (items <= 0) return;
-#define CALL(L_) ks32_launch_digits<L_>(D16, false, DS, items, G, S, primes, st)
+#define CALL(L_) ks32_launch_digits<L_>(D16, false, DS, items, G, S, primes, form, st)
     KS32_SWITCH(logn, CALL)
 #undef CALL
 }
 
-void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes,
+void ks32_digits32(const int32_t* D, uint32_t* DS, int items, int G, int S, int logn, const Prime32* primes, int form,
                    hipStream_t st) {
     if (items <= 0) return;
-#define CALL(L_) ks32_launch_digits<L_>(D, true, DS, items, G, S, primes, st)
+#define CALL(L_) ks32_launch_digits<L_>(D, true, DS, items, G, S, primes, form, st)
     KS32_SWITCH(logn, CALL)
 #undef CALL
 }
 
 void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, const Prime32* primes,
-              const PrimeConst* qprimes, hipStream_t st) {
+              const PrimeConst* qprimes, int form, hipStream_t st) {
     if (rows <= 0) return;
-#define CALL(L_) ks32_launch_key<L_>(K, RS, rows, L, S, primes, qprimes, st)
+#define CALL(L_) ks32_launch_key<L_>(K, RS, rows, L, S, primes, qprimes, form, st)
     KS32_SWITCH(logn, CALL)
 #undef CALL
 }
@@ -463,9 +479,13 @@ void ks32_digit_sum(const void* D, bool in8, int npairs, const int* term_start, 
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
-              const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
+              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st) {
     if (items <= 0) return;
-#define CALL(L_) ks32_launch_crt<L_>(U, R, r_stride, items, L, S, KT, primes, qprimes, st)
+#define CALL(L_)                                                                                           \
+    do {                                                                                                   \
+        if (form == F32_LAZY) ks32_launch_crt<L_, true>(U, R, r_stride, items, L, S, KT, primes, qprimes, st); \
+        else ks32_launch_crt<L_, false>(U, R, r_stride, items, L, S, KT, primes, qprimes, st);                \
+    } while (0)
     KS32_SWITCH(logn, CALL)
 #undef CALL
 }

@@ -61,15 +61,13 @@ __device__ __forceinline__ u64 lo_only(uint32_t x) {
     return __builtin_bit_cast(u64, v);
 }
 
-// Prime ranges of a 31-bit basis, and the butterfly form each takes (block-uniform choice):
+// Prime ranges of a 31-bit basis, and the butterfly form each takes (a template parameter of the
+// kernels, chosen on the host from the basis: Ks32Basis::mac_form uses the same numbering):
 //   F32_LAZY   p < 2^30 (4p < 2^32): Harvey's lazy butterflies, values in [0, 4p) forward and
 //              [0, 2p) inverse between stages, one conditional subtraction per butterfly;
 //   F32_NARROW p < 2^32 / 3: values in [0, 3p] forward, both inverse inputs reduced to [0, p);
 //   F32_WIDE   p < 2^31: values below 2p, every operand reduced to [0, p).
 enum { F32_WIDE = 0, F32_NARROW = 1, F32_LAZY = 2 };
-__device__ __forceinline__ int form32(uint32_t p) {
-    return p < (1u << 30) ? F32_LAZY : p <= 0x55555555u ? F32_NARROW : F32_WIDE;
-}
 
 // One round: stage bits BHI..LO of the 4-bit window at LO.
 // Narrow primes (3p < 2^32): values in [0, 3p] between stages.  X is brought to [0, p) (two
@@ -136,25 +134,15 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
 // x (element tid + k T, canonical: round 0 relies on it) -> NTT, stored coalesced at dst (element tid + k T of the
 // bit-reversed-order evaluation array), as balanced residues in (-p/2, p/2] (int32 bits): the
 // only consumer, ks32_mac_kernel, multiplies balanced values
-template <int LOGN>
+template <int LOGN, int FORM>
 __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P,
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     const uint32_t p = P.p, half = p >> 1;
-    const int form = form32(p);   // block-uniform
-    if (form == F32_LAZY) {
-        fwd32_rounds<LOGN, 0, F32_LAZY>(x, lds, tid, P.tw_fwd, p);
+    fwd32_rounds<LOGN, 0, FORM>(x, lds, tid, P.tw_fwd, p);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = red32(min(x[k], x[k] - 2 * p), p);   // [0, 4p) -> [0, p)
-    } else if (form == F32_NARROW) {
-        fwd32_rounds<LOGN, 0, F32_NARROW>(x, lds, tid, P.tw_fwd, p);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = red32(min(x[k], x[k] - 2 * p), p);   // [0, 3p] -> [0, p)
-    } else {
-        fwd32_rounds<LOGN, 0, F32_WIDE>(x, lds, tid, P.tw_fwd, p);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = red32(x[k], p);
-    }
+    for (int k = 0; k < 16; ++k)   // lazy [0, 4p) / narrow [0, 3p] / wide [0, 2p) -> [0, p)
+        x[k] = FORM == F32_WIDE ? red32(x[k], p) : red32(min(x[k], x[k] - 2 * p), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = x[k] > half ? x[k] - p : x[k];
     lds_sync();
@@ -228,13 +216,6 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
     if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY>(x, lds, tid, P);
 }
 
-// inverse transform of x (inputs below 2p) in the form of the block's prime range
-template <int LOGN>
-__device__ __forceinline__ void inv32_any(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
-    if (form32(P.p) == F32_LAZY) inv32_rounds<LOGN, 0, true>(x, lds, tid, P);
-    else inv32_rounds<LOGN, 0, false>(x, lds, tid, P);
-}
-
 // One coefficient's centred Garner lift of its S residues v[s] (canonical mod p_s) evaluated mod
 // q_l = 2^60 - dq, plus r (canonical mod q_l): the result canonical.  The lift mod q is a Horner
 // evaluation x = a_0 + p_0 (a_1 + p_1 (a_2 + ...)) whose every step folds the 92-bit product through
@@ -279,7 +260,7 @@ __device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, cons
 // coefficient domain).  The lift mod q = 2^60 - d is a Horner evaluation x = a_0 + p_0 (a_1 + p_1
 // (a_2 + ...)) whose every step folds the 92-bit product through 2^60 == d (5 instructions); the
 // centring (x > floor(P/2)) is decided on the mixed-radix digits and adds q - (P mod q).
-template <int LOGN, int S>
+template <int LOGN, int S, bool LAZY>
 __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __restrict__ U, const u64* __restrict__ R,
                                                 long r_stride, int L, uint32_t b, uint32_t* lds, int tid,
                                                 const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
@@ -298,7 +279,7 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
             const uint4 w = src[h];
             v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
         }
-        inv32_any<LOGN>(v[s], lds, tid, primes[s]);
+        inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
     }
     uint32_t pr[S], hp[S];
 #pragma unroll
