@@ -355,12 +355,12 @@ struct exacto_ctx {
     std::vector<ProfRec> recs;
 };
 
-// EXACTO_DEBUG_BOOT=1: every device allocation and release of the library is logged
-// to stderr with its pointer, size, pool and stream, and with the allocation range the runtime
-// reports for it (hipMemGetAddressRange), so that the failing bootstrap call's blocks can be checked
-// for overlap with any other live block.
-static bool dbg_alloc_on() {
-    static const bool on = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
+// EXACTO_DEBUG_ALLOC=1: every device allocation and release of the library is logged
+// to stderr with its pointer, size, pool and stream; =2 adds the allocation range the runtime reports
+// for it (hipMemGetAddressRange), so that the failing bootstrap call's blocks can be checked for
+// overlap with any other live block.  (Round 5: with the range lookups the failure no longer showed.)
+static int dbg_alloc_on() {
+    static const int on = [] { const char* e = getenv("EXACTO_DEBUG_ALLOC"); return e ? atoi(e) : 0; }();
     return on;
 }
 static void dbg_alloc_log(const char* what, const void* p, size_t bytes, const void* pool, const void* stream,
@@ -368,7 +368,7 @@ static void dbg_alloc_log(const char* what, const void* p, size_t bytes, const v
     if (!dbg_alloc_on()) return;
     hipDeviceptr_t base = nullptr;
     size_t sz = 0;
-    if (range && p) {
+    if (range && p && dbg_alloc_on() > 1) {
         if (hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)p) != hipSuccess) base = nullptr;
         (void)hipGetLastError();   // a failed lookup must not reach the next CHECK_LAUNCH
     }
@@ -3280,17 +3280,20 @@ struct BootDebug {
     u64* dbuf = nullptr;
     u64* xbuf = nullptr;
     uint32_t* xcc = nullptr;
+    uint32_t* whit = nullptr;   // write-watch flags (kernels.hip DbgWatch)
     std::vector<std::pair<std::string, size_t>> names;
     std::vector<std::string> xnames;
     explicit BootDebug(hipStream_t st) : s(st) {
         static const bool env = [] { const char* e = getenv("EXACTO_DEBUG_BOOT"); return e && e[0] == '1'; }();
         on = env && hipMalloc((void**)&dbuf, DN * DW * sizeof(u64)) == hipSuccess &&
              hipMalloc((void**)&xbuf, XN * XB * 4 * sizeof(u64)) == hipSuccess &&
-             hipMalloc((void**)&xcc, XN * XB * sizeof(uint32_t)) == hipSuccess;
+             hipMalloc((void**)&xcc, XN * XB * sizeof(uint32_t)) == hipSuccess &&
+             hipMalloc((void**)&whit, 8 * sizeof(uint32_t)) == hipSuccess;
+        if (on) launch_fill_u32(whit, 0, 8, s);
     }
     ~BootDebug() {
-        if (dbuf || xbuf || xcc) (void)hipStreamSynchronize(s);
-        free_dev(dbuf); free_dev(xbuf); free_dev(xcc);
+        if (dbuf || xbuf || xcc || whit) (void)hipStreamSynchronize(s);
+        free_dev(dbuf); free_dev(xbuf); free_dev(xcc); free_dev(whit);
     }
     // null source (an earlier allocation failed; the call's rc carries the real error): skipped, so the
     // diagnostic never faults the GPU and hides that error
@@ -3398,7 +3401,18 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     u64* c1pt = c0pt + B * n;
     // debug: the library's generic writers (rows / copy / fill kernels) report writes into c0pt and
     // c1pt from here to the end of the call (the rows copies below are the expected ones, kind 0)
-    if (dbg.on && rc == 0) debug_watch_set(c0pt, c0pt + 2 * B * n, b->stream);
+    // EXACTO_DEBUG_WATCH=1: the watch alone, its flag buffer allocated once per process (the least
+    // perturbing diagnostic: the snapshots' per-call allocations made the failure disappear in round 5)
+    static uint32_t* watch_hit = [] {
+        uint32_t* p = nullptr;
+        const char* e = getenv("EXACTO_DEBUG_WATCH");
+        if (e && e[0] == '1' && hipMalloc((void**)&p, 8 * sizeof(uint32_t)) == hipSuccess &&
+            hipMemset(p, 0, 8 * sizeof(uint32_t)) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+            return p;
+        return (uint32_t*)nullptr;
+    }();
+    uint32_t* whit = dbg.on ? dbg.whit : watch_hit;
+    if (whit && rc == 0) debug_watch_set(c0pt, c0pt + 2 * B * n, whit);
     dbg.snap("small_again", small, B * 2 * n);
     dbg.xsnap("small", small);
     dbg.xsnap("c0pt_before", c0pt);
@@ -3450,10 +3464,17 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     }
     rc = drain.finish(rc);
     dbg.dump();
-    if (dbg.on) {
+    if (whit) {
+        debug_watch_set(nullptr, nullptr, nullptr);
+        uint32_t hh[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        (void)hipMemcpy(hh, whit, sizeof(hh), hipMemcpyDeviceToHost);
+        (void)hipMemset(whit, 0, sizeof(hh));
+        uint32_t hits = 0;
+        for (int k = 0; k < 8; ++k) hits |= hh[k] ? (1u << k) : 0;
         std::fprintf(stderr, "boot-dbg watch c0pt=%p..%p hits=0x%x (bit k: 0 rows copy, 1 rows zero, 2 copy_u64, "
-                     "3 fill 0, 4 fill other)\n", (void*)c0pt, (void*)(c0pt + 2 * B * n), debug_watch_hits(b->stream));
-        debug_watch_set(nullptr, nullptr, b->stream);
+                     "3 fill 0, 4 fill other)\n", (void*)c0pt, (void*)(c0pt + 2 * B * n), hits);
+    }
+    if (dbg.on) {
         std::fprintf(stderr, "boot-dbg ptrs coef=%p small=%p flags=%p c0pt=%p out=%p o.pool=%p b.pool=%p o.stream=%p "
                      "b.stream=%p\n", (void*)coef, (void*)small, (void*)flags, (void*)c0pt, (void*)out, (void*)o->pool,
                      (void*)b->pool, (void*)o->stream, (void*)b->stream);

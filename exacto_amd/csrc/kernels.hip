@@ -1218,41 +1218,33 @@ relin_mac_lds_kernel(const u64* __restrict__ base, long base_stride, const u64* 
 // Strided row copy / zero fill: dst[r * dst_stride + k] = src ? src[r * src_stride + k] : 0 for
 // k < len, r < rows: the strided ciphertext-component fills and copies as one ordinary kernel on
 // the context stream (no 2D memset/memcpy engine path).
-// EXACTO_DEBUG_BOOT: a watched byte range [lo, hi) (lo >= hi: off); the library's
-// generic writers (rows, copy, fill) record in g_dbg_watch_hit[kind] (a vector store) when they write
-// inside it: 0 rows copy, 1 rows zero fill, 2 copy_u64, 3 fill_u32 of 0, 4 fill_u32 of another value
-__device__ u64 g_dbg_watch[2];
-__device__ uint32_t g_dbg_watch_hit[8];
-__device__ __forceinline__ void dbg_watch(const void* a, int kind) {
+// EXACTO_DEBUG_BOOT: a watched byte range [lo, hi) (lo >= hi: off), passed to the
+// library's generic writers (rows, copy, fill) as kernel arguments; a write inside it sets
+// hit[kind] (a vector store): 0 rows copy, 1 rows zero fill, 2 copy_u64, 3 fill_u32 of 0, 4 fill_u32
+// of another value.  Arguments rather than a device symbol: setting a symbol needs a copy and a
+// synchronisation on the stream, and with those the round-5 failing runs no longer failed.
+struct DbgWatch {
+    u64 lo = 0, hi = 0;
+    uint32_t* hit = nullptr;
+};
+static DbgWatch g_watch;   // host side, read by the launchers below
+__device__ __forceinline__ void dbg_watch(const void* a, int kind, u64 lo, u64 hi, uint32_t* hit) {
     const u64 x = (u64)a;
-    if (x >= g_dbg_watch[0] && x < g_dbg_watch[1]) g_dbg_watch_hit[kind] = 1;
+    if (x >= lo && x < hi) hit[kind] = 1;
 }
 
-void debug_watch_set(const void* lo, const void* hi, hipStream_t s) {
-    static u64 h[2];   // static: the copy reads it after this returns
-    h[0] = (u64)lo;
-    h[1] = (u64)hi;
-    static const uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg_watch_hit), z, sizeof(z), 0, hipMemcpyHostToDevice, s);
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dbg_watch), h, sizeof(h), 0, hipMemcpyHostToDevice, s);
-    (void)hipStreamSynchronize(s);
-}
-
-uint32_t debug_watch_hits(hipStream_t s) {
-    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg_watch_hit), sizeof(h), 0, hipMemcpyDeviceToHost);
-    uint32_t m = 0;
-    for (int k = 0; k < 8; ++k) m |= h[k] ? (1u << k) : 0;
-    return m;
+void debug_watch_set(const void* lo, const void* hi, uint32_t* hit) {
+    g_watch.lo = (u64)lo;
+    g_watch.hi = (u64)hi;
+    g_watch.hit = hit;
 }
 
 __global__ void __launch_bounds__(TPB)
 rows_kernel(u64* __restrict__ dst, long dst_stride, const u64* __restrict__ src, long src_stride, long len,
-            long total) {
+            long total, u64 wlo, u64 whi, uint32_t* whit) {
     for (long t = (long)blockIdx.x * TPB + threadIdx.x; t < total; t += (long)gridDim.x * TPB) {
         const long r = t / len, k = t - r * len;
-        dbg_watch(&dst[r * dst_stride + k], src ? 0 : 1);
+        dbg_watch(&dst[r * dst_stride + k], src ? 0 : 1, wlo, whi, whit);
         dst[r * dst_stride + k] = src ? src[r * src_stride + k] : 0;
     }
 }
@@ -1276,7 +1268,7 @@ void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, lon
     if (total <= 0) return;
     const long blocks = std::min<long>((total + TPB - 1) / TPB, 65536);
     hipLaunchKernelGGL(rows_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, dst, dst_stride, src, src_stride, len,
-                       total);
+                       total, g_watch.lo, g_watch.hi, g_watch.hit);
 }
 
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
@@ -1400,10 +1392,10 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
 
 // dst <- src, u64 words, as a kernel (context.hip dev_copy: the library's device copies)
 __global__ void __launch_bounds__(256)
-copy_u64_kernel(u64* __restrict__ dst, const u64* __restrict__ src, long words) {
+copy_u64_kernel(u64* __restrict__ dst, const u64* __restrict__ src, long words, u64 wlo, u64 whi, uint32_t* whit) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-        dbg_watch(&dst[i], 2);
+        dbg_watch(&dst[i], 2, wlo, whi, whit);
         dst[i] = src[i];
     }
 }
@@ -1412,15 +1404,16 @@ void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words);
+    hipLaunchKernelGGL(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words, g_watch.lo, g_watch.hi,
+                       g_watch.hit);
 }
 
 
 __global__ void __launch_bounds__(256)
-fill_u32_kernel(uint32_t* __restrict__ dst, uint32_t v, long words) {
+fill_u32_kernel(uint32_t* __restrict__ dst, uint32_t v, long words, u64 wlo, u64 whi, uint32_t* whit) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-        dbg_watch(&dst[i], v == 0 ? 3 : 4);
+        dbg_watch(&dst[i], v == 0 ? 3 : 4, wlo, whi, whit);
         dst[i] = v;
     }
 }
@@ -1429,7 +1422,8 @@ void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words);
+    hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words, g_watch.lo, g_watch.hi,
+                       g_watch.hit);
 }
 
 }  // namespace exacto

@@ -216,66 +216,6 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     for (int k = 0; k < 16; ++k) dst[k * T + tid] = x[k];
 }
 
-// The same per (item, c, l) block with its S inverse transforms run side by side: S groups of n/16
-// threads (S waves-groups, 12 waves at n = 4096, S = 3), group s transforms row s in its own LDS
-// slice, leaves the coefficients there in natural order, and then every thread lifts coefficients
-// j = tid + S T m (coalesced R reads and stores).  The serial form above runs the S transforms one
-// after the other in 4 waves (the launch's 12 waves per SIMD then issue at 0.68); here a block has
-// S times the independent waves.  n <= 4096 (S n/16 <= 1024 threads).
-template <int LOGN, int S, bool LAZY>
-__global__ void __launch_bounds__(S * (1 << LOGN) / 16)
-ks32_crt_par_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
-                    const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
-                    const PrimeConst* __restrict__ qprimes) {
-    constexpr int N = 1 << LOGN, T = N / 16, TT = S * T;
-    __shared__ uint32_t lds[S * N];
-    const int tid = threadIdx.x;
-    const int g = tid / T, lt = tid - g * T;        // group = prime s, thread within it
-    const uint32_t b = blockIdx.x;                  // (item, cl)
-    uint32_t* my = lds + g * N;
-    {
-        uint32_t v[16];
-        const uint4* src = reinterpret_cast<const uint4*>(U + ((long)b * S + g) * N + 16 * lt);
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const uint4 w = src[h];
-            v[4 * h] = w.x; v[4 * h + 1] = w.y; v[4 * h + 2] = w.z; v[4 * h + 3] = w.w;
-        }
-        inv32_rounds<LOGN, 0, LAZY>(v, my, lt, primes[g]);
-        // element k T + lt is in v[k]; the last round's exchange reads are done before the slice
-        // is overwritten with the natural-order result
-        lds_sync();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) my[k * T + lt] = v[k];
-    }
-    lds_sync();
-    uint32_t pr[S], hp[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        pr[s] = primes[s].p;
-        hp[s] = KT->halfP[s];
-    }
-    const uint32_t CL = 2 * L;
-    const long item = b / CL;
-    const int cl = (int)(b - (uint32_t)item * CL);
-    const int l = cl % L;
-    const u64 q = qprimes[l].q;
-    const uint32_t dq = (uint32_t)((1ull << 60) - q);
-    const u64 negP = KT->negP[l];
-    const u64* rs = R + item * r_stride + (long)cl * N;
-    u64* dst = R + item * r_stride + (long)cl * N;
-#pragma unroll
-    for (int m = 0; m < (N + TT - 1) / TT; ++m) {
-        const int j = tid + m * TT;
-        if (j < N) {
-            uint32_t vj[S];
-#pragma unroll
-            for (int s = 0; s < S; ++s) vj[s] = lds[s * N + j];
-            dst[j] = ks32_lift_one<S>(vj, rs[j], pr, hp, KT, q, dq, negP);
-        }
-    }
-}
-
 // dBFV: the gadget digits of the products of one output limb k summed before their transforms.
 // Every step after the digits (NTT mod p_s, MAC with the key, lift) is linear in them, so the sum
 // of the products' key switches is the key switch of the summed digits (an integer identity; the
@@ -364,21 +304,6 @@ template <int LOGN, bool LAZY>
 static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
                             const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
     const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
-    // side-by-side transforms (ks32_crt_par_kernel) where S n/16 threads fit one block;
-    // EXACTO_KS_CRT_PAR=0 keeps the serial form (A/B)
-    static const bool par = [] { const char* e = std::getenv("EXACTO_KS_CRT_PAR"); return !(e && e[0] == '0'); }();
-    if constexpr (LOGN <= 12) {
-        if (par && S == 3) {
-            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 3, LAZY>), grid, dim3(3 * block.x), 0, st, U, R, r_stride, L,
-                               KT, primes, qprimes);
-            return;
-        }
-        if (par && S == 2) {
-            hipLaunchKernelGGL((ks32_crt_par_kernel<LOGN, 2, LAZY>), grid, dim3(2 * block.x), 0, st, U, R, r_stride, L,
-                               KT, primes, qprimes);
-            return;
-        }
-    }
     if (S == 2)
         hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else if (S == 3)
