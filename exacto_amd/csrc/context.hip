@@ -225,7 +225,10 @@ struct exacto_ctx {
     u64* d_rlk_s = nullptr;  // Shoup companions of the key (limb-wise relinearisation MAC)
     size_t rlk_keys = 0, rlk_cap = 0, rlk_s_cap = 0;
     bool rlk_s_valid = false;
-    bool ntt_asm = true;    // EXACTO_NTT_ASM=0: compiler-scheduled forward NTT everywhere (A/B)
+    // EXACTO_NTT_ASM=0: no special-prime (2^60 - d) asm rounds; those batches then take the generated
+    // generic-prime asm rounds where their size has them (n = 1024 / 4096 / 8192, lazy primes), and the
+    // compiler-scheduled C++ rounds only with EXACTO_NTT_GEN=0 as well (A/B switches)
+    bool ntt_asm = true;
     bool ntt_asm_inv = true;  // EXACTO_NTT_ASM_INV=0: compiler-scheduled inverse NTT (A/B)
     // relinearisation MAC in an auxiliary basis of S 31-bit primes (ks32.hip; EXACTO_KS32=0: the
     // limb-wise 60-bit digit NTTs + relin_mac)
@@ -242,6 +245,9 @@ struct exacto_ctx {
     // S32 / d_p32 / d_tw32 / d_kst / ks32_sum_max / ks32_mac_form describe the active one.
     Ks32Basis kn, kz;
     bool ks32_lazy_active = false;
+    // profiling only (run_inv_tensor's algorithmic bytes): a dBFV pass with shared extensions, d and
+    // its products per item (0: plain BFV products)
+    int tensor_share_d = 0, tensor_share_npairs = 0;
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
@@ -1158,10 +1164,21 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
         near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
     }
     // algorithmic bytes per (item, prime): the four operands a0, a1, b0, b1 in and the three
-    // components out (7 polys); psum's auxiliary primes only c2 = a1 b1 (2 in, 1 out)
+    // components out (7 polys); psum's auxiliary primes only c2 = a1 b1 (2 in, 1 out).  dBFV with
+    // shared extensions (tensor_share_d > 0): the d^2 products of an item read only its 2d distinct
+    // ciphertexts, so the inputs count once per ciphertext (the chunk's ceil(cnt / npairs) items),
+    // not once per product (which overcounted: u64_dbfv's measured traffic was 0.95 of it)
     const double pb = 8.0 * c->n;
-    const double per_item = p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP;
-    ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), per_item * cnt);
+    double bytes;
+    if (c->tensor_share_d > 0 && c->tensor_share_npairs > 0) {
+        const double items = (double)((cnt + c->tensor_share_npairs - 1) / c->tensor_share_npairs);
+        const double cts = items * 2.0 * c->tensor_share_d;
+        bytes = pb * (c->L * (2.0 * cts + 3.0 * cnt) +
+                      c->K * (p2only ? cts + (double)cnt : 2.0 * cts + 3.0 * cnt));
+    } else {
+        bytes = cnt * (p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP);
+    }
+    ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), bytes);
     launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
                       qbits);
     CHECK_LAUNCH();
@@ -2135,7 +2152,12 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         c->psum.out = cf;
     }
     bool coef = false;
+    if (op.ea) {
+        c->tensor_share_d = (int)d;
+        c->tensor_share_npairs = npairs;
+    }
     const int rc = run_mul(c, op, P, c->prod, Ln2, true, &coef);
+    c->tensor_share_d = c->tensor_share_npairs = 0;
     c->ks_defer = nullptr;
     const bool in8 = c->ks_defer8;
     c->ks_defer8 = false;

@@ -148,3 +148,31 @@ def test_errors(gpu_available):
     assert e.value.variant == "InvalidParam"
     with pytest.raises(ValueError):
         ctx.gen_secret_key([1, 2, 3])
+
+
+def test_resident_relin_key_under_boot_debug(gpu_available):
+    """exacto_gen_relin_key with rlk = NULL (straight into the resident key) under EXACTO_DEBUG_BOOT=1:
+    the host-call debug print once dereferenced the NULL host output (fixed in 355108a).  The switch
+    is read once per process, so the call runs in a child process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (
+        "import sys; sys.path[:0] = [%r, %r]\n"
+        "import torch; torch.cuda.init()\n"
+        "import numpy as np\n"
+        "from oracle import params as P\n"
+        "from exacto_amd._ffi import HipContext\n"
+        "prm = P.compact_bfv(); ctx = HipContext.from_params(prm)\n"
+        "K = %r\n"
+        "sk = ctx.gen_secret_key(K, stream=31)\n"
+        "ctx.gen_relin_key(sk, K, stream=32, resident=True)\n"
+        "pa = np.zeros((1, 1024), dtype=np.uint64); pa[0, 0] = 6\n"
+        "ca = ctx.encrypt_sk(pa, sk, K, stream=33)\n"
+        "d = ctx.bfv_decrypt(ctx.bfv_mul_and_relin(ca, ca), sk)\n"
+        "assert int(d[0, 0]) == 36, d[0, :4]\n"
+        "print('ok')\n" % (os.path.dirname(here), here, KEY))
+    env = dict(os.environ, EXACTO_DEBUG_BOOT="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

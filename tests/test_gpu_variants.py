@@ -41,7 +41,6 @@ VARIANTS = {
     "ks32_off": ({"EXACTO_KS32": "0"}, ["cfg3", "cfg4", "cfg5"]),
     "ks32_wide_off": ({"EXACTO_KS32_WIDE": "0"}, ["cfg4"]),
     "ks32_lazy_off": ({"EXACTO_KS32_LAZY": "0"}, ["cfg3", "cfg4", "cfg5"]),
-    "ks_crt_serial": ({"EXACTO_KS_CRT_PAR": "0"}, ["cfg3"]),
     "ks32_wide_primary": ({"EXACTO_KS32_WIDE": "2"}, ["cfg3", "cfg4"]),
     "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
     "dot30_off": ({"EXACTO_DOT30": "0"}, ["cfg3", "cfg5"]),
