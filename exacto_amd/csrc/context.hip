@@ -245,8 +245,8 @@ struct exacto_ctx {
     // S32 / d_p32 / d_tw32 / d_kst / ks32_sum_max / ks32_mac_form describe the active one.
     Ks32Basis kn, kz;
     bool ks32_lazy_active = false;
-    // profiling only (run_inv_tensor's algorithmic bytes): a dBFV pass with shared extensions, d and
-    // its products per item (0: plain BFV products)
+    // a dBFV pass with shared extensions: d and its products per item (0: plain BFV products), for
+    // run_inv_tensor's algorithmic bytes and the tensor kernels' prime-major block order
     int tensor_share_d = 0, tensor_share_npairs = 0;
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
@@ -1180,7 +1180,7 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
     }
     ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), bytes);
     launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
-                      qbits);
+                      qbits, c->tensor_share_npairs);
     CHECK_LAUNCH();
     return 0;
 }

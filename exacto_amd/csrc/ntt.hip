@@ -858,6 +858,46 @@ __device__ __forceinline__ void tensor_unit(int rem, int L, int p2only, int& t, 
     }
 }
 
+// Block -> (product, unit rem in tensor_unit's order).  share_np = 0: product-major (the units of
+// one product together; xcd_group_remap keeps each (product, prime)'s three components, or with
+// p2only a whole product, on one XCD).  share_np > 0 (dBFV with shared extensions; the launch holds
+// whole items of share_np products that read the same 2d ciphertexts): prime-major within an item,
+// so the products of one (item, prime) run back to back on one XCD and read the item's operands in
+// that prime (2d ciphertexts x 2 components, 1 MiB at n = 4096 / 2 MiB at n = 8192) once from HBM,
+// the repeats from its L2.  Region 1: the primes with three components, order (item, prime,
+// component, product), XCD groups of 3 share_np blocks = one (item, prime); region 2 (p2only): the
+// auxiliary primes' c2, order (item, prime, product), groups of share_np.
+__device__ __forceinline__ void tensor_block(long b, long total, int per, int L, int K, int p2only, int np,
+                                             int remap, long& prod, int& rem) {
+    if (np <= 0) {
+        const long p = remap ? xcd_group_remap(b, total, p2only ? per : 3) : b;
+        prod = p / per;
+        rem = (int)(p - prod * per);
+        return;
+    }
+    const long items = total / ((long)per * np);
+    const int LQ = p2only ? L : L + K;
+    const long nQ = items * LQ * 3 * np;
+    if (b < nQ) {
+        const long G = 3L * np;
+        const long p = remap ? xcd_group_remap(b, nQ, (int)G) : b;
+        const long g = p / G;
+        const int w = (int)(p - g * G);
+        const long ib = g / LQ;
+        const int t = (int)(g - ib * LQ), c = w / np, pi = w - c * np;
+        prod = ib * np + pi;
+        rem = 3 * t + c;
+    } else {
+        const long bb = b - nQ;
+        const long p = remap ? xcd_group_remap(bb, total - nQ, np) : bb;
+        const long g = p / np;
+        const int pi = (int)(p - g * np);
+        const long ib = g / K;
+        prod = ib * np + pi;
+        rem = 3 * L + (int)(g - ib * K);
+    }
+}
+
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic operands
 // instead of the loads, stores skipped at run time), 2 = no transform (the loads, the pointwise
 // products and the stores), 3 = the product kernel with its first generation staggered.  (Round 4
@@ -869,7 +909,7 @@ template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                      const PrimeConst* __restrict__ primes, int remap, int p2only = 0) {
+                      const PrimeConst* __restrict__ primes, int remap, int p2only = 0, int share_np = 0) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     constexpr int LAST_LO = LOGN - 4;
@@ -885,9 +925,9 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
     const int per = p2only ? 3 * L + K : 3 * NP;
     // groups of 3 keep each (item, prime)'s components together only while every item's blocks are a
     // multiple of 3; p2only's 3L + K is not (cfg5: 17), so there a whole item is one group
-    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
-    const long item = p / per;
-    const int rem = (int)(p - item * per);
+    long item;
+    int rem;
+    tensor_block(blockIdx.x, gridDim.x, per, L, K, p2only, share_np, remap, item, rem);
     int t, c;
     tensor_unit(rem, L, p2only, t, c);
     const PrimeConst& P = primes[t];
@@ -993,7 +1033,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
-                          const PrimeConst* __restrict__ primes, int remap, int p2only) {
+                          const PrimeConst* __restrict__ primes, int remap, int p2only, int share_np) {
     static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
     constexpr int N = 1 << LOGN;
     constexpr int LAST_LO = LOGN - 4;
@@ -1002,9 +1042,9 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
     const int NP = L + K;
     const int per = p2only ? 3 * L + K : 3 * NP;
     // p2only: a whole item per group (see ntt_inv_tensor_kernel)
-    const long p = remap ? xcd_group_remap(blockIdx.x, gridDim.x, p2only ? per : 3) : (long)blockIdx.x;
-    const long item = p / per;
-    const int rem = (int)(p - item * per);
+    long item;
+    int rem;
+    tensor_block(blockIdx.x, gridDim.x, per, L, K, p2only, share_np, remap, item, rem);
     int t, c;
     tensor_unit(rem, L, p2only, t, c);
     const PrimeConst& P = primes[t];
@@ -1302,7 +1342,8 @@ static bool gen_small(int qbits) {
 
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
-                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64) {
+                      const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64,
+                      int np = 0) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
@@ -1310,13 +1351,13 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
         if (asm_inv && tensor_pin_at(LOGN)) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L, K,
-                               primes, remap, p2only);
+                               primes, remap, p2only, np);
             return;
         }
         if (asm_inv) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
-                               T, L, K, primes, remap, p2only);
+                               T, L, K, primes, remap, p2only, np);
             return;
         }
     }
@@ -1324,10 +1365,10 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
         if (lazy && !p2only && ntt_gen_on()) {   // every prime below 2^60: the generated generic-prime rounds
             if (gen_small<LOGN>(qbits))
                 hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true, gen_qb<LOGN>()>), dim3(blocks),
-                                   dim3(threads), 0, s, op, extP, T, L, K, primes, remap);
+                                   dim3(threads), 0, s, op, extP, T, L, K, primes, remap, 0, np);
             else
                 hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0,
-                                   s, op, extP, T, L, K, primes, remap);
+                                   s, op, extP, T, L, K, primes, remap, 0, np);
             return;
         }
     }
@@ -1340,12 +1381,17 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits, int share_np) {
+    // prime-major block order needs whole dBFV items in the launch (tensor_block)
+    // (measured: cfg5, 36 products per item, tensor 270 -> 261 us; cfg4's 3 products per item and
+    // u64_dbfv within noise: applied from 8 products per item)
+    static const int pm = env_switch("EXACTO_TENSOR_PRIME_MAJOR", 1);
+    if (!pm || share_np < 8 || items % share_np != 0) share_np = 0;
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
-        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
-        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1);
+        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np);
+        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np);
         return;
     }
     switch (logn) {
@@ -1355,10 +1401,10 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 7: launch_it<7>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 8: launch_it<8>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s, false, 0, qbits); break;
+        case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s, false, 0, qbits, share_np); break;
         case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
-        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np); break;
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }

@@ -8,7 +8,8 @@ the rest of the suite (test_gpu_golden.py digests, test_gpu_published.py, test_g
 test_gpu_psum.py); bit-exact, integer work.
 
 Not listed (no effect on results): EXACTO_SCRATCH_POOL / EXACTO_DEBUG_SCRATCH / EXACTO_DEBUG_FILL /
-EXACTO_LEAK_CTX (allocation diagnostics, tools/diag.sh), EXACTO_DEBUG_BOOT (bootstrap snapshots), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
+EXACTO_LEAK_CTX (allocation diagnostics, tools/diag.sh), EXACTO_DEBUG_BOOT / EXACTO_DEBUG_WATCH /
+EXACTO_DEBUG_ALLOC (bootstrap snapshots, write watch, allocation log), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
 EXACTO_PROF_RAW (profiling arithmetic), EXACTO_RCCL_LIB (library path).
 """
 
@@ -44,7 +45,8 @@ VARIANTS = {
     "ks32_wide_primary": ({"EXACTO_KS32_WIDE": "2"}, ["cfg3", "cfg4"]),
     "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
     "dot30_off": ({"EXACTO_DOT30": "0"}, ["cfg3", "cfg5"]),
-    "xcd_remap_off": ({"EXACTO_XCD_REMAP": "0"}, ["cfg3"]),
+    "xcd_remap_off": ({"EXACTO_XCD_REMAP": "0"}, ["cfg3", "cfg5"]),
+    "tensor_product_major": ({"EXACTO_TENSOR_PRIME_MAJOR": "0"}, ["cfg5", "hps"]),
     "mac_lds_off": ({"EXACTO_MAC_LDS": "0"}, ["hps"]),
     # HPS: the literal i128 scale against the division-free one, per-product relinearisation against
     # dbfv_mul's per-limb digit sums
@@ -81,7 +83,8 @@ def test_every_library_switch_is_covered():
             with open(os.path.join(src, f)) as fh:
                 found |= set(re.findall(r'(?:getenv|env_switch)\("(EXACTO_[A-Z0-9_]+)"', fh.read()))
     neutral = {"EXACTO_SCRATCH_POOL", "EXACTO_DEBUG_SCRATCH", "EXACTO_DEBUG_FILL", "EXACTO_DBFV_GROUP_MB",
-               "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB", "EXACTO_DEBUG_BOOT", "EXACTO_LEAK_CTX"}
+               "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB", "EXACTO_DEBUG_BOOT", "EXACTO_LEAK_CTX",
+               "EXACTO_DEBUG_ALLOC", "EXACTO_DEBUG_WATCH"}
     assert found - neutral == set(SWITCHES), found ^ (set(SWITCHES) | neutral)
 
 
