@@ -7,6 +7,12 @@
 
 namespace exacto {
 
+// Twiddles through the global address space: the generic pointers of Prime32 gave flat loads,
+// which count against lgkmcnt, so every LDS barrier of a round also waited for the next twiddles
+// (the same fix as ntt.hip's TwTab)
+typedef const uint2 __attribute__((address_space(1)))* Tw32;
+__device__ __forceinline__ Tw32 tw32(const uint2* p) { return (Tw32)p; }
+
 // x * w mod p in [0, 2p) for any x < 2^32 (ws = floor(w 2^32 / p), p < 2^31)
 __device__ __forceinline__ uint32_t shoup32(uint32_t x, uint32_t w, uint32_t ws, uint32_t p) {
     return x * w - __umulhi(x, ws) * p;
@@ -81,7 +87,7 @@ enum { F32_WIDE = 0, F32_NARROW = 1, F32_LAZY = 2 };
 // CANON: the round's inputs are canonical (round 0: the caller's values are in [0, p)), so the first
 // stage's X needs no reduction (8 butterflies x 4 VALU per thread less in the digit transforms).
 template <int LOGN, int LO, int BHI, int FORM, bool CANON = false>
-__device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const uint2* __restrict__ tw, uint32_t p) {
+__device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, Tw32 tw, uint32_t p) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
     const uint32_t p2 = 2 * p, np = 0u - p;
@@ -91,7 +97,7 @@ __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const ui
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
         for (int g = 0; g < (8 >> lb); ++g) {
-            const uint2 t = tw[base + g];
+            const uint2 t = make_uint2(tw[base + g].x, tw[base + g].y);
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m, k1 = k0 + half;
@@ -117,7 +123,7 @@ __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, const ui
 }
 
 template <int LOGN, int R, int FORM>
-__device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const uint2* tw, uint32_t p) {
+__device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, Tw32 tw, uint32_t p) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
     if constexpr (R > 0) {
@@ -139,7 +145,7 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     const uint32_t p = P.p, half = p >> 1;
-    fwd32_rounds<LOGN, 0, FORM>(x, lds, tid, P.tw_fwd, p);
+    fwd32_rounds<LOGN, 0, FORM>(x, lds, tid, tw32(P.tw_fwd), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k)   // lazy [0, 4p) / narrow [0, 3p] / wide [0, 2p) -> [0, p)
         x[k] = FORM == F32_WIDE ? red32(x[k], p) : red32(min(x[k], x[k] - 2 * p), p);
@@ -163,6 +169,7 @@ template <int LOGN, int LO, int BLO, int BHI, bool LAZY>
 __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Prime32& P) {
     constexpr int N = 1 << LOGN;
     const uint32_t p = P.p, p2 = 2 * p;
+    const Tw32 twi = tw32(P.tw_inv);
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
 #pragma unroll
     for (int b = BLO; b <= BHI; ++b) {
@@ -171,7 +178,7 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
 #pragma unroll
         for (int g = 0; g < (8 >> lb); ++g) {
             uint2 t = make_uint2(0, 0);
-            if (b != LOGN - 1) t = P.tw_inv[base + g];
+            if (b != LOGN - 1) t = make_uint2(twi[base + g].x, twi[base + g].y);
 #pragma unroll
             for (int m = 0; m < half; ++m) {
                 const int k0 = g * 2 * half + m, k1 = k0 + half;

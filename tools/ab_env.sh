@@ -10,7 +10,7 @@ cd $R
 for c in ${@:-cfg3}; do
   for rep in 1 2; do
     for v in $VARS; do
-      tag=$(echo "$v" | tr ',=' '__')
+      tag=$(echo "$v" | tr ',=/' '___')
       envs=(); [ "$v" != "-" ] && IFS=',' read -ra envs <<< "$v"
       env "${envs[@]}" timeout -k 10 200 python3 bench.py --config $c --no-cpu-baseline --min-time 1.5 \
         > $O/${tag}_${c}_$rep.json 2>> $O/err.log || exit 1
