@@ -39,22 +39,6 @@ __device__ __forceinline__ void garner_q_fast(u64 (&v)[EXACTO_MAX_L], const u64 
     }
 }
 
-// p t mod q for a special prime q = 2^60 - d (d < 2^24), a canonical t and a plaintext modulus p below
-// 2^32 (every BASELINE exact-path config): the 92-bit product folded once through 2^60 == d, below
-// 2^60 + 2^56 < 2q (garner_q_fast's input range); 3 multiplies instead of a Shoup product's 6
-__device__ __forceinline__ u64 mul_small_sp(u64 t, uint32_t p, u64 q) {
-    const uint32_t d = (uint32_t)((1ull << 60) - q);
-    const u64 lo = (u64)(uint32_t)t * p;
-    const u64 hi = (u64)(uint32_t)(t >> 32) * p + (lo >> 32);      // t p = hi 2^32 + lo.lo
-    const u64 l60 = ((hi & 0x0FFFFFFFull) << 32) | (uint32_t)lo;
-    return l60 + (hi >> 28) * d;
-}
-
-// u = p T mod q_i (< 2q_i) for the SP kernels: the small-p product when p < 2^32 (uniform branch)
-__device__ __forceinline__ u64 scale_p_sp(u64 t, const CrtTables* __restrict__ C, int i, u64 q) {
-    return C->plain < (1ull << 32) ? mul_small_sp(t, (uint32_t)C->plain, q) : shoup_mul(t, C->pmod_w[i], C->pmod_ws[i], q);
-}
-
 // ---- 30-bit-limb dot products (SP: every prime 2^60 - d, d < 2^24) ----
 // sum_k x_k c_k with x_k, c_k < 2^60, kept exactly as a0 + a1 2^30 + a2 2^60: each operand is
 // split into 30-bit limbs, so every limb product is below 2^60 and one v_mad_u64_u32 adds it to

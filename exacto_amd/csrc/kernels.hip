@@ -547,7 +547,7 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
     const u64* Tin = T + (item * 3 + comp) * NP * n + j;
     u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
-    for (int i = 0; i < L; ++i) u[i] = scale_p_sp(Tin[(long)i * n], C, i, primes[i].q);
+    for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
     garner_q_fast<LT>(v, u, L, C, primes);
     const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
     uint32_t v0[L], v1[L];
@@ -641,7 +641,7 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
         const u64* Tin = T + ((ib * npairs + terms[t].pair) * 3 + c) * (long)NP * n + j;
         u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
-        for (int i = 0; i < L; ++i) u[i] = scale_p_sp(Tin[(long)i * n], C, i, primes[i].q);
+        for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
         garner_q_fast<LT>(v, u, L, C, primes);
         const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
         uint32_t v0[L], v1[L];

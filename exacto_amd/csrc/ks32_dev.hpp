@@ -228,7 +228,9 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
 // evaluation x = a_0 + p_0 (a_1 + p_1 (a_2 + ...)) whose every step folds the 92-bit product through
 // 2^60 == d (5 instructions); the centring (x > floor(P/2)) is decided on the mixed-radix digits and
 // adds q - (P mod q).
-template <int S>
+// LAZY (every p_s below 2^30): a_kk < p_kk < 2 p_s enters t + 2 p_s - a_kk < 4 p_s < 2^32 unreduced
+// (the Shoup product takes any 32-bit input): one min-subtraction less per Garner term.
+template <int S, bool LAZY = false>
 __device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, const uint32_t (&pr)[S],
                                              const uint32_t (&hp)[S], const Ks32Tables* __restrict__ KT, u64 q,
                                              uint32_t dq, u64 negP) {
@@ -239,7 +241,8 @@ __device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, cons
         uint32_t t = v[s];
 #pragma unroll
         for (int kk = 0; kk < s; ++kk) {   // a_kk < p_kk < 2 p_s
-            t = t + ps - red32(a[kk], ps);                       // (0, 2 p_s)
+            t = LAZY ? t + 2 * ps - a[kk]                        // (0, 4 p_s)
+                     : t + ps - red32(a[kk], ps);                // (0, 2 p_s)
             t = red32(shoup32(t, KT->ginv[s][kk], KT->ginv_s[s][kk], ps), ps);
         }
         a[s] = t;
@@ -304,7 +307,7 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
         uint32_t vk[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) vk[s] = v[s][k];
-        x[k] = ks32_lift_one<S>(vk, src[k * T + tid], pr, hp, KT, q, dq, negP);
+        x[k] = ks32_lift_one<S, LAZY>(vk, src[k * T + tid], pr, hp, KT, q, dq, negP);
     }
 }
 
