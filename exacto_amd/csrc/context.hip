@@ -248,6 +248,10 @@ struct exacto_ctx {
     // a dBFV pass with shared extensions: d and its products per item (0: plain BFV products), for
     // run_inv_tensor's algorithmic bytes and the tensor kernels' prime-major block order
     int tensor_share_d = 0, tensor_share_npairs = 0;
+    // dBFV chain: the step that formed the output limbs in the coefficient domain also lifted them to
+    // the auxiliary primes into ext_a and transformed both in one launch; the next step's extension of
+    // its left operand is then already in ext_a (measured A/B: DESIGN.md §6.4)
+    bool ext_a_ready = false;
     int16_t* ks_defer = nullptr;  // run_mul: int16 digits of product p to ks_defer + p G n, no key switch
     bool ks_defer8 = false;       // ... int8 digits instead (base <= 2^8; EXACTO_DIGIT8=0: int16)
     bool digit8_env = true;
@@ -1151,6 +1155,22 @@ static int run_ntt(exacto_ctx* c, const NttBatch& nb, long count, bool inverse) 
     launch_ntt(nb, (int)count, c->logn, inverse, lazy, c->d_primes, c->stream, near60, near60 && c->ntt_asm_inv, qbits);
     CHECK_LAUNCH();
     return 0;
+}
+
+// two forward batches in one launch where both take the pinned rounds (every prime 2^60 - d, n = 4096
+// / 8192), else two launches
+static int run_ntt_fwd2(exacto_ctx* c, const NttBatch& nb1, long count1, const NttBatch& nb2, long count2) {
+    bool near60 = c->ntt_asm && !nb1.src16 && !nb2.src16;
+    for (u64 q : c->primes) near60 &= q < (1ull << 60) && q > (1ull << 60) - (1ull << 32);
+    if (near60 && count1 > 0 && count2 > 0) {
+        ProfScope ps(c, PK_FWD, (u64)(count1 + count2), 16.0 * c->n * (double)(count1 + count2));
+        if (launch_ntt_fwd2(nb1, (int)count1, nb2, (int)count2, c->logn, c->d_primes, c->stream)) {
+            CHECK_LAUNCH();
+            return 0;
+        }
+    }
+    if (int e = run_ntt(c, nb1, count1, false)) return e;
+    return run_ntt(c, nb2, count2, false);
 }
 
 static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only = false) {
@@ -2057,8 +2077,13 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     op.b = b; op.b_off = c->d_off + BP; op.b_stride = 0;
     if (c->share_ext && c->K > 0 && !c->deferred_code) {
         const size_t nct = B * d, bytes = nct * 2 * c->K * poly_bytes(c);
-        if (grow(&c->ext_a, &c->ext_a_cap, bytes)) return EXACTO_ERR_HIP;
-        if (int e = extend_cts(c, a, nct, c->ext_a, c->coef_in)) return e;
+        if (c->ext_a_ready) {   // made by the previous chain step (same ciphertexts, same buffer size)
+            if (c->ext_a_cap < bytes) return fail(EXACTO_ERR_HIP, "internal: pre-extended operand buffer too small");
+        } else {
+            if (grow(&c->ext_a, &c->ext_a_cap, bytes)) return EXACTO_ERR_HIP;
+            if (int e = extend_cts(c, a, nct, c->ext_a, c->coef_in)) return e;
+        }
+        c->ext_a_ready = false;
         if (!b_extended) {
             if (grow(&c->ext_b, &c->ext_b_cap, bytes)) return EXACTO_ERR_HIP;
             if (int e = extend_cts(c, b, nct, c->ext_b)) return e;
@@ -2209,7 +2234,27 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     if (coef) {
         NttBatch ob = contiguous(out, (long)B * dout, 2L * c->L, 0, c->L, c->n);
         ob.src = cf;   // (== out unless a chain keeps the coefficient form)
-        if (int e = run_ntt(c, ob, (long)B * dout * 2 * c->L, false)) return e;
+        // a chain step whose limbs stay in the coefficient domain (cf) for the next step: that step's
+        // extension of its left operand (exact lift of cf to the auxiliary primes, then their forward
+        // transform: extend_cts with coef = cf) is made here, and the two forward batches go in one
+        // launch (cfg5: 512 + 640 polynomials instead of two launches that each fill about one
+        // generation of the 512 resident workgroups)
+        const bool pre = cf != out && op.ea != nullptr && dout == d && !c->deferred_code &&
+                         c->path != EXACTO_PATH_HPS && c->ext_a_cap >= (size_t)B * d * 2 * c->K * poly_bytes(c);
+        if (pre) {
+            const long cts = (long)B * d;
+            {
+                ProfScope pl(c, PK_LIFT, 2ull * cts, 8.0 * (c->L + c->K) * c->n * 2.0 * cts);
+                launch_exact_lift(cf, c->ext_a, 2 * cts, c->n, c->d_crt, c->d_primes, c->L, c->K, crt_mode(c),
+                                  c->stream);
+                CHECK_LAUNCH();
+            }
+            const NttBatch eb = contiguous(c->ext_a, cts, 2L * c->K, c->L, c->K, c->n);
+            if (int e = run_ntt_fwd2(c, ob, cts * 2 * c->L, eb, cts * 2 * c->K)) return e;
+            c->ext_a_ready = true;
+        } else {
+            if (int e = run_ntt(c, ob, (long)B * dout * 2 * c->L, false)) return e;
+        }
         c->coef_written = cf != out;
     }
     if (hps_sum) {
@@ -2414,6 +2459,7 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     // the next step lifts it directly: one batched inverse NTT of its input less per step
     // (dbfv_mul_group allocates chain_coef, two halves of `bytes`, only when the step runs psum)
     const bool carry = depth > 1 && c->share_ext && c->K > 0;
+    c->ext_a_ready = false;
     const uint64_t* src = x;
     const u64* src_coef = nullptr;
     int rc = 0;
@@ -2433,6 +2479,7 @@ extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base,
     c->coef_out = nullptr;
     c->coef_slot = -1;
     c->coef_written = false;
+    c->ext_a_ready = false;
     return rc;
 }
 

@@ -76,6 +76,10 @@ struct CrtTables {
 // asm_fwd / asm_inv: every prime of the batch is in (2^60 - 2^32, 2^60): the forward / inverse
 // transforms at n = 4096 / 8192 run the pinned-home kernels over the generated rounds (ntt_asm.inc)
 // qbits: bit length of the batch's largest prime (the generic kernels' smaller-prime forms)
+// one forward launch over two batches (n = 4096 / 8192, every prime 2^60 - d of the pinned rounds);
+// false: not applicable, nothing launched
+bool launch_ntt_fwd2(const NttBatch& nb1, int count1, const NttBatch& nb2, int count2, int logn,
+                     const PrimeConst* primes, hipStream_t s);
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,
                 hipStream_t s, bool asm_fwd = false, bool asm_inv = false, int qbits = 64);
 

@@ -706,15 +706,21 @@ ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // canonical inputs, no global loads, stores skipped at run time), 2 = memory only (loads, the
 // same LDS exchanges and stores, no butterflies and no twiddle loads), 3 = the product kernel with
 // its first generation staggered (probe_stagger).
+// nb2 / split: blocks from `split` on transform a second batch (nb2, block - split): one launch for
+// two batches of the same transform size (a dBFV chain step's output limbs and the next step's
+// extension)
 template <int LOGN, int PROBE = 0>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
-ntt_fwd_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
+ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch nb2 = NttBatch{},
+                   int split = 0x7fffffff) {
     static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
-    const int p = blockIdx.x;
+    const bool second = (int)blockIdx.x >= split;
+    const NttBatch& nb = second ? nb2 : nb1;
+    const int p = second ? (int)blockIdx.x - split : (int)blockIdx.x;
     const int item = p / nb.ppi, sub = p - item * nb.ppi;
     const PrimeConst& P = primes[nb.prime_base + sub % nb.period];
     const u64 q = P.q;
@@ -1384,9 +1390,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
                        const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits, int share_np) {
     // prime-major block order needs whole dBFV items in the launch (tensor_block)
     // (measured: cfg5, 36 products per item, tensor 270 -> 261 us; cfg4's 3 products per item and
-    // u64_dbfv within noise: applied from 8 products per item)
-    static const int pm = env_switch("EXACTO_TENSOR_PRIME_MAJOR", 1);
-    if (!pm || share_np < 8 || items % share_np != 0) share_np = 0;
+    // u64_dbfv within noise: applied from 8 products per item; DESIGN.md §6.4)
+    if (share_np < 8 || items % share_np != 0) share_np = 0;
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
@@ -1408,6 +1413,15 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }
+}
+
+bool launch_ntt_fwd2(const NttBatch& nb1, int count1, const NttBatch& nb2, int count2, int logn,
+                     const PrimeConst* primes, hipStream_t s) {
+    if (count1 <= 0 || count2 <= 0 || (logn != 12 && logn != 13)) return false;
+    const dim3 grid((unsigned)(count1 + count2));
+    if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), grid, dim3(256), 0, s, nb1, primes, nb2, count1);
+    else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), grid, dim3(512), 0, s, nb1, primes, nb2, count1);
+    return true;
 }
 
 void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy, const PrimeConst* primes,

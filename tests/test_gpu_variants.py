@@ -46,7 +46,6 @@ VARIANTS = {
     "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
     "dot30_off": ({"EXACTO_DOT30": "0"}, ["cfg3", "cfg5"]),
     "xcd_remap_off": ({"EXACTO_XCD_REMAP": "0"}, ["cfg3", "cfg5"]),
-    "tensor_product_major": ({"EXACTO_TENSOR_PRIME_MAJOR": "0"}, ["cfg5", "hps"]),
     "mac_lds_off": ({"EXACTO_MAC_LDS": "0"}, ["hps"]),
     # HPS: the literal i128 scale against the division-free one, per-product relinearisation against
     # dbfv_mul's per-limb digit sums
