@@ -43,12 +43,15 @@ ks32_digit_ntt_kernel(const DT* __restrict__ D16, uint32_t* __restrict__ DS, int
     const Prime32& P = primes[s];
     const DT* src = D16 + ig * N;
     uint32_t x[16];
+    // int16 digits under the lazy form: the transform's first stage takes the signed values as they
+    // are (fwd32_round SIN); otherwise they become canonical residues first
+    constexpr bool SIN = FORM == F32_LAZY && sizeof(DT) == 2;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int d = src[tid + k * T];
-        x[k] = d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
+        x[k] = SIN ? (uint32_t)d : d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
     }
-    fwd32_store<LOGN, FORM>(x, lds, tid, P, DS + (long)b * N);
+    fwd32_store<LOGN, FORM, SIN>(x, lds, tid, P, DS + (long)b * N);
 }
 
 // key rows [rows][n] canonical mod q_{row's limb} (u64) -> RS [rows][S][n]: balanced, mod p_s, NTT

@@ -86,13 +86,38 @@ enum { F32_WIDE = 0, F32_NARROW = 1, F32_LAZY = 2 };
 // Wide primes (up to 2^31): values < 2p between stages, X and T reduced to [0, p) separately.
 // CANON: the round's inputs are canonical (round 0: the caller's values are in [0, p)), so the first
 // stage's X needs no reduction (8 butterflies x 4 VALU per thread less in the digit transforms).
-template <int LOGN, int LO, int BHI, int FORM, bool CANON = false>
+// SIN (lazy primes, round 0 only): the inputs are int16 values x in [-2^15, 2^15) as int32 bits, not
+// residues.  The first stage (one twiddle w, b = LOGN - 1) takes them as they are: Y + 2^15 >= 0 goes
+// through the Shoup chain (T' = (Y + 2^15) w mod p, in [0, 2p)), and the constants K1 == -c, K2 == c
+// with c = 2^15 w mod p, K1 in [2^15, p + 2^15), K2 in [2p + 2^15, 3p + 2^15), bring
+//   X + T' + K1 == X + Y w  and  X - T' + K2 == X - Y w  into [0, 4p)
+// (4 VALU per butterfly less than converting both inputs to canonical residues first).
+template <int LOGN, int LO, int BHI, int FORM, bool CANON = false, bool SIN = false>
 __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, Tw32 tw, uint32_t p) {
     constexpr int N = 1 << LOGN;
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
     const uint32_t p2 = 2 * p, np = 0u - p;
+    static_assert(!SIN || (FORM == F32_LAZY && CANON && BHI == LOGN - 1), "signed inputs: lazy round 0 only");
+    if constexpr (SIN) {
+        const uint2 t = make_uint2(tw[1].x, tw[1].y);
+        const uint32_t c = red32(shoup32(1u << 15, t.x, t.y, p), p);
+        const uint32_t k1 = (p - c) < (1u << 15) ? 2 * p - c : p - c;
+        const uint32_t k2 = c < (1u << 15) ? c + 3 * p : c + p2;
+        const uint32_t kd = k2 - k1;
 #pragma unroll
-    for (int b = BHI; b >= LO; --b) {
+        for (int m = 0; m < 8; ++m) {
+            const uint32_t XK = x[m] + k1, Y = x[m + 8] + (1u << 15);
+            const uint32_t qh = __umulhi(Y, t.y);
+            const uint32_t o0 = (uint32_t)mad64(qh, np, mad64(Y, t.x, lo_only(XK)));
+            // 2 XK + kd in one instruction (as C++, hipcc reassociates it into three)
+            uint32_t x2;
+            asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(x2) : "v"(XK), "v"(kd));
+            x[m] = o0;                       // X + T' + K1
+            x[m + 8] = x2 - o0;              // X - T' + K2
+        }
+    }
+#pragma unroll
+    for (int b = SIN ? BHI - 1 : BHI; b >= LO; --b) {
         const int lb = b - LO, half = 1 << lb;
         const int base = (N >> (b + 1)) + (thigh << (LO + 3 - b));
 #pragma unroll
@@ -122,7 +147,7 @@ __device__ __forceinline__ void fwd32_round(uint32_t (&x)[16], int tid, Tw32 tw,
     }
 }
 
-template <int LOGN, int R, int FORM>
+template <int LOGN, int R, int FORM, bool SIN = false>
 __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, Tw32 tw, uint32_t p) {
     constexpr int LO = (LOGN - 4 * (R + 1)) > 0 ? (LOGN - 4 * (R + 1)) : 0;
     constexpr int BHI = LOGN - 1 - 4 * R;
@@ -133,30 +158,28 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
         lds_sync();
         lds32_load<LO>(lds, x, tid);
     }
-    fwd32_round<LOGN, LO, BHI, FORM, R == 0>(x, tid, tw, p);   // round 0: canonical inputs (fwd32_store)
+    // round 0: canonical inputs (fwd32_store), or int16 values (SIN)
+    fwd32_round<LOGN, LO, BHI, FORM, R == 0, SIN && R == 0>(x, tid, tw, p);
     if constexpr (LO > 0) fwd32_rounds<LOGN, R + 1, FORM>(x, lds, tid, tw, p);
 }
 
-// x (element tid + k T, canonical: round 0 relies on it) -> NTT, stored coalesced at dst (element tid + k T of the
-// bit-reversed-order evaluation array), as balanced residues in (-p/2, p/2] (int32 bits): the
-// only consumer, ks32_mac_kernel, multiplies balanced values
-template <int LOGN, int FORM>
+// x (element tid + k T, canonical: round 0 relies on it) -> NTT, stored in ntt.hip's evaluation
+// order (evaluation 16 tid + k at position tid + k T: coalesced, no LDS transpose), as balanced
+// residues in (-p/2, p/2] (int32 bits): the only consumer, ks32_mac_kernel, multiplies balanced
+// values position by position, and ks32_crt_values reads its sums in the same order
+template <int LOGN, int FORM, bool SIN = false>
 __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P,
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     const uint32_t p = P.p, half = p >> 1;
-    fwd32_rounds<LOGN, 0, FORM>(x, lds, tid, tw32(P.tw_fwd), p);
+    fwd32_rounds<LOGN, 0, FORM, SIN>(x, lds, tid, tw32(P.tw_fwd), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k)   // lazy [0, 4p) / narrow [0, 3p] / wide [0, 2p) -> [0, p)
         x[k] = FORM == F32_WIDE ? red32(x[k], p) : red32(min(x[k], x[k] - 2 * p), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = x[k] > half ? x[k] - p : x[k];
-    lds_sync();
-    lds32_store<0>(lds, x, tid);
-    lds_sync();
-    lds32_load<LOGN - 4>(lds, x, tid);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];   // evaluation 16 tid + k (ntt.hip store_evals)
 }
 
 // ---------------------------------------------------------------- inverse (Gentleman-Sande)
@@ -283,12 +306,9 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
     uint32_t v[S][16];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const uint4* src = reinterpret_cast<const uint4*>(U + ((long)b * S + s) * N + 16 * tid);
+        const uint32_t* src = U + ((long)b * S + s) * N + tid;   // evaluation 16 tid + k at tid + k T
 #pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const uint4 w = src[h];
-            v[s][4 * h] = w.x; v[s][4 * h + 1] = w.y; v[s][4 * h + 2] = w.z; v[s][4 * h + 3] = w.w;
-        }
+        for (int k = 0; k < 16; ++k) v[s][k] = src[k * T];
         inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
     }
     uint32_t pr[S], hp[S];

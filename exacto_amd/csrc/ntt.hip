@@ -185,9 +185,25 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTa
 #ifndef EXACTO_NTT_PRELOAD
 #define EXACTO_NTT_PRELOAD 1
 #endif
-#ifndef EXACTO_NTT_TOUT
-#define EXACTO_NTT_TOUT 1  // forward: transpose through LDS so the output stores coalesce
-#endif
+
+// NTT-domain storage order: evaluation k = a(psi^(2 brv(k) + 1)) is stored at
+// position (k mod 16) (n/16) + floor(k / 16).  The forward's last round leaves evaluations
+// 16 tid .. 16 tid + 15 in thread tid and the inverse's first round wants exactly those, so both
+// move them as x[k] <-> position tid + k n/16: every load / store instruction of a wave covers
+// contiguous memory, and the forward needs no LDS transpose before its stores.  (Round 5: with
+// the standard order the inverse-side loads ran at a 128-byte lane stride; the cfg3 tensor kernel
+// 308 -> 265 us.)
+template <int N>
+__device__ __forceinline__ void store_evals(u64* __restrict__ dst, const u64 (&x)[16], int tid) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * (N / 16)] = x[k];
+}
+
+template <int N>
+__device__ __forceinline__ void load_evals(u64 (&x)[16], const u64* __restrict__ src, int tid) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * (N / 16)];
+}
 #ifdef EXACTO_NTT_WAVES
 #define NTT_OCC __attribute__((amdgpu_waves_per_eu(EXACTO_NTT_WAVES)))
 #else
@@ -246,20 +262,7 @@ ntt_fwd_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         v = v >= q2 ? v - q2 : v;
         x[k] = v >= q ? v - q : v;
     }
-    if constexpr (EXACTO_NTT_TOUT) {
-        // element 16*tid+k -> element tid+k*T: every store instruction then writes 512
-        // contiguous bytes per wave instead of touching 64 cache lines
-        lds_barrier();
-        lds_store<0>(lds, x, tid);
-        lds_barrier();
-        lds_load<LOGN - 4>(lds, x, tid);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
-    } else {
-        ulonglong2* d2 = reinterpret_cast<ulonglong2*>(dst + 16 * tid);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d2[k] = make_ulonglong2(x[2 * k], x[2 * k + 1]);
-    }
+    store_evals<N>(dst, x, tid);
 }
 
 // ---------------------------------------------------------------- forward, hand-scheduled rounds
@@ -433,15 +436,7 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
 
     u64 x[16];
-    {   // element 16*tid + k (coalesced loads + an LDS transpose measured slower, round 1)
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const ulonglong2 v = s2[k];
-            x[2 * k] = v.x;
-            x[2 * k + 1] = v.y;
-        }
-    }
+    load_evals<N>(x, src, tid);   // evaluation 16 tid + k
 
     inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
 
@@ -483,20 +478,6 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
 // below 2^64 is larger); the host picks the kernel instance (launch_ntt / launch_inv_tensor: qbits).
 template <int LOGN>
 constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
-
-// The inverse's first round works on elements 16*tid + k (stage bits 0..3 in one thread): each
-// thread loads its 16 consecutive words (8 x 16 B).  (Coalesced 8-B loads transposed through LDS
-// measured neutral for the asm inverse and the tensor kernel, round 3, and were removed.)
-template <int N>
-__device__ __forceinline__ void load_rows16(u64 (&x)[16], const u64* __restrict__ src, int tid) {
-    const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const ulonglong2 v = s2[k];
-        x[2 * k] = v.x;
-        x[2 * k + 1] = v.y;
-    }
-}
 
 // ---------------------------------------------------------------- pinned-home rounds
 
@@ -615,16 +596,11 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
                      (long)sub * N;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     EXACTO_PIN_DECL
-    {
-        const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-        { const ulonglong2 w_ = s2[0]; PIN_SET(0, w_.x) PIN_SET(1, w_.y) }
-        { const ulonglong2 w_ = s2[1]; PIN_SET(2, w_.x) PIN_SET(3, w_.y) }
-        { const ulonglong2 w_ = s2[2]; PIN_SET(4, w_.x) PIN_SET(5, w_.y) }
-        { const ulonglong2 w_ = s2[3]; PIN_SET(6, w_.x) PIN_SET(7, w_.y) }
-        { const ulonglong2 w_ = s2[4]; PIN_SET(8, w_.x) PIN_SET(9, w_.y) }
-        { const ulonglong2 w_ = s2[5]; PIN_SET(10, w_.x) PIN_SET(11, w_.y) }
-        { const ulonglong2 w_ = s2[6]; PIN_SET(12, w_.x) PIN_SET(13, w_.y) }
-        { const ulonglong2 w_ = s2[7]; PIN_SET(14, w_.x) PIN_SET(15, w_.y) }
+    {   // evaluation 16 tid + k from position tid + k T (store_evals' order)
+        constexpr int T = N / 16;
+#define PIN_INP(k) PIN_SET(k, src[tid + (k) * T])
+        PIN_X16(PIN_INP)
+#undef PIN_INP
     }
     PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
 #define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
@@ -653,12 +629,11 @@ __device__ __forceinline__ void probe_stagger(int slots, int sleeps_per_phase) {
 
 // Forward NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not all of the
 // 2^60 - d form (the HPS primes): ntt_fwd_kernel's loads, the generated generic-prime rounds
-// (FwdRoundGenAsm, canonical outputs) and coalesced stores (element tid + k T through LDS).
+// (FwdRoundGenAsm, canonical outputs) and store_evals' output order.
 template <int LOGN, int QB = 60>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
 ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const int p = blockIdx.x;
@@ -670,12 +645,7 @@ ntt_fwd_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64 x[16];
     load_coeffs<N>(x, nb, src, item, sub, P.q, tid);
     fwd_rounds_asm<LOGN, 0, true, QB>(x, lds, tid, tw_table(P.tw_fwd), make_asmk(P.q));
-    lds_barrier();
-    lds_store_x<0>(lds, x, tid);
-    lds_barrier();
-    lds_load_x<LOGN - 4>(lds, x, tid);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];
+    store_evals<N>(dst, x, tid);
 }
 
 // Inverse NTT, n = 1024 / 4096 / 8192, every prime of the batch below 2^60 but not of the 2^60 - d form
@@ -694,14 +664,14 @@ ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
                      (long)sub * N;
     u64* dst = nb.dst + (long)item * nb.dst_item_stride + (long)sub * N;
     u64 x[16];
-    load_rows16<N>(x, src, tid);
+    load_evals<N>(x, src, tid);
     inv_rounds_asm<LOGN, 0, true, QB>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
 }
 
-// Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds, exchanges and
-// coalesced output (element tid + k T), with the u64 or int16-digit input of load_coeffs.
+// Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds and exchanges, output in
+// store_evals' order, with the u64 or int16-digit input of load_coeffs.
 // PROBE (tools/ntt_probe.hip only; the library instantiates 0): 1 = compute only (synthetic
 // canonical inputs, no global loads, stores skipped at run time), 2 = memory only (loads, the
 // same LDS exchanges and stores, no butterflies and no twiddle loads), 3 = the product kernel with
@@ -754,8 +724,7 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
     } else {
         PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q))
     }
-    // canonical, element 16*tid+k -> element tid+k*T through LDS, coalesced stores
-    PIN_EXCHANGE(lds, tid, 0, LOGN - 4)
+    // canonical, evaluation 16 tid + k -> position tid + k T (store_evals' order)
     if constexpr (PROBE == 1) {
         if (nb.dst_item_stride != -7) return;   // never stored; the compiler cannot drop the work
     }
@@ -968,16 +937,8 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
             const u64 h = (u64)(src - op.a) ^ ((u64)tid << 40);
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = ((h + k) * 0x9E3779B97F4A7C15ull) & ((1ull << 59) - 1);
-        } else if constexpr (ASM) {
-            load_rows16<N>(v, src, tid);
         } else {
-            const ulonglong2* s2 = reinterpret_cast<const ulonglong2*>(src + 16 * tid);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const ulonglong2 w = s2[k];
-                v[2 * k] = w.x;
-                v[2 * k + 1] = w.y;
-            }
+            load_evals<N>(v, src, tid);
         }
     };
     u64 x[16], y[16];
@@ -1070,37 +1031,33 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
     }
     const uint32_t dq = (uint32_t)((1ull << 60) - P.q), e16 = 16 * dq;
     EXACTO_PIN_DECL
+    // operands in store_evals' order: evaluation 16 tid + k at position tid + k T
+    constexpr int T = N / 16;
     if (c != 1) {
-        const ulonglong2* sa = reinterpret_cast<const ulonglong2*>((c == 0 ? A0 : A1) + 16 * tid);
-        const ulonglong2* sb = reinterpret_cast<const ulonglong2*>((c == 0 ? B0 : B1) + 16 * tid);
-#define PIN_T1(e, k0, k1)                                                \
+        const u64* sa = (c == 0 ? A0 : A1) + tid;
+        const u64* sb = (c == 0 ? B0 : B1) + tid;
+#define PIN_T1(k0, k1)                                                   \
         {                                                          \
-            const ulonglong2 u_ = sa[e], v_ = sb[e];               \
             u64 r0_, r1_;                                          \
-            MulNear60PinAsm<2>::run(r0_, r1_, u_.x, v_.x, u_.y, v_.y, dq, e16);   \
+            MulNear60PinAsm<2>::run(r0_, r1_, sa[(k0) * T], sb[(k0) * T], sa[(k1) * T], sb[(k1) * T], dq, e16); \
             PIN_SET(k0, r0_) PIN_SET(k1, r1_)                      \
         }
-        PIN_T1(0, 0, 1) PIN_T1(1, 2, 3) PIN_T1(2, 4, 5) PIN_T1(3, 6, 7)
-        PIN_T1(4, 8, 9) PIN_T1(5, 10, 11) PIN_T1(6, 12, 13) PIN_T1(7, 14, 15)
+        PIN_T1(0, 1) PIN_T1(2, 3) PIN_T1(4, 5) PIN_T1(6, 7)
+        PIN_T1(8, 9) PIN_T1(10, 11) PIN_T1(12, 13) PIN_T1(14, 15)
 #undef PIN_T1
     } else {
-        const ulonglong2* sa0 = reinterpret_cast<const ulonglong2*>(A0 + 16 * tid);
-        const ulonglong2* sa1 = reinterpret_cast<const ulonglong2*>(A1 + 16 * tid);
-        const ulonglong2* sb0 = reinterpret_cast<const ulonglong2*>(B0 + 16 * tid);
-        const ulonglong2* sb1 = reinterpret_cast<const ulonglong2*>(B1 + 16 * tid);
-#define PIN_T2(e, k0, k1)                                                \
+        const u64 *sa0 = A0 + tid, *sa1 = A1 + tid, *sb0 = B0 + tid, *sb1 = B1 + tid;
+#define PIN_T2(k0, k1)                                                   \
         {                                                          \
-            const ulonglong2 u0_ = sa0[e], v1_ = sb1[e];           \
-            const ulonglong2 u1_ = sa1[e], v0_ = sb0[e];           \
             u64 r0_, r1_, s0_, s1_;                                \
-            MulNear60PinAsm<2>::run(r0_, r1_, u0_.x, v1_.x, u0_.y, v1_.y, dq, e16); \
-            MulNear60PinAsm<2>::run(s0_, s1_, u1_.x, v0_.x, u1_.y, v0_.y, dq, e16); \
+            MulNear60PinAsm<2>::run(r0_, r1_, sa0[(k0) * T], sb1[(k0) * T], sa0[(k1) * T], sb1[(k1) * T], dq, e16); \
+            MulNear60PinAsm<2>::run(s0_, s1_, sa1[(k0) * T], sb0[(k0) * T], sa1[(k1) * T], sb0[(k1) * T], dq, e16); \
             PIN_SET(k0, r0_ + s0_) PIN_SET(k1, r1_ + s1_)          \
         }
         // two halves of 16 loads each: hoisting all 32 (128 VGPRs) past the products would spill
-        PIN_T2(0, 0, 1) PIN_T2(1, 2, 3) PIN_T2(2, 4, 5) PIN_T2(3, 6, 7)
+        PIN_T2(0, 1) PIN_T2(2, 3) PIN_T2(4, 5) PIN_T2(6, 7)
         __builtin_amdgcn_sched_barrier(0);
-        PIN_T2(4, 8, 9) PIN_T2(5, 10, 11) PIN_T2(6, 12, 13) PIN_T2(7, 14, 15)
+        PIN_T2(8, 9) PIN_T2(10, 11) PIN_T2(12, 13) PIN_T2(14, 15)
 #undef PIN_T2
     }
     PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
@@ -1130,14 +1087,8 @@ ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
     const PrimeConst& P = primes[(int)(blockIdx.x % (unsigned)period)];
     const uint32_t dq = (uint32_t)((1ull << 60) - P.q);
     u64 x[16], y[16];
-    const ulonglong2* a2 = reinterpret_cast<const ulonglong2*>(A + p * N + 16 * tid);
-    const ulonglong2* b2 = reinterpret_cast<const ulonglong2*>(B + p * N + 16 * tid);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const ulonglong2 u = a2[k], v = b2[k];
-        x[2 * k] = u.x; x[2 * k + 1] = u.y;
-        y[2 * k] = v.x; y[2 * k + 1] = v.y;
-    }
+    load_evals<N>(x, A + p * N, tid);
+    load_evals<N>(y, B + p * N, tid);
     if constexpr (ASM) {
         mul16_near60<false>(x, x, y, dq);
     } else {

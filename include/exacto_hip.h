@@ -20,8 +20,10 @@
  *   - NTT domain: ciphertexts are stored as NttPoly evaluations (src/ring/ntt.rs:11-15)
  *     in THIS library's documented convention (DESIGN.md "NTT convention"): negacyclic
  *     Cooley-Tukey, evaluation k = a(psi^(2*brv(k)+1)), psi = smallest-generator
- *     primitive 2n-th root.  concrete-ntt's own order is not observable from the
- *     reference's tests; all parity is checked after the inverse transform.
+ *     primitive 2n-th root, stored at position (k mod 16)*(n/16) + k/16 (the order
+ *     the device threads hold the values in: contiguous loads and stores).
+ *     concrete-ntt's own order is not observable from the reference's tests; all
+ *     parity is checked after the inverse transform.
  *   - Functions without suffix take HOST pointers and are synchronous.  The `_dev`
  *     variants take DEVICE pointers (hipMalloc'd on the context's device) and are
  *     asynchronous on the context's stream (exacto_ctx_set_stream); call

@@ -95,6 +95,21 @@ static void plan_init(plan_t* p, int n, u64 q) {
 }
 static void plan_free(plan_t* p) { free(p->fwd); free(p->inv); }
 
+/* NTT-domain storage order (oracle/ring.py NttPlan.storage_order): evaluation k
+   (bit-reversed order) at position (k mod 16) n/16 + k / 16; the identity at n = 16 */
+static void ntt_store_order(u64* a, int n, int to_storage) {
+    const int T = n / 16;
+    if (T <= 1) return;
+    u64* tmp = (u64*)malloc(sizeof(u64) * (size_t)n);
+    memcpy(tmp, a, sizeof(u64) * (size_t)n);
+    for (int k = 0; k < n; ++k) {
+        const int pos = (k & 15) * T + (k >> 4);
+        if (to_storage) a[pos] = tmp[k];
+        else a[k] = tmp[pos];
+    }
+    free(tmp);
+}
+
 static void ntt_fwd(const plan_t* p, u64* a) {
     const int n = p->n;
     const u64 q = p->q;
@@ -110,11 +125,13 @@ static void ntt_fwd(const plan_t* p, u64* a) {
             }
         }
     }
+    ntt_store_order(a, n, 1);
 }
 static void ntt_inv(const plan_t* p, u64* a) { /* inv + normalize */
     const int n = p->n;
     const u64 q = p->q;
     int t = 1;
+    ntt_store_order(a, n, 0);
     for (int m = n; m > 1; m >>= 1) {
         const int h = m >> 1;
         int j1 = 0;

@@ -8,8 +8,11 @@ bit-for-bit:
 
 * psi = x^((q-1)/2n) for the smallest x = 2, 3, ... with psi^n == -1 (mod q);
 * forward = Cooley-Tukey negacyclic NTT, natural-order input, bit-reversed
-  output: evals[k] = a(psi^(2*brv(k)+1)) (Longa-Naehrig 2016, Alg. 1);
-* inverse = Gentleman-Sande, bit-reversed input, natural output, unscaled;
+  evaluation order: evaluation k = a(psi^(2*brv(k)+1)) (Longa-Naehrig 2016,
+  Alg. 1), stored at position (k mod 16) n/16 + k // 16 (``storage_order``;
+  round 5: the order in which the device threads hold their values, so the
+  device loads and stores of NTT-domain data are contiguous);
+* inverse = Gentleman-Sande from that storage, natural output, unscaled;
   ``normalize`` multiplies by n^-1 (concrete-ntt's inv/normalize split,
   pinned by the roundtrip KAT ntt.rs:170-178).
 
@@ -106,8 +109,16 @@ class NttPlan:
     def modulus(self) -> int:
         return self.q
 
+    def storage_order(self) -> list[int]:
+        """position -> evaluation index of this build's NTT-domain storage: position
+        (k mod 16) (n/16) + k // 16 holds evaluation k = a(psi^(2 brv(k) + 1)) (the order in which
+        the device transforms' threads hold their 16 values; the identity at n = 16)."""
+        T = self.n // 16
+        return [((p % T) << 4) | (p // T) for p in range(self.n)]
+
     def fwd(self, a: list[int]) -> None:
-        """In-place forward negacyclic NTT (Cooley-Tukey, bit-reversed output)."""
+        """In-place forward negacyclic NTT (Cooley-Tukey, bit-reversed evaluation order), stored in
+        storage_order()."""
         n, q, tw = self.n, self.q, self.psi_rev
         t = n
         m = 1
@@ -122,10 +133,16 @@ class NttPlan:
                     a[j] = (u + v) % q
                     a[j + t] = (u - v) % q
             m <<= 1
+        std = list(a)
+        for p, k in enumerate(self.storage_order()):
+            a[p] = std[k]
 
     def inv(self, a: list[int]) -> None:
-        """In-place inverse (Gentleman-Sande, bit-reversed input), NOT scaled by n^-1."""
+        """In-place inverse (Gentleman-Sande, input in storage_order()), NOT scaled by n^-1."""
         n, q, tw = self.n, self.q, self.psi_inv_rev
+        stored = list(a)
+        for p, k in enumerate(self.storage_order()):
+            a[k] = stored[p]
         t = 1
         m = n
         while m > 1:

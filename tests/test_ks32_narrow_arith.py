@@ -131,6 +131,40 @@ def test_lazy_butterflies_bounds_and_congruence():
             assert o0 < 2 * p and o1 < 2 * p
 
 
+def _signed_first_stage(x0, x1, w, p):
+    """fwd32_round SIN: int16 x0, x1 as int32 bits, one twiddle w; returns (o0, o1) as u32."""
+    c = _shoup(1 << 15, w, p)
+    c = min(c, (c - p) & M32)
+    k1 = 2 * p - c if (p - c) < (1 << 15) else p - c
+    k2 = c + 3 * p if c < (1 << 15) else c + 2 * p
+    kd = (k2 - k1) & M32
+    XK = (x0 + k1) & M32
+    Y = (x1 + (1 << 15)) & M32
+    qh = (Y * ((w << 32) // p)) >> 32
+    o0 = (qh * ((-p) & M32) + Y * w + XK) & M32
+    o1 = (2 * XK + kd - o0) & M32
+    return o0, o1
+
+
+def test_signed_first_stage_bounds_and_congruence():
+    """The digit transform's first stage over raw int16 digits (ks32_dev.hpp fwd32_round SIN): both
+    outputs in [0, 4p) and congruent to x0 +- x1 w, at the int16 extremes and for twiddles whose
+    2^15 w mod p lands near 0 and p (the K1 / K2 adjustments)."""
+    rng = np.random.default_rng(15)
+    for p in _lazy_primes():
+        ws = [int(v) for v in rng.integers(0, p, size=300)] + [0, 1, p - 1]
+        inv = pow(1 << 15, -1, p)
+        ws += [(c * inv) % p for c in (0, 1, (1 << 15) - 1, 1 << 15, p - 1, p - (1 << 15), p - (1 << 15) + 1)]
+        edge = [-(1 << 15), -1, 0, 1, (1 << 15) - 1]
+        for w in ws:
+            xs = [(a, b) for a in edge for b in edge]
+            xs += [(int(a), int(b)) for a, b in rng.integers(-(1 << 15), 1 << 15, size=(20, 2))]
+            for a, b in xs:
+                o0, o1 = _signed_first_stage(a & M32, b & M32, w, p)
+                assert o0 < 4 * p and o1 < 4 * p, (p, w, a, b, o0, o1)
+                assert o0 % p == (a + b * w) % p and o1 % p == (a - b * w) % p, (p, w, a, b)
+
+
 def test_lazy_mac_reduction():
     """The MAC's lazy reduction of a signed 64-bit accumulator: [0, 2p), congruent (ks32.hip)."""
     rng = np.random.default_rng(64)

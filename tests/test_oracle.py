@@ -97,19 +97,25 @@ def test_reference_kat(kat):
     assert got == kat["expected"], kat["source"]
 
 
-def test_ntt_convention_is_negacyclic_evaluation():
-    """evals[k] = a(psi^(2*brv(k)+1)) — the documented convention."""
-    n, q = 16, 65537
+@pytest.mark.parametrize("n,q", [(16, 65537), (64, 65537), (256, 65537)])
+def test_ntt_convention_is_negacyclic_evaluation(n, q):
+    """Position (k mod 16) n/16 + k // 16 holds a(psi^(2*brv(k)+1)) — the documented convention
+    (the identity order at n = 16)."""
     plan = NttPlan(n, q)
     rng = random.Random(3)
     a = [rng.randrange(q) for _ in range(n)]
     ev = list(a)
     plan.fwd(ev)
     from oracle.ring import bit_reverse
+    logn = n.bit_length() - 1
     for k in range(n):
-        x = pow(plan.psi, 2 * bit_reverse(k, 4) + 1, q)
-        assert ev[k] == sum(c * pow(x, i, q) for i, c in enumerate(a)) % q
+        x = pow(plan.psi, 2 * bit_reverse(k, logn) + 1, q)
+        assert ev[(k % 16) * (n // 16) + k // 16] == sum(c * pow(x, i, q) for i, c in enumerate(a)) % q
     assert pow(plan.psi, n, q) == q - 1
+    back = list(ev)
+    plan.inv(back)
+    plan.normalize(back)
+    assert back == a
 
 
 def test_make_plan_errors():

@@ -30,7 +30,6 @@ for v in "$@"; do
     as1) build as1 -DEXACTO_TW_AS=1 ;;
     as1_w4) build as1_w4 -DEXACTO_TW_AS=1 -DEXACTO_NTT_WAVES=4 ;;
     as4_w4) build as4_w4 -DEXACTO_NTT_WAVES=4 ;;
-    notout) build notout -DEXACTO_NTT_TOUT=0 ;;
     nopre) build nopre -DEXACTO_NTT_PRELOAD=0 ;;
     nopre_w5) build nopre_w5 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=5 ;;
     nopre_w6) build nopre_w6 -DEXACTO_NTT_PRELOAD=0 -DEXACTO_NTT_WAVES=6 ;;
