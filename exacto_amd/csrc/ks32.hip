@@ -214,9 +214,9 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     ks32_crt_values<LOGN, S, LAZY>(x, U, R, r_stride, L, b, lds, tid, KT, primes, qprimes);
     const uint32_t CL = 2 * L;
     const long item = b / CL;
-    u64* dst = R + item * r_stride + (long)(b - (uint32_t)item * CL) * N;
+    const __amdgpu_buffer_rsrc_t rd = poly_rsrc(R + item * r_stride + (long)(b - (uint32_t)item * CL) * N, N * 8);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[k * T + tid] = x[k];
+    for (int k = 0; k < 16; ++k) buf_st64(rd, x[k], tid * 8, k * T * 8);
 }
 
 // dBFV: the gadget digits of the products of one output limb k summed before their transforms.

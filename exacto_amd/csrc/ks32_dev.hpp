@@ -4,6 +4,7 @@
 // the centred CRT lift of the key-switched sums.
 #pragma once
 #include "exacto_internal.hpp"
+#include "bufmem.hpp"
 
 namespace exacto {
 
@@ -178,8 +179,9 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
         x[k] = FORM == F32_WIDE ? red32(x[k], p) : red32(min(x[k], x[k] - 2 * p), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = x[k] > half ? x[k] - p : x[k];
+    const __amdgpu_buffer_rsrc_t rd = poly_rsrc(dst, T * 16 * 4);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * T] = x[k];   // evaluation 16 tid + k (ntt.hip store_evals)
+    for (int k = 0; k < 16; ++k) buf_st32(rd, x[k], tid * 4, k * T * 4);   // evaluation 16 tid + k (ntt.hip store_evals)
 }
 
 // ---------------------------------------------------------------- inverse (Gentleman-Sande)
@@ -306,9 +308,10 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
     uint32_t v[S][16];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const uint32_t* src = U + ((long)b * S + s) * N + tid;   // evaluation 16 tid + k at tid + k T
+        // evaluation 16 tid + k at tid + k T
+        const __amdgpu_buffer_rsrc_t rs = poly_rsrc(U + ((long)b * S + s) * N, N * 4);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[s][k] = src[k * T];
+        for (int k = 0; k < 16; ++k) v[s][k] = buf_ld32(rs, tid * 4, k * T * 4);
         inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
     }
     uint32_t pr[S], hp[S];
@@ -321,13 +324,13 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
     const u64 q = qprimes[l].q;
     const uint32_t dq = (uint32_t)((1ull << 60) - q);
     const u64 negP = KT->negP[l];
-    const u64* src = R + item * r_stride + (long)cl * N;
+    const __amdgpu_buffer_rsrc_t rr = poly_rsrc(R + item * r_stride + (long)cl * N, N * 8);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         uint32_t vk[S];
 #pragma unroll
         for (int s = 0; s < S; ++s) vk[s] = v[s][k];
-        x[k] = ks32_lift_one<S, LAZY>(vk, src[k * T + tid], pr, hp, KT, q, dq, negP);
+        x[k] = ks32_lift_one<S, LAZY>(vk, buf_ld64(rr, tid * 8, k * T * 8), pr, hp, KT, q, dq, negP);
     }
 }
 

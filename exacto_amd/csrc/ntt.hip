@@ -13,6 +13,7 @@
 // Gentleman-Sande inverse, bit-reversed in / natural out.
 #include "exacto_internal.hpp"
 #include "ks32_dev.hpp"
+#include "bufmem.hpp"
 
 namespace exacto {
 
@@ -193,16 +194,29 @@ __device__ __forceinline__ void fwd_rounds(u64 (&x)[16], u64* lds, int tid, TwTa
 // contiguous memory, and the forward needs no LDS transpose before its stores.  (Round 5: with
 // the standard order the inverse-side loads ran at a 128-byte lane stride; the cfg3 tensor kernel
 // 308 -> 265 us.)
+// (Also the order of the inverse's output, elem_index<LOGN - 4>(tid, k) = tid + k n/16, and of the
+// forward's coefficient input.)  Buffer accesses (bufmem.hpp): no VALU for the addresses.
+#ifndef EXACTO_BUF_LD
+#define EXACTO_BUF_LD 1
+#endif
+#ifndef EXACTO_BUF_ST
+#define EXACTO_BUF_ST 1
+#endif
+typedef PolyIO<EXACTO_BUF_LD != 0> PolyRd;
+typedef PolyIO<EXACTO_BUF_ST != 0> PolyWr;
+
 template <int N>
-__device__ __forceinline__ void store_evals(u64* __restrict__ dst, const u64 (&x)[16], int tid) {
+__device__ __forceinline__ void store_evals(u64* dst, const u64 (&x)[16], int tid) {
+    const PolyWr w(dst, N * 8);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * (N / 16)] = x[k];
+    for (int k = 0; k < 16; ++k) w.st64(x[k], tid * 8, k * (N / 16) * 8);
 }
 
 template <int N>
-__device__ __forceinline__ void load_evals(u64 (&x)[16], const u64* __restrict__ src, int tid) {
+__device__ __forceinline__ void load_evals(u64 (&x)[16], const u64* src, int tid) {
+    const PolyRd r(src, N * 8);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = src[tid + k * (N / 16)];
+    for (int k = 0; k < 16; ++k) x[k] = r.ld64(tid * 8, k * (N / 16) * 8);
 }
 #ifdef EXACTO_NTT_WAVES
 #define NTT_OCC __attribute__((amdgpu_waves_per_eu(EXACTO_NTT_WAVES)))
@@ -224,8 +238,7 @@ __device__ __forceinline__ void load_coeffs(u64 (&x)[16], const NttBatch& nb, co
             x[k] = d < 0 ? q + (u64)d : (u64)d;
         }
     } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = src[tid + k * T];
+        load_evals<N>(x, src, tid);
     }
 }
 
@@ -424,7 +437,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
@@ -440,8 +452,7 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 
     inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
 
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+    store_evals<N>(dst, x, tid);
 }
 
 // ---------------------------------------------------------------- inverse, hand-scheduled rounds
@@ -586,7 +597,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_
 ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
     constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const int p = blockIdx.x;
@@ -598,14 +608,18 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     EXACTO_PIN_DECL
     {   // evaluation 16 tid + k from position tid + k T (store_evals' order)
         constexpr int T = N / 16;
-#define PIN_INP(k) PIN_SET(k, src[tid + (k) * T])
+        const PolyRd rs(src, N * 8);
+#define PIN_INP(k) PIN_SET(k, rs.ld64(tid * 8, (k) * T * 8))
         PIN_X16(PIN_INP)
 #undef PIN_INP
     }
     PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
-#define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
-    PIN_X16(PIN_OUT)
+    {
+        const PolyWr rd(dst, N * 8);
+#define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, (k) * (N / 16) * 8);
+        PIN_X16(PIN_OUT)
 #undef PIN_OUT
+    }
 }
 
 // Probe mode 3 (tools/ntt_probe.hip): the first generation of resident blocks (`slots`, one per CU
@@ -654,7 +668,6 @@ template <int LOGN, int QB = 60>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(3)))
 ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const int p = blockIdx.x;
@@ -666,8 +679,7 @@ ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
     u64 x[16];
     load_evals<N>(x, src, tid);
     inv_rounds_asm<LOGN, 0, true, QB>(x, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P));
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+    store_evals<N>(dst, x, tid);
 }
 
 // Forward NTT, n = 4096 / 8192, pinned homes: fwd_rounds_asm's rounds and exchanges, output in
@@ -712,8 +724,9 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
 #undef PIN_IN16
     } else {
         const u64* src = nb.src + (nb.src_off ? (long)nb.src_off[item] : (long)item * nb.src_item_stride) +
-                         (long)sub * N + tid;
-#define PIN_IN64(k) PIN_SET(k, src[(k) * T])
+                         (long)sub * N;
+        const PolyRd rs(src, N * 8);
+#define PIN_IN64(k) PIN_SET(k, rs.ld64(tid * 8, (k) * T * 8))
         PIN_X16(PIN_IN64)
 #undef PIN_IN64
     }
@@ -728,7 +741,8 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
     if constexpr (PROBE == 1) {
         if (nb.dst_item_stride != -7) return;   // never stored; the compiler cannot drop the work
     }
-#define PIN_OUT(k) dst[tid + (k) * T] = PIN_GET(k);
+    const PolyWr rd(dst, N * 8);
+#define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, (k) * T * 8);
     PIN_X16(PIN_OUT)
 #undef PIN_OUT
 }
@@ -887,7 +901,6 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
                       const PrimeConst* __restrict__ primes, int remap, int p2only = 0, int share_np = 0) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
@@ -989,8 +1002,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         if (remap != -7) return;   // never stored; the compiler cannot drop the work
     }
     u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+    store_evals<N>(dst, x, tid);
 }
 
 // The tensor kernel over pinned homes (n = 4096 / 8192, special primes): the products
@@ -1003,7 +1015,6 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
                           const PrimeConst* __restrict__ primes, int remap, int p2only, int share_np) {
     static_assert(LOGN == 12 || LOGN == 13, "pinned rounds exist for n = 4096 and 8192");
     constexpr int N = 1 << LOGN;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const int NP = L + K;
@@ -1033,25 +1044,26 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
     EXACTO_PIN_DECL
     // operands in store_evals' order: evaluation 16 tid + k at position tid + k T
     constexpr int T = N / 16;
+    const int vo = tid * 8;
+#define LDE(r_, k_) r_.ld64(vo, (k_) * T * 8)
     if (c != 1) {
-        const u64* sa = (c == 0 ? A0 : A1) + tid;
-        const u64* sb = (c == 0 ? B0 : B1) + tid;
+        const PolyRd sa(c == 0 ? A0 : A1, N * 8), sb(c == 0 ? B0 : B1, N * 8);
 #define PIN_T1(k0, k1)                                                   \
         {                                                          \
             u64 r0_, r1_;                                          \
-            MulNear60PinAsm<2>::run(r0_, r1_, sa[(k0) * T], sb[(k0) * T], sa[(k1) * T], sb[(k1) * T], dq, e16); \
+            MulNear60PinAsm<2>::run(r0_, r1_, LDE(sa, k0), LDE(sb, k0), LDE(sa, k1), LDE(sb, k1), dq, e16); \
             PIN_SET(k0, r0_) PIN_SET(k1, r1_)                      \
         }
         PIN_T1(0, 1) PIN_T1(2, 3) PIN_T1(4, 5) PIN_T1(6, 7)
         PIN_T1(8, 9) PIN_T1(10, 11) PIN_T1(12, 13) PIN_T1(14, 15)
 #undef PIN_T1
     } else {
-        const u64 *sa0 = A0 + tid, *sa1 = A1 + tid, *sb0 = B0 + tid, *sb1 = B1 + tid;
+        const PolyRd sa0(A0, N * 8), sa1(A1, N * 8), sb0(B0, N * 8), sb1(B1, N * 8);
 #define PIN_T2(k0, k1)                                                   \
         {                                                          \
             u64 r0_, r1_, s0_, s1_;                                \
-            MulNear60PinAsm<2>::run(r0_, r1_, sa0[(k0) * T], sb1[(k0) * T], sa0[(k1) * T], sb1[(k1) * T], dq, e16); \
-            MulNear60PinAsm<2>::run(s0_, s1_, sa1[(k0) * T], sb0[(k0) * T], sa1[(k1) * T], sb0[(k1) * T], dq, e16); \
+            MulNear60PinAsm<2>::run(r0_, r1_, LDE(sa0, k0), LDE(sb1, k0), LDE(sa0, k1), LDE(sb1, k1), dq, e16); \
+            MulNear60PinAsm<2>::run(s0_, s1_, LDE(sa1, k0), LDE(sb0, k0), LDE(sa1, k1), LDE(sb0, k1), dq, e16); \
             PIN_SET(k0, r0_ + s0_) PIN_SET(k1, r1_ + s1_)          \
         }
         // two halves of 16 loads each: hoisting all 32 (128 VGPRs) past the products would spill
@@ -1060,11 +1072,15 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
         PIN_T2(8, 9) PIN_T2(10, 11) PIN_T2(12, 13) PIN_T2(14, 15)
 #undef PIN_T2
     }
+#undef LDE
     PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
     u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
-#define PIN_OUT(k) dst[elem_index<LAST_LO>(tid, k)] = PIN_GET(k);
-    PIN_X16(PIN_OUT)
+    {
+        const PolyWr rd(dst, N * 8);
+#define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, (k) * (N / 16) * 8);
+        PIN_X16(PIN_OUT)
 #undef PIN_OUT
+    }
 }
 
 // ---------------------------------------------------------------- fused product + inverse
@@ -1079,7 +1095,6 @@ ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
                   const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
     constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = T < 64 ? vtid() : (int)threadIdx.x;
     if (tid >= T) return;
@@ -1102,8 +1117,7 @@ ntt_mulinv_kernel(const u64* A, const u64* B, u64* out, int period,
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
     u64* dst = out + p * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = x[k];
+    store_evals<N>(dst, x, tid);
 }
 
 template <int LOGN>
@@ -1157,8 +1171,6 @@ template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(2)))
 ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const PrimeConst* __restrict__ primes) {
     constexpr int N = 1 << LOGN;
-    constexpr int T = N / 16;
-    constexpr int LAST_LO = LOGN - 4;
     __shared__ u64 lds[N];
     const int tid = threadIdx.x;
     const long p = blockIdx.x;
@@ -1167,10 +1179,8 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     const u64* a = A + p * N;
     const u64* b = B + p * N;
     u64 xa[16], xb[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) xa[k] = a[tid + k * T];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) xb[k] = b[tid + k * T];
+    load_evals<N>(xa, a, tid);   // coefficients tid + k T
+    load_evals<N>(xb, b, tid);
     const AsmK K = make_asmk(q);
     const TwTab tf = tw_table(P.tw_fwd);
     fwd_rounds_asm<LOGN, 0>(xa, lds, tid, tf, K);
@@ -1180,8 +1190,7 @@ ntt_polymul_kernel(const u64* A, const u64* B, u64* out, int period, const Prime
     const AsmK AK = make_asmk_inv(P);
     inv_rounds_asm<LOGN, 0>(xa, lds, tid, tw_table(P.tw_inv), AK);
     u64* dst = out + p * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dst[elem_index<LAST_LO>(tid, k)] = xa[k];
+    store_evals<N>(dst, xa, tid);
 }
 
 bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period, int logn, const PrimeConst* primes,

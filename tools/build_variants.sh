@@ -37,6 +37,9 @@ for v in "$@"; do
     ilp) build ilp -mllvm -amdgpu-sched-strategy=max-ilp ;;
     ilp_w3) build ilp_w3 -mllvm -amdgpu-sched-strategy=max-ilp -DEXACTO_NTT_WAVES=3 ;;
     nomulasm) build nomulasm -DEXACTO_MUL_ASM=0 ;;
+    ld1st0) build ld1st0 -DEXACTO_BUF_ST=0 ;;
+    ld0st1) build ld0st1 -DEXACTO_BUF_LD=0 ;;
+    ld0st0) build ld0st0 -DEXACTO_BUF_LD=0 -DEXACTO_BUF_ST=0 ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
