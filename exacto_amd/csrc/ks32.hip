@@ -51,7 +51,7 @@ ks32_digit_ntt_kernel(const DT* __restrict__ D16, uint32_t* __restrict__ DS, int
         const int d = src[tid + k * T];
         x[k] = SIN ? (uint32_t)d : d < 0 ? P.p + (uint32_t)d : (uint32_t)d;
     }
-    fwd32_store<LOGN, FORM, SIN>(x, lds, tid, P, DS + (long)b * N);
+    fwd32_store<LOGN, FORM, SIN, FORM != F32_LAZY>(x, lds, tid, P, DS + (long)b * N);
 }
 
 // key rows [rows][n] canonical mod q_{row's limb} (u64) -> RS [rows][S][n]: balanced, mod p_s, NTT
@@ -143,12 +143,14 @@ __device__ __forceinline__ long long red_s64_lazy(long long x, const Prime32& P)
 // U[item][cl][s][j] = sum_g DS[item][g][s][j] * RS[g][cl][s][j] mod p_s   (cl = c * L + l)
 // Block: 64 coefficients j of one prime s, CLB consecutive (c, l) pairs starting at cl0, and up to
 // 4 NW items; its key words (G * CLB * 64, balanced) are staged in LDS once.  Lane = coefficient,
-// wave w handles items it0 + w, it0 + w + NW, ...  Digit residues and key are stored balanced by
-// their transforms, |product| < (p/2)^2 < 2^60, so seven signed products plus the carried value
-// (< 2^33.6) stay below 2^63 (one v_mad_i64_i32 each) before a lazy reduction.
+// wave w handles items it0 + w, it0 + w + NW, ...  The key is stored balanced by its transform, the
+// digit residues balanced too except under the lazy form (canonical, < p < 2^30: |product| <
+// 2^30 2^29 = 2^59 still), so the run's signed products plus the carried value (< 2^33.6) stay
+// below 2^63 (one v_mad_i64_i32 each) before a lazy reduction.
 constexpr int KS_LS = 64;
-// RUN: signed products summed between reductions: 12 for primes below 2^32 / 3 (products below
-// 2^58.9), 7 for primes up to 2^31 (products below 2^60; 7 * 2^60 + 2^33.6 < 2^63)
+// RUN: signed products summed between reductions: 12 for primes below 2^32 / 3 (balanced products
+// below 2^58.9; lazy basis: below 2^59), 7 for primes up to 2^31 (products below 2^60;
+// 7 * 2^60 + 2^33.6 < 2^63)
 // LZ: lazy basis (p < 2^30), sums written in [0, 2p) (red_s64_lz) for the lazy inverse transforms
 template <int CLB, int NW, int RUN, bool LZ = false>
 __global__ void __launch_bounds__(NW * 64)

@@ -168,17 +168,23 @@ __device__ __forceinline__ void fwd32_rounds(uint32_t (&x)[16], uint32_t* lds, i
 // order (evaluation 16 tid + k at position tid + k T: coalesced, no LDS transpose), as balanced
 // residues in (-p/2, p/2] (int32 bits): the only consumer, ks32_mac_kernel, multiplies balanced
 // values position by position, and ks32_crt_values reads its sums in the same order
-template <int LOGN, int FORM, bool SIN = false>
+// BAL = false (the digit transforms under the lazy form): canonical [0, p) instead of balanced; with
+// p < 2^30 and the key balanced (|r| <= p/2), a product stays below 2^59 and the MAC's runs of 12
+// below 2^63 all the same (3 VALU per value less)
+template <int LOGN, int FORM, bool SIN = false, bool BAL = true>
 __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P,
                                             uint32_t* __restrict__ dst) {
     constexpr int T = (1 << LOGN) / 16;
     const uint32_t p = P.p, half = p >> 1;
+    static_assert(BAL || FORM == F32_LAZY, "canonical digit residues: lazy primes only (MAC bound)");
     fwd32_rounds<LOGN, 0, FORM, SIN>(x, lds, tid, tw32(P.tw_fwd), p);
 #pragma unroll
     for (int k = 0; k < 16; ++k)   // lazy [0, 4p) / narrow [0, 3p] / wide [0, 2p) -> [0, p)
         x[k] = FORM == F32_WIDE ? red32(x[k], p) : red32(min(x[k], x[k] - 2 * p), p);
+    if constexpr (BAL) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = x[k] > half ? x[k] - p : x[k];
+        for (int k = 0; k < 16; ++k) x[k] = x[k] > half ? x[k] - p : x[k];
+    }
     const __amdgpu_buffer_rsrc_t rd = poly_rsrc(dst, T * 16 * 4);
 #pragma unroll
     for (int k = 0; k < 16; ++k) buf_st32(rd, x[k], tid * 4, k * T * 4);   // evaluation 16 tid + k (ntt.hip store_evals)
@@ -190,7 +196,9 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
 // min-subtraction and U + 2p - V < 4p goes to the Shoup product as is (9 VALU per butterfly);
 // otherwise both inputs are first reduced to [0, p) (11 VALU).  Outputs below 2p, the last stage's
 // canonical.
-template <int LOGN, int LO, int BLO, int BHI, bool LAZY>
+// OUT2P (lazy only): the last stage's outputs stay in [0, 2p) (the Garner terms of ks32_lift_one
+// for s >= 1 take them unreduced)
+template <int LOGN, int LO, int BLO, int BHI, bool LAZY, bool OUT2P = false>
 __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Prime32& P) {
     constexpr int N = 1 << LOGN;
     const uint32_t p = P.p, p2 = 2 * p;
@@ -209,9 +217,13 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
                 const int k0 = g * 2 * half + m, k1 = k0 + half;
                 if constexpr (LAZY) {
                     const uint32_t U = x[k0], V = x[k1];
-                    if (b == LOGN - 1) {  // n^-1 folded in, canonical
-                        x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
-                        x[k1] = red32(shoup32(U + p2 - V, P.last_w, P.last_ws, p), p);
+                    if (b == LOGN - 1) {  // n^-1 folded in, canonical (OUT2P: below 2p)
+                        x[k0] = shoup32(U + V, P.n_inv, P.n_inv_s, p);
+                        x[k1] = shoup32(U + p2 - V, P.last_w, P.last_ws, p);
+                        if constexpr (!OUT2P) {
+                            x[k0] = red32(x[k0], p);
+                            x[k1] = red32(x[k1], p);
+                        }
                     } else {
                         const uint32_t sum = U + V;
                         x[k0] = min(sum, sum - p2);
@@ -232,7 +244,7 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
     }
 }
 
-template <int LOGN, int R, bool LAZY>
+template <int LOGN, int R, bool LAZY, bool OUT2P = false>
 __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -244,8 +256,8 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
         lds_sync();
         lds32_load<LO>(lds, x, tid);
     }
-    inv32_round<LOGN, LO, BLO, BHI, LAZY>(x, tid, P);
-    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY>(x, lds, tid, P);
+    inv32_round<LOGN, LO, BLO, BHI, LAZY, OUT2P>(x, tid, P);
+    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY, OUT2P>(x, lds, tid, P);
 }
 
 // One coefficient's centred Garner lift of its S residues v[s] (canonical mod p_s) evaluated mod
@@ -254,7 +266,8 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
 // 2^60 == d (5 instructions); the centring (x > floor(P/2)) is decided on the mixed-radix digits and
 // adds q - (P mod q).
 // LAZY (every p_s below 2^30): a_kk < p_kk < 2 p_s enters t + 2 p_s - a_kk < 4 p_s < 2^32 unreduced
-// (the Shoup product takes any 32-bit input): one min-subtraction less per Garner term.
+// (the Shoup product takes any 32-bit input): one min-subtraction less per Garner term; v[s] for
+// s >= 1 may then be anywhere in [0, 2 p_s) (the inverse transforms' OUT2P form).
 template <int S, bool LAZY = false>
 __device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, const uint32_t (&pr)[S],
                                              const uint32_t (&hp)[S], const Ks32Tables* __restrict__ KT, u64 q,
@@ -312,7 +325,9 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
         const __amdgpu_buffer_rsrc_t rs = poly_rsrc(U + ((long)b * S + s) * N, N * 4);
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[s][k] = buf_ld32(rs, tid * 4, k * T * 4);
-        inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
+        // s >= 1 (lazy): residues in [0, 2p), which the Garner terms take as they are
+        if (s == 0) inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
+        else inv32_rounds<LOGN, 0, LAZY, LAZY>(v[s], lds, tid, primes[s]);
     }
     uint32_t pr[S], hp[S];
 #pragma unroll
