@@ -1199,8 +1199,10 @@ static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only
         bytes = cnt * (p2only ? pb * (7.0 * c->L + 3.0 * c->K) : pb * 7.0 * NP);
     }
     ProfScope ps(c, PK_TENSOR, (u64)cnt * (p2only ? 3 * c->L + c->K : 3 * NP), bytes);
+    // the exact path's scale kernels take T in [0, 2q) (shoup products, 30-bit-limb dot products with
+    // headroom); the HPS scale subtracts residues as canonical
     launch_inv_tensor(o, c->ws_extP, c->ws_T, cnt, c->logn, c->L, c->K, lazy, c->d_primes, c->stream, near60, p2only,
-                      qbits, c->tensor_share_npairs);
+                      qbits, c->tensor_share_npairs, near60 && c->path != EXACTO_PATH_HPS);
     CHECK_LAUNCH();
     return 0;
 }

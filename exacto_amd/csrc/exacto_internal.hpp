@@ -155,7 +155,9 @@ void launch_mul_inv(const u64* A, const u64* B, u64* out, long rows, int period,
 // psum; asm_inv and n = 4096 / 8192 only)
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
                        const PrimeConst* primes, hipStream_t s, bool asm_inv = false, bool p2only = false,
-                       int qbits = 64, int share_np = 0);
+                       int qbits = 64, int share_np = 0, bool lazy_out = false);
+// lazy_out (asm_inv only): T's residues in [0, 2q) instead of canonical -- for the exact path's
+// scale kernels (shoup products and 30-bit-limb dot products), never for HPS
 // Decryption (bfv/encrypt.rs:111-178, dbfv/decrypt.rs:20-79), kernels.hip.
 void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* out, int items, int n, int L,
                   const PrimeConst* primes, hipStream_t s);

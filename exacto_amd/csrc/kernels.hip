@@ -560,7 +560,9 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
 #pragma unroll
     for (int a = 0; a < K; ++a) {
         const u64 pa = primes[L + a].q, np = (u64)0 - pa;
-        const u64 ta = Tin[(long)(L + a) * n];   // canonical (the inverse tensor's last stage)
+        // [0, 2q) (the tensor's lazy last stage): ta >> 30 < 2^31 doubles one term of a1 and a2,
+        // still far inside dot30_fold's budget (< (m + 4.1) 2^60 with m = L + 1 <= 7 terms)
+        const u64 ta = Tin[(long)(L + a) * n];
         Dot30 A{negs ? 1ull : 0ull, 0, 0};
         dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->pq_w[a]);
 #pragma unroll

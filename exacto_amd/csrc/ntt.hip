@@ -463,7 +463,9 @@ ntt_inv_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // convention, twiddle layout and LDS exchanges as inv_rounds.
 // GEN: the generic-prime statements (InvRoundGenAsm: any prime below 2^60, conditional-subtraction
 // reductions; the HPS auxiliary primes), same layout and bounds contract.
-template <int LOGN, int R, bool GEN = false, int QB = 60>
+// LZ (special primes only): the last round leaves its outputs in [0, 2q) (InvRoundAsm<.., true>;
+// the tensor kernels' consumers take them)
+template <int LOGN, int R, bool GEN = false, int QB = 60, bool LZ = false>
 __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, TwTab tab, const AsmK& K) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -480,8 +482,8 @@ __device__ __forceinline__ void inv_rounds_asm(u64 (&x)[16], u64* lds, int tid, 
         lds_load_x<LO>(lds, x, t2);
     }
     if constexpr (GEN) InvRoundGenAsm<LOGN, R, QB>::run(x, tw, K);
-    else InvRoundAsm<LOGN, R>::run(x, tw, K);
-    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1, GEN, QB>(x, lds, tid, tab, K);
+    else InvRoundAsm<LOGN, R, LZ && BHI == LOGN - 1>::run(x, tw, K);
+    if constexpr (BHI < LOGN - 1) inv_rounds_asm<LOGN, R + 1, GEN, QB, LZ>(x, lds, tid, tab, K);
 }
 
 // The smaller-prime forms of the generic rounds (tools/gen_ntt_asm.py GEN_QBITS): a batch whose
@@ -529,7 +531,8 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
 // The inverse rounds over the pinned homes (inputs < 4q; output element LAST_LO-layout, canonical):
 // inv_rounds_asm's twiddles and exchanges.  A macro because the homes are the enclosing
 // kernel's register variables.
-#define PIN_INV_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
+// SFX_: empty, or _LZ for the tensor kernels' last round with outputs in [0, 2q)
+#define PIN_INV_ROUNDS(LOGN_, lds_, tid_, tab_, K_, SFX_)                                        \
     {                                                                                            \
         const AsmK pin_K = (K_);                                                                 \
         const TwTab pin_tab = (tab_);                                                            \
@@ -548,13 +551,13 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
             TwPair tw[15];                                                                       \
             load_round_tw_inv<LOGN_, 8, 8, 11>(tw, tid_, pin_tab);                               \
             PIN_EXCHANGE(lds_, tid_, 4, 8)                                                       \
-            if constexpr (LOGN_ == 12) EXACTO_INV_PIN_12_2(tw, pin_K); else EXACTO_INV_PIN_13_2(tw, pin_K); \
+            if constexpr (LOGN_ == 12) EXACTO_INV_PIN_12_2##SFX_(tw, pin_K); else EXACTO_INV_PIN_13_2(tw, pin_K); \
         }                                                                                        \
         if constexpr (LOGN_ == 13) {                                                             \
             TwPair tw[15];                                                                       \
             load_round_tw_inv<13, 9, 12, 12>(tw, tid_, pin_tab);                                 \
             PIN_EXCHANGE(lds_, tid_, 8, 9)                                                       \
-            EXACTO_INV_PIN_13_3(tw, pin_K);                                                      \
+            EXACTO_INV_PIN_13_3##SFX_(tw, pin_K);                                                \
         }                                                                                        \
     }
 
@@ -613,7 +616,7 @@ ntt_inv_pin_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
         PIN_X16(PIN_INP)
 #undef PIN_INP
     }
-    PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
+    PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P), )
     {
         const PolyWr rd(dst, N * 8);
 #define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, (k) * (N / 16) * 8);
@@ -894,7 +897,8 @@ __device__ __forceinline__ void tensor_block(long b, long total, int per, int L,
 // after the transform: 296 -> 357 us, removed.)
 // GEN (n = 4096 / 8192, every prime below 2^60 but not all 2^60 - d: HPS): lazy Barrett products,
 // then the generated generic-prime inverse rounds (InvRoundGenAsm) instead of the C++ ones.
-template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false, int QB = 60>
+// LZO (ASM only): outputs in [0, 2q), as ntt_inv_tensor_pin_kernel
+template <int LOGN, bool LAZY, bool ASM = false, int PROBE = 0, bool GEN = false, int QB = 60, bool LZO = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16)
 __attribute__((amdgpu_waves_per_eu(3)))  // the ASM form otherwise takes 184 VGPRs (2 waves/SIMD)
 ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
@@ -994,7 +998,7 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
         // no transform: the products are stored as they are
     } else if constexpr (ASM || GEN) {
         const AsmK AK = GEN ? make_asmk_inv_mont(P) : make_asmk_inv(P);
-        inv_rounds_asm<LOGN, 0, GEN, QB>(x, lds, tid, tw_table(P.tw_inv), AK);
+        inv_rounds_asm<LOGN, 0, GEN, QB, LZO && ASM && !GEN>(x, lds, tid, tw_table(P.tw_inv), AK);
     } else {
         inv_rounds<LOGN, 0, LAZY>(x, lds, tid, tw_table(P.tw_inv), P);
     }
@@ -1009,7 +1013,9 @@ ntt_inv_tensor_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict
 // (MulNear60PinAsm: temps v44-v71, below the homes; < 2q, c1 < 4q) go straight into the homes, and the inverse rounds are
 // PIN_INV_ROUNDS -- one set of value registers, four waves per SIMD (n = 8192: two 8-wave
 // workgroups per CU).  Same blocks, remap and p2only as ntt_inv_tensor_kernel.
-template <int LOGN>
+// LZO: outputs in [0, 2q) (the exact path's scale kernels take them; never for HPS, whose scale
+// subtracts residues as canonical)
+template <int LOGN, bool LZO = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __restrict__ Tout, int L, int K,
                           const PrimeConst* __restrict__ primes, int remap, int p2only, int share_np) {
@@ -1073,7 +1079,11 @@ ntt_inv_tensor_pin_kernel(Operands op, const u64* __restrict__ extP, u64* __rest
 #undef PIN_T2
     }
 #undef LDE
-    PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P))
+    if constexpr (LZO) {
+        PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P), _LZ)
+    } else {
+        PIN_INV_ROUNDS(LOGN, lds, tid, tw_table(P.tw_inv), make_asmk_inv(P), )
+    }
     u64* dst = Tout + ((item * 3 + c) * NP + t) * N;   // [item][c][prime][n]
     {
         const PolyWr rd(dst, N * 8);
@@ -1309,21 +1319,29 @@ static bool gen_small(int qbits) {
 template <int LOGN>
 static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, int L, int K, bool lazy,
                       const PrimeConst* primes, hipStream_t s, bool asm_inv = false, int p2only = 0, int qbits = 64,
-                      int np = 0) {
+                      int np = 0, bool lzo = false) {
     constexpr int threads = (1 << LOGN) / 16;
     // EXACTO_XCD_REMAP=0: plain block order (A/B switch)
     static const int remap = [] { const char* e = std::getenv("EXACTO_XCD_REMAP"); return (e && e[0] == '0') ? 0 : 1; }();
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv && tensor_pin_at(LOGN)) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
-            hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L, K,
-                               primes, remap, p2only, np);
+            if (lzo)
+                hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN, true>), dim3(b2), dim3(threads), 0, s, op, extP, T,
+                                   L, K, primes, remap, p2only, np);
+            else
+                hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L,
+                                   K, primes, remap, p2only, np);
             return;
         }
         if (asm_inv) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
-            hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
-                               T, L, K, primes, remap, p2only, np);
+            if (lzo)
+                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 0, false, 60, true>), dim3(b2),
+                                   dim3(threads), 0, s, op, extP, T, L, K, primes, remap, p2only, np);
+            else
+                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
+                                   T, L, K, primes, remap, p2only, np);
             return;
         }
     }
@@ -1347,7 +1365,8 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
 }
 
 void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, int logn, int L, int K, bool lazy,
-                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits, int share_np) {
+                       const PrimeConst* primes, hipStream_t s, bool asm_inv, bool p2only, int qbits, int share_np,
+                       bool lazy_out) {
     // prime-major block order needs whole dBFV items in the launch (tensor_block)
     // (measured: cfg5, 36 products per item, tensor 270 -> 261 us; cfg4's 3 products per item and
     // u64_dbfv within noise: applied from 8 products per item)
@@ -1355,8 +1374,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;
     if (p2only) {   // the caller checks asm_inv and n = 4096 / 8192
-        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np);
-        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np);
+        if (logn == 12) launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np, lazy_out);
+        else if (logn == 13) launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, true, 1, 64, share_np, lazy_out);
         return;
     }
     switch (logn) {
@@ -1368,8 +1387,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
         case 9: launch_it<9>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         case 10: launch_it<10>(op, extP, T, blocks, L, K, lazy, primes, s, false, 0, qbits, share_np); break;
         case 11: launch_it<11>(op, extP, T, blocks, L, K, lazy, primes, s); break;
-        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np); break;
-        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np); break;
+        case 12: launch_it<12>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np, lazy_out); break;
+        case 13: launch_it<13>(op, extP, T, blocks, L, K, lazy, primes, s, asm_inv, 0, qbits, share_np, lazy_out); break;
         case 14: launch_it<14>(op, extP, T, blocks, L, K, lazy, primes, s); break;
         default: break;
     }

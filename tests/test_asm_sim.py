@@ -26,6 +26,12 @@ def test_rounds_match_exact_arithmetic():
                     asm_sim.check_inv_round(logn, r, q, rng, approx)
                     asm_sim.check_round_pinned(logn, r, q, rng, approx)
                     asm_sim.check_inv_round_pinned(logn, r, q, rng, approx)
+            # the tensor kernels' last round: outputs congruent and below 2q (bound_out = 2)
+            r = (logn + 3) // 4 - 1
+            for i in range(15):
+                q = asm_sim.PRIMES[i % len(asm_sim.PRIMES)]
+                asm_sim.check_inv_round(logn, r, q, rng, approx, lazy_out=True)
+                asm_sim.check_inv_round_pinned(logn, r, q, rng, approx, lazy_out=True)
 
 
 def test_generic_rounds_match_exact_arithmetic():

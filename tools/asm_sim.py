@@ -204,9 +204,9 @@ def check_round(logn, r, q, rng, approx=True, generic=False, qbits=60):
             assert got[k] < rd.bound_out * q, ("bound", logn, r, k, got[k] / q)
 
 
-def check_inv_round(logn, r, q, rng, approx=True, generic=False, qbits=60):
+def check_inv_round(logn, r, q, rng, approx=True, generic=False, qbits=60, lazy_out=False):
     rd = G.inv_rounds(logn, approx, generic, qbits)[r]
-    rd = G.InvRound(logn, r, rd.bound_in, approx, generic, qbits)
+    rd = G.InvRound(logn, r, rd.bound_in, approx, generic, qbits, lazy_out=lazy_out)
     seq = rd.gen()
     x = _inputs(rng, rd.bound_in * q)
     tw = [rng.randrange(q) for _ in range(15)]
@@ -258,9 +258,9 @@ def check_round_pinned(logn, r, q, rng, approx=True):
         assert got[k] < (q if rd.last else rd.bound_out * q), ("pinned fwd bound", logn, r, k, got[k] / q)
 
 
-def check_inv_round_pinned(logn, r, q, rng, approx=True):
+def check_inv_round_pinned(logn, r, q, rng, approx=True, lazy_out=False):
     b = G.inv_rounds_pinned(logn, approx)[r].bound_in
-    rd = G.InvRoundPinned(logn, r, b, approx)
+    rd = G.InvRoundPinned(logn, r, b, approx, lazy_out=lazy_out)
     x = _inputs(rng, b * q)
     tw = [rng.randrange(q) for _ in range(15)]
     got, n_inv, last_w = _run_pinned(rd, x, tw, q, logn)

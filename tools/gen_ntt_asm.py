@@ -482,9 +482,13 @@ class InvRound(Statement):
     """One inverse round (Gentleman-Sande, stage bits BLO..BHI ascending) as one asm statement.
     bound_in: every input value < bound_in * q."""
 
-    def __init__(self, logn, r, bound_in, approx=True, generic=False, qbits=60):
+    def __init__(self, logn, r, bound_in, approx=True, generic=False, qbits=60, lazy_out=False):
         super().__init__()
         self.logn, self.r, self.approx = logn, r, approx
+        # lazy_out (the last round of the tensor kernels' inverse): the final stage's exact Shoup
+        # products are left in [0, 2q) (every consumer of the tensor's output takes them:
+        # DESIGN.md §6.4), one 64-bit move instead of the 5-instruction canonical reduction
+        self.lazy_out = lazy_out
         # qbits < 60 (generic, q < 2^qbits): sums may reach 2^64 / 2^qbits q before a halving
         self.qbits = qbits
         self.cap = 16 if qbits >= 60 else (1 << (64 - qbits))
@@ -644,10 +648,13 @@ class InvRound(Statement):
                             wn, sn = ("lw", "ls") if w == "l" else ("ni", "ns")
                             s += shoup_seq(self, lo(y), hi(y), self.kc(wn + "l"), self.kc(wn + "h"),
                                            self.kc(sn + "l"), self.kc(sn + "h"), ex, c, False)
-                            s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
+                            if self.lazy_out:
+                                s.append(Ins(f"v_lshl_add_u64 {dst}, {ex['E']}, 0, 0"))
+                            else:
+                                s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
                         released += [p for p in {S, loc[k1]} if p is not None]
                         loc[k0] = loc[k1] = None
-                        bnd[k0] = bnd[k1] = 1
+                        bnd[k0] = bnd[k1] = 2 if self.lazy_out else 1
                     streams.append(s)
                 seq += interleave(streams)
                 free.extend(int(lo(p)[1:]) for p in released)
@@ -658,7 +665,7 @@ class InvRound(Statement):
     def emit(self):
         seq = self.gen()
         struct = f"InvRoundGenAsm<{self.logn}, {self.r}, {self.qbits}>" if self.generic else \
-            f"InvRoundAsm<{self.logn}, {self.r}>"
+            f"InvRoundAsm<{self.logn}, {self.r}, true>" if self.lazy_out else f"InvRoundAsm<{self.logn}, {self.r}>"
         return emit_statement(struct, self, seq, self.vmax,
                               f"round {self.r} of the {1 << self.logn}-point inverse NTT"
                               f"{f' for any prime below 2^{self.qbits}' if self.generic else ''}: stage bits "
@@ -721,8 +728,11 @@ class InvRoundPinned(InvRound):
                             wn, sn = ("lw", "ls") if w == "l" else ("ni", "ns")
                             s += shoup_seq(self, lo(y), hi(y), self.kc(wn + "l"), self.kc(wn + "h"),
                                            self.kc(sn + "l"), self.kc(sn + "h"), ex, c, False)
-                            s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
-                        bnd[k0] = bnd[k1] = 1
+                            if self.lazy_out:
+                                s.append(Ins(f"v_lshl_add_u64 {dst}, {ex['E']}, 0, 0"))
+                            else:
+                                s += canon_seq(self, dst, ex["E"], ex["B"], ex["F"])
+                        bnd[k0] = bnd[k1] = 2 if self.lazy_out else 1
                     streams.append(s)
                 seq += interleave(streams)
         self.bound_out = max(bnd.values())
@@ -730,7 +740,7 @@ class InvRoundPinned(InvRound):
 
     def emit(self):
         seq = self.gen()
-        return emit_pinned(f"EXACTO_INV_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
+        return emit_pinned(f"EXACTO_INV_PIN_{self.logn}_{self.r}{'_LZ' if self.lazy_out else ''}", self, seq, self.vmax,
                            f"round {self.r} of the {1 << self.logn}-point inverse NTT, pinned homes: stage "
                            f"bits {self.blo}..{self.bhi}, inputs < {self.bound_in}q, outputs < {self.bound_out}q")
 
@@ -888,7 +898,7 @@ __device__ __forceinline__ AsmK make_asmk_inv_mont(const PrimeConst& P) {
 }
 
 template <int LOGN, int R> struct FwdRoundAsm;
-template <int LOGN, int R> struct InvRoundAsm;
+template <int LOGN, int R, bool LZ = false> struct InvRoundAsm;   // LZ: last round, outputs < 2q
 // any prime below 2^QB (the HPS primes; QB < 60: fewer reductions, the values' headroom is larger)
 template <int LOGN, int R, int QB = 60> struct InvRoundGenAsm;
 template <int LOGN, int R, int QB = 60> struct FwdRoundGenAsm;
@@ -911,6 +921,9 @@ def main():
         for rd in inv_rounds(logn, approx):
             parts.append(InvRound(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
+        rd = inv_rounds(logn, approx)[-1]   # the tensor kernels' last round, outputs in [0, 2q)
+        parts.append(InvRound(logn, rd.r, rd.bound_in, approx, lazy_out=True).emit())
+        parts.append("\n")
         for rd in inv_rounds(logn, approx, generic=True):
             parts.append(InvRound(logn, rd.r, rd.bound_in, approx, generic=True).emit())
             parts.append("\n")
@@ -920,6 +933,9 @@ def main():
         for rd in inv_rounds_pinned(logn, approx):
             parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
+        rd = inv_rounds_pinned(logn, approx)[-1]
+        parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx, lazy_out=True).emit())
+        parts.append("\n")
     for logn in GEN_LOGN:   # the generic-prime forward rounds (and n = 1024's inverse rounds)
         for rd in fwd_rounds(logn, approx, addx, generic=True):
             parts.append(rd.emit())
