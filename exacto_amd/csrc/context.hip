@@ -1173,15 +1173,22 @@ static int run_ntt_fwd2(exacto_ctx* c, const NttBatch& nb1, long count1, const N
     return run_ntt(c, nb2, count2, false);
 }
 
+// the tensor runs the asm kernels (products by MulNear60*Asm, special-prime inverse rounds)
+static bool tensor_asm(const exacto_ctx* c) {
+    bool near60 = c->ntt_asm && c->ntt_asm_inv;
+    for (int t = 0; t < c->L + c->K; ++t)   // the fused product needs d = 2^60 - q < 2^24
+        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
+    return near60;
+}
+
 static int run_inv_tensor(exacto_ctx* c, const Operands& o, int cnt, bool p2only = false) {
     const int NP = c->L + c->K;
-    bool lazy = true, near60 = c->ntt_asm && c->ntt_asm_inv;
+    bool lazy = true;
+    const bool near60 = tensor_asm(c);
     int qbits = 0;
     for (int t = 0; t < NP; ++t) {
         qbits = std::max(qbits, 64 - __builtin_clzll(c->primes[t]));
         lazy &= c->primes[t] < (1ull << 60);
-        // the fused product (mulmod_near60) needs d = 2^60 - q < 2^24; the asm rounds d < 2^32
-        near60 &= c->primes[t] < (1ull << 60) && c->primes[t] > (1ull << 60) - (1ull << 24);
     }
     // algorithmic bytes per (item, prime): the four operands a0, a1, b0, b1 in and the three
     // components out (7 polys); psum's auxiliary primes only c2 = a1 b1 (2 in, 1 out).  dBFV with
@@ -1496,8 +1503,11 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                                   crt_mode(c), c->stream);
             }
             CHECK_LAUNCH();
-            // 3. forward NTT of the extended polynomials
-            if (int e = run_ntt(c, contiguous(c->ws_extP, cnt, 4L * K, L, K, n), (long)cnt * 4 * K, false)) return e;
+            // 3. forward NTT of the extended polynomials (exact path with the asm tensor, its only
+            // reader: outputs left in [0, 2q), which its products take)
+            NttBatch eb = contiguous(c->ws_extP, cnt, 4L * K, L, K, n);
+            eb.lazy_out = c->path != EXACTO_PATH_HPS && tensor_asm(c);
+            if (int e = run_ntt(c, eb, (long)cnt * 4 * K, false)) return e;
         } else {
             o.ea_off += s;
             o.eb_off += s;

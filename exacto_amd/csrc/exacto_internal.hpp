@@ -22,6 +22,9 @@ struct NttBatch {
     // src16 + item * src16_item_stride + (sub / period) * n, converted to residues mod its prime
     const int16_t* src16;
     long src16_item_stride;
+    // forward, pinned kernels only: outputs in [0, 2q) (set only for the exact path's extension
+    // transforms, whose sole reader is the asm tensor product: MulPair takes operands below 2^61)
+    int lazy_out;
 };
 
 enum class MulPath : int { Exact = 0, Hps = 1 };

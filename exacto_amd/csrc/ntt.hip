@@ -563,7 +563,8 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
 
 // The forward rounds over the pinned homes (canonical inputs, element tid + k T; canonical outputs,
 // element 16 tid + k): fwd_rounds_asm's twiddles and exchanges.
-#define PIN_FWD_ROUNDS(LOGN_, lds_, tid_, tab_, K_)                                              \
+// SFX_: empty, or _LZ for the last round with outputs in [0, 2q) (NttBatch::lazy_out)
+#define PIN_FWD_ROUNDS(LOGN_, lds_, tid_, tab_, K_, SFX_)                                        \
     {                                                                                            \
         const AsmK pin_K = (K_);                                                                 \
         const TwTab pin_tab = (tab_);                                                            \
@@ -583,13 +584,13 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
             TwPair tw[15];                                                                       \
             load_round_tw<LOGN_, pin_lo, LOGN_ - 9, pin_lo>(tw, tid_, pin_tab);                  \
             PIN_EXCHANGE(lds_, tid_, LOGN_ - 8, pin_lo)                                          \
-            if constexpr (LOGN_ == 12) EXACTO_FWD_PIN_12_2(tw, pin_K); else EXACTO_FWD_PIN_13_2(tw, pin_K); \
+            if constexpr (LOGN_ == 12) EXACTO_FWD_PIN_12_2##SFX_(tw, pin_K); else EXACTO_FWD_PIN_13_2(tw, pin_K); \
         }                                                                                        \
         if constexpr (LOGN_ == 13) {                                                             \
             TwPair tw[15];                                                                       \
             load_round_tw<13, 0, 0, 0>(tw, tid_, pin_tab);                                       \
             PIN_EXCHANGE(lds_, tid_, 1, 0)                                                       \
-            EXACTO_FWD_PIN_13_3(tw, pin_K);                                                      \
+            EXACTO_FWD_PIN_13_3##SFX_(tw, pin_K);                                                \
         }                                                                                        \
     }
 
@@ -694,7 +695,7 @@ ntt_inv_gen_kernel(NttBatch nb, const PrimeConst* __restrict__ primes) {
 // nb2 / split: blocks from `split` on transform a second batch (nb2, block - split): one launch for
 // two batches of the same transform size (a dBFV chain step's output limbs and the next step's
 // extension)
-template <int LOGN, int PROBE = 0>
+template <int LOGN, int PROBE = 0, bool LZO = false>
 __global__ void __launch_bounds__((1 << LOGN) / 16) __attribute__((amdgpu_waves_per_eu(4)))
 ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch nb2 = NttBatch{},
                    int split = 0x7fffffff) {
@@ -737,8 +738,10 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
         PIN_EXCHANGE(lds, tid, LOGN - 4, LOGN - 8)
         PIN_EXCHANGE(lds, tid, LOGN - 8, LOGN == 12 ? 0 : 1)
         if constexpr (LOGN == 13) PIN_EXCHANGE(lds, tid, 1, 0)
+    } else if constexpr (LZO) {
+        PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q), _LZ)
     } else {
-        PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q))
+        PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q), )
     }
     // canonical, evaluation 16 tid + k -> position tid + k T (store_evals' order)
     if constexpr (PROBE == 1) {
@@ -1410,8 +1413,13 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
     // non-pinned asm kernels and the persistent LDS-DMA forward kernel measured slower and were removed,
     // DESIGN.md §6)
     if (asm_fwd && !inverse && (logn == 12 || logn == 13)) {
-        if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        if (nb.lazy_out) {
+            if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12, 0, true>), dim3(count), dim3(256), 0, s, nb, primes);
+            else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 0, true>), dim3(count), dim3(512), 0, s, nb, primes);
+        } else {
+            if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+            else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        }
         return;
     }
     if (asm_inv && inverse && (logn == 12 || logn == 13)) {

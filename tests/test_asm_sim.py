@@ -32,6 +32,7 @@ def test_rounds_match_exact_arithmetic():
                 q = asm_sim.PRIMES[i % len(asm_sim.PRIMES)]
                 asm_sim.check_inv_round(logn, r, q, rng, approx, lazy_out=True)
                 asm_sim.check_inv_round_pinned(logn, r, q, rng, approx, lazy_out=True)
+                asm_sim.check_round_pinned(logn, r, q, rng, approx, lazy_out=True)
 
 
 def test_generic_rounds_match_exact_arithmetic():
@@ -66,6 +67,7 @@ def test_tensor_products_match_exact_arithmetic():
     for i in range(2000):
         for w in (1, 2):
             asm_sim.check_mulpair(w, asm_sim.PRIMES[i % 4], rng)
+            asm_sim.check_mulpair(w, asm_sim.PRIMES[i % 4], rng, bound=2)   # lazy extension operands
 
 
 def test_committed_inc_is_current(tmp_path):

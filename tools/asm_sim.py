@@ -242,8 +242,8 @@ def _run_pinned(rd, x, tw, q, logn):
     return got, n_inv, last_w
 
 
-def check_round_pinned(logn, r, q, rng, approx=True):
-    rd = G.Round(logn, r, approx, True, pinned=True)
+def check_round_pinned(logn, r, q, rng, approx=True, lazy_out=False):
+    rd = G.Round(logn, r, approx, True, pinned=True, lazy_out=lazy_out)
     bound_in = q if r == 0 else 16 * q
     x = _inputs(rng, bound_in)
     tw = [rng.randrange(q) for _ in range(15)]
@@ -255,7 +255,8 @@ def check_round_pinned(logn, r, q, rng, approx=True):
             want[k0], want[k1] = (want[k0] + t) % q, (want[k0] - t) % q
     for k in range(16):
         assert got[k] % q == want[k], ("pinned fwd", logn, r, k)
-        assert got[k] < (q if rd.last else rd.bound_out * q), ("pinned fwd bound", logn, r, k, got[k] / q)
+        assert got[k] < ((2 if lazy_out else 1) * q if rd.last else rd.bound_out * q), \
+            ("pinned fwd bound", logn, r, k, got[k] / q)
 
 
 def check_inv_round_pinned(logn, r, q, rng, approx=True, lazy_out=False):
@@ -277,17 +278,19 @@ def check_inv_round_pinned(logn, r, q, rng, approx=True, lazy_out=False):
         assert got[k] < rd.bound_out * q, ("pinned inv bound", logn, r, k, got[k] / q)
 
 
-def check_mulpair(w, q, rng):
-    """MulNear60Asm<w>: r_k == a_k b_k (mod q) and r_k < 2q for a_k, b_k < q (extremes included)."""
+def check_mulpair(w, q, rng, bound=1):
+    """MulNear60Asm<w>: r_k == a_k b_k (mod q) and r_k < 2q for a_k, b_k < bound q (extremes
+    included; bound 2: the extension transforms' lazy outputs)."""
     st = G.MulPair(w)
     seq = st.gen()
     d = (1 << 60) - q
     vals = []
+    top = bound * q
     for k in range(w):
         if rng.random() < 0.3:
-            a, b = q - 1 - rng.randrange(3), q - 1 - rng.randrange(3)
+            a, b = top - 1 - rng.randrange(3), top - 1 - rng.randrange(3)
         else:
-            a, b = rng.randrange(q), rng.randrange(q)
+            a, b = rng.randrange(top), rng.randrange(top)
         vals.append((a, b))
     named = {"d": [d, 32], "e": [16 * d, 32]}
     for k, (a, b) in enumerate(vals):

@@ -300,9 +300,13 @@ def emit_pinned(name, st, seq, vmax, comment):
 class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
-    def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False, qbits=60, bound_in=None):
+    def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False, qbits=60, bound_in=None,
+                 lazy_out=False):
         super().__init__()
         self.logn, self.r, self.approx, self.addx, self.pinned = logn, r, approx, addx, pinned
+        # lazy_out (last round, special primes: the extension transforms that only the asm tensor
+        # products read): the final values are left in [0, 2q) after the fold, no canonical step
+        self.lazy_out = lazy_out
         # generic: any prime q < 2^60 (the HPS primes): the round-start reduction of X from < 16q to
         # < 2q is three conditional subtractions (8q, 4q, 2q; halve_seq) instead of the special-prime
         # fold, and the final canonical reduction a chain of them down to q.
@@ -458,14 +462,18 @@ class Round(Statement):
                         streams[j].append(Ins(f"v_lshl_add_u64 {xop[k]}, {R}, 0, 0"))
                     continue
                 streams[j] += reduce_seq(self, R, R, v(P[k] + 1), v(t["B"]), v(t["B"] + 1))
-                streams[j] += canon_seq(self, xop[k], R, vp(t["E"]), vp(t["F"]))
+                if not self.lazy_out:
+                    streams[j] += canon_seq(self, xop[k], R, vp(t["E"]), vp(t["F"]))
+                elif xop[k] != R:
+                    streams[j].append(Ins(f"v_lshl_add_u64 {xop[k]}, {R}, 0, 0"))
             seq += interleave(streams)
         return seq
 
     def emit(self):
         seq = self.gen()
         if self.pinned:
-            return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}", self, seq, self.vmax,
+            return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}{'_LZ' if self.lazy_out else ''}", self, seq,
+                               self.vmax,
                                f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes: "
                                f"stage bits {self.bhi}..{self.lo}")
         struct = f"FwdRoundGenAsm<{self.logn}, {self.r}, {self.qbits}>" if self.generic else \
@@ -930,6 +938,9 @@ def main():
         for r in range((logn + 3) // 4):
             parts.append(Round(logn, r, approx, True, pinned=True).emit())
             parts.append("\n")
+        # the extension transforms' last round, outputs in [0, 2q)
+        parts.append(Round(logn, (logn + 3) // 4 - 1, approx, True, pinned=True, lazy_out=True).emit())
+        parts.append("\n")
         for rd in inv_rounds_pinned(logn, approx):
             parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
