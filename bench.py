@@ -44,6 +44,7 @@ Also reported on the same JSON line:
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import math
 import os
@@ -131,54 +132,6 @@ def relaunch(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
-def _near60(q, bits=32):
-    return (1 << 60) - (1 << bits) < q < (1 << 60)
-
-
-def kernel_names(n, L, S, cfg, env=os.environ):
-    """Kernel (template instance) behind each profiled family for this configuration, as rocprofv3
-    names it (context.hip / ntt.hip launch choices)."""
-    logn = n.bit_length() - 1
-    on = lambda k: env.get(k, "1") != "0"
-    _, moduli, aux, *_ = CONFIGS[cfg]
-    gen = logn in (10, 12, 13) and on("EXACTO_NTT_GEN")   # generated generic-prime rounds
-    if aux:   # HPS: generic kernels for the primes outside (2^60 - 2^32, 2^60)
-        primes = list(moduli) + list(aux)
-        lazy = max(primes) < (1 << 60)
-        # the smaller-prime instances (ntt.hip gen_qb): compact_bfv's primes below 2^50 at n = 1024,
-        # u64_dbfv's auxiliary primes below 2^56 at n = 4096 (the transform batches hold only those)
-        qb = {10: 50, 12: 56}.get(logn, 60) if on("EXACTO_NTT_GENQ") else 60
-        qsmall = qb if max(aux) < (1 << qb) else 60
-        if gen and lazy:
-            gfwd, ginv = f"ntt_fwd_gen_kernel<{logn}, {qsmall}>", f"ntt_inv_gen_kernel<{logn}, {qsmall}>"
-        else:
-            gfwd, ginv = f"ntt_fwd_kernel<{logn}, true>", f"ntt_inv_kernel<{logn}, true>"
-        near_q = logn in (12, 13) and _near60(moduli[0]) and on("EXACTO_NTT_ASM")
-        fwd = f"ntt_fwd_pin_kernel<{logn}> + {gfwd}" if near_q else gfwd
-        inv = f"ntt_inv_pin_kernel<{logn}> + {ginv}" if near_q else ginv
-        tq = qb if max(primes) < (1 << qb) else 60
-        tensor = (f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true, {tq}>" if gen and lazy else
-                  f"ntt_inv_tensor_kernel<{logn}, {'true' if lazy else 'false'}, false>")
-        return {0: fwd, 1: inv, 2: tensor, 12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel",
-                14: "hps_extend_kernel", 15: "relin_mac_lds_kernel", 16: "hps_scale_kernel<true, *>"}
-    asm = logn in (12, 13) and on("EXACTO_NTT_ASM")
-    gfwd = f"ntt_fwd_gen_kernel<{logn}, 60>" if gen else f"ntt_fwd_kernel<{logn}, true>"
-    ginv = f"ntt_inv_gen_kernel<{logn}, 60>" if gen else f"ntt_inv_kernel<{logn}, true>"
-    fwd = f"ntt_fwd_pin_kernel<{logn}>" if asm else gfwd
-    inv = f"ntt_inv_pin_kernel<{logn}>" if asm and on("EXACTO_NTT_ASM_INV") else ginv
-    tp = env.get("EXACTO_TENSOR_PIN", "")
-    pin = asm and on("EXACTO_NTT_ASM_INV") and (tp != "0" if tp else logn == 13)
-    if asm and on("EXACTO_NTT_ASM_INV"):
-        tensor = f"ntt_inv_tensor_pin_kernel<{logn}>" if pin else f"ntt_inv_tensor_kernel<{logn}, true, true>"
-    else:
-        tensor = f"ntt_inv_tensor_kernel<{logn}, true, false, 0, true, 60>" if gen else f"ntt_inv_tensor_kernel<{logn}, true, false>"
-    polymul = f"ntt_polymul_kernel<{logn}>"
-    return {0: fwd, 1: inv, 2: tensor, 3: polymul, 4: f"exact_lift_sp_kernel<{L}>",
-            5: f"exact_scale_sp_kernel<{L}, *>", 6: f"ks32_digit_ntt_kernel<{logn}, *>", 7: "ks32_mac_kernel<*>",
-            8: f"ks32_crt_kernel<{logn}, {S}>", 9: "dbfv_pairsum_kernel", 10: f"exact_psum_sp_kernel<{L}>",
-            12: "ks32_digit_sum_kernel", 13: "dbfv_combine_kernel"}
-
-
 def _entry(rec, name, share=None):
     ms, nl, by = rec["ms"], max(rec["launches"], 1), rec["bytes"]
     achieved = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
@@ -208,8 +161,10 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
         step_one()
     torch.cuda.synchronize()
     recs = {k: ctx.prof_read(k) for k in KINDS}
+    # what actually ran, as the library recorded it at launch (exacto_prof_kernels: the rocprofv3 names)
+    ran = {k: ctx.prof_kernels(k) for k in KINDS}
     ctx.prof_enable(False)
-    names = kernel_names(n, L, S, cfg)
+    names = {k: " + ".join(nm for nm, _, _ in v) for k, v in ran.items() if v}
     total = sum(r["ms"] for r in recs.values())
     table = {KINDS[k]: _entry(r, names.get(k, KINDS[k]), r["ms"] / total if total else 0.0)
              for k, r in recs.items() if r["launches"]}
@@ -220,11 +175,13 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     roof["traffic"] = None
     # HBM bytes per launch from the committed PMC passes over this bench configuration
     # (tools/pmc_traffic.sh: 2*FETCH_SIZE + WRITE_SIZE per dispatch with the gfx950 corrections)
+    top_kernel = roof["kernel"].split(" + ")[0]
     tfile = _latest_profile(f"{cfg}_traffic.json")
     if tfile:
         with open(tfile) as f:
             tr = json.load(f).get("kernels", {})
-        hit = [v for k, v in tr.items() if roof["kernel"].split("<")[0] in k]
+        hit = [v for k, v in tr.items() if k == top_kernel] or \
+              [v for k, v in tr.items() if top_kernel.split("<")[0] in k]
         if hit:
             roof["traffic"] = round(hit[0]["traffic_bytes_avg"], 1)
             roof["traffic_over_algorithmic"] = round(hit[0]["traffic_bytes_avg"] / roof["bytes_per_launch"], 4)
@@ -236,7 +193,8 @@ def roofline_block(ctx, step_one, cfg, n, L, S, batches=3):
     if vfile:
         with open(vfile) as f:
             vc = json.load(f).get("kernels", {})
-        hit = [v for k, v in vc.items() if roof["kernel"].split("<")[0] in k]
+        hit = [v for k, v in vc.items() if k == top_kernel] or \
+              [v for k, v in vc.items() if top_kernel.split("<")[0] in k]
         if hit:
             v = hit[0]
             need = v["valu_insts"] * 4.4 / 1024.0
@@ -393,14 +351,22 @@ def main():
         print("bench.py: --split limbs needs a dBFV config (cfg4, cfg5, u64dbfv)", file=sys.stderr)
         sys.exit(2)
     distributed = world > 1
+    # deadline per phase of a multi-rank run: a rank that never joins a collective ends the job with a
+    # diagnostic line instead of blocking it until the driver's time limit (exacto_amd.dist.Watchdog;
+    # torch.distributed's own timeout and the library's RCCL deadlines, EXACTO_RCCL_TIMEOUT_S, likewise)
+    wd = xdist.Watchdog(rank, enabled=distributed, withhold_ok=args.dry)
+    # (torch's own collective timeout a minute later: the watchdog names the phase first)
+    pg_timeout = datetime.timedelta(seconds=xdist.deadline_s() + 60.0)
+    if distributed:
+        wd.arm("init")
     if args.dry:
         device = torch.device("cpu")
         if distributed:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
     else:
         if distributed:
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
         device = torch.device("cuda", local)
         torch.cuda.set_device(device)
     backend = dist.get_backend() if distributed else None
@@ -438,10 +404,13 @@ def main():
     # resident key (ncclBroadcast over xGMI)
     key_collective = None
     comm, rccl_nranks = None, None
+    if distributed:
+        wd.arm("comm_init" if not args.dry else "key_broadcast")
     if distributed and not args.dry:
         # the library's own RCCL communicator; ncclCommCount on the line shows RCCL spans every rank
         comm = xdist.rccl_comm_for(ctx, local)
         rccl_nranks = comm.count()
+        wd.arm("key_broadcast")
     if args.config != "cfg2":
         kgen = torch.Generator(device=device)
         kgen.manual_seed(0xE7AC7003)
@@ -457,6 +426,7 @@ def main():
                 ctx.load_relin_key_dev(rlk, G)
             if distributed:
                 ctx.broadcast_relin_key(comm, 0, G)
+                ctx.rccl_sync(comm)   # the broadcast's completion, with the library's deadline
                 key_collective = "exacto_ctx_broadcast_relin_key (ncclBroadcast, library RCCL communicator)"
             sync()
 
@@ -580,11 +550,14 @@ def main():
         metric = "ciphertext muls/sec (dbfv_mul)" if depth == 1 else f"dbfv_mul chains/sec (depth {depth})"
     sync()
 
+    if distributed:
+        wd.arm("warmup")
     for w in range(args.warmup):
         one(w % nbuf)
     sync()
     # batches per step: the K timed steps last >= --min-time (the slowest rank decides)
     reps = args.reps
+    per = 0.0
     if reps <= 0:
         t0 = time.perf_counter()
         for i in range(nbuf):
@@ -599,6 +572,8 @@ def main():
             one(r % nbuf)
 
     if distributed:
+        # the timed region: one deadline plus ten times its expected length
+        wd.arm("timed", xdist.deadline_s() + 10.0 * args.steps * reps * per)
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -614,6 +589,8 @@ def main():
     units_per_step = B * reps
     total_units = (world if args.split == "batch" else 1) * units_per_step * args.steps
     value = total_units / elapsed
+    if distributed:
+        wd.arm("report")
 
     dry_check = None
     if args.dry and args.split == "limbs":
@@ -701,6 +678,7 @@ def main():
             sync()
             comm.close()
         dist.destroy_process_group()
+        wd.disarm()
 
 
 if __name__ == "__main__":

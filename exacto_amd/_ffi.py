@@ -29,13 +29,16 @@ class ExactoError(Exception):
         self.variant = VARIANTS[code - 1] if 1 <= code <= 9 else "HipError"
 
 
+NTT_ORDER = 1   # exacto_hip.h EXACTO_NTT_ORDER: evaluation k at (k mod 16) n/16 + k/16
+
+
 class CtxInfo(C.Structure):
     _fields_ = [("ring_degree", C.c_size_t), ("num_ct_moduli", C.c_size_t),
                 ("num_aux_moduli", C.c_size_t), ("num_internal_aux", C.c_size_t),
                 ("gadget_digits", C.c_size_t), ("gadget_base", C.c_uint64),
                 ("plain_modulus", C.c_uint64), ("mul_path", C.c_int), ("device", C.c_int),
                 ("ks32_primes", C.c_int), ("psum_max", C.c_int),
-                ("ks32_lazy", C.c_int)]
+                ("ks32_lazy", C.c_int), ("ntt_order", C.c_int), ("dbfv_key_switch", C.c_int)]
 
 
 _lib = None
@@ -138,10 +141,12 @@ _SIGS = [
     ("exacto_ctx_broadcast_relin_key", [_P, _P, C.c_int, _SZ], C.c_int),
     ("exacto_broadcast_galois_key", [_P, _P, C.c_int, _P, _SZ], C.c_int),
     ("exacto_rccl_allgather_u64", [_P, _P, _P, _P, _SZ], C.c_int),
+    ("exacto_rccl_sync", [_P, _P], C.c_int),
     ("exacto_last_error", [C.c_char_p, _SZ], _SZ),
     ("exacto_prof_enable", [_P, C.c_int], C.c_int),
     ("exacto_prof_read", [_P, C.c_int, C.POINTER(_U64), C.POINTER(C.c_double),
                           C.POINTER(C.c_double), C.POINTER(_U64)], C.c_int),
+    ("exacto_prof_kernels", [_P, C.c_int, C.c_char_p, _SZ], _SZ),
     ("exacto_version", [], C.c_char_p),
 ]
 
@@ -301,6 +306,10 @@ class HipContext:
         self.psum_max = info.psum_max
         self.ct_moduli = [int(q) for q in ct_moduli]
         self.plain_modulus = int(info.plain_modulus)
+        # the NTT-domain storage order this binding was written for (exacto_hip.h EXACTO_NTT_ORDER): keys and
+        # ciphertexts kept from a library of another order would give wrong results silently
+        if info.ntt_order != NTT_ORDER:
+            raise RuntimeError(f"libexacto_hip uses NTT-domain order {info.ntt_order}, this binding expects {NTT_ORDER}")
 
     @property
     def ks32_lazy(self) -> bool:
@@ -308,6 +317,14 @@ class HipContext:
         info = CtxInfo()
         check(self._lib.exacto_ctx_get_info(self._h, C.byref(info)))
         return bool(info.ks32_lazy)
+
+    @property
+    def dbfv_key_switch(self) -> int:
+        """The last dbfv_mul's key switch: 1 summed digits (primary 31-bit basis), 2 summed (wide basis),
+        0 per product, -1 none yet (exacto_ctx_info.dbfv_key_switch)."""
+        info = CtxInfo()
+        check(self._lib.exacto_ctx_get_info(self._h, C.byref(info)))
+        return int(info.dbfv_key_switch)
 
     @classmethod
     def from_params(cls, params, device=0):
@@ -745,6 +762,11 @@ class HipContext:
         """recv = [nranks][count] u64 (ncclAllGather on the context stream)."""
         check(self._lib.exacto_rccl_allgather_u64(self._h, comm.handle, self._p(send), self._p(recv), count))
 
+    def rccl_sync(self, comm: "RcclComm"):
+        """Wait for the collectives on the context stream, at most $EXACTO_RCCL_TIMEOUT_S seconds
+        (exacto_rccl_sync); raises ExactoError on expiry (the communicator is then aborted)."""
+        check(self._lib.exacto_rccl_sync(self._h, comm.handle))
+
     def dbfv_mul_chain_dev(self, d, base, plain, x, y, out, batch, depth):
         check(self._lib.exacto_dbfv_mul_chain_dev(self._h, d, base, plain, self._p(x), self._p(y),
                                                   self._p(out), batch, depth))
@@ -766,3 +788,16 @@ class HipContext:
         check(self._lib.exacto_prof_read(self._h, kind, C.byref(nl), C.byref(ms), C.byref(by),
                                          C.byref(pl)))
         return {"launches": nl.value, "ms": ms.value, "bytes": by.value, "polys": pl.value}
+
+    def prof_kernels(self, kind: int) -> list[tuple[str, int, float]]:
+        """The kernels that ran for family `kind` in the records prof_read consumed, as rocprofv3 names
+        them, by descending time: [(name, launches, ms)] (exacto_prof_kernels)."""
+        n = self._lib.exacto_prof_kernels(self._h, kind, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        self._lib.exacto_prof_kernels(self._h, kind, buf, n + 1)
+        out = []
+        for part in filter(None, buf.value.decode().split("; ")):
+            name, _, tail = part.rpartition(" (")
+            cnt, ms = tail.rstrip(")").split(", ")
+            out.append((name, int(cnt), float(ms.split()[0])))
+        return out

@@ -5,20 +5,29 @@
 // HBM, the exact-CRT tables, the resident relinearisation key and a chunked
 // workspace.  Every `_dev` entry point only enqueues kernels on the context stream.
 #include <algorithm>
+#include <cxxabi.h>
+#include <dlfcn.h>
+#include <chrono>
+#include <condition_variable>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/exacto_hip.h"
 #include "exacto_internal.hpp"
 
 using namespace exacto;
+
+thread_local const void* exacto::g_last_kernel = nullptr;
 
 // ============================================================== errors
 
@@ -176,6 +185,7 @@ struct ProfRec {
     hipEvent_t a, b;
     u64 polys;
     double bytes;
+    const void* kern;   // host handle of the last kernel launched inside the scope (EXACTO_LAUNCH)
 };
 
 // A 31-bit auxiliary basis of the ks32 key switch (ks32.hip) with its device tables and the
@@ -245,6 +255,8 @@ struct exacto_ctx {
     // S32 / d_p32 / d_tw32 / d_kst / ks32_sum_max / ks32_mac_form describe the active one.
     Ks32Basis kn, kz;
     bool ks32_lazy_active = false;
+    int ks32_need_m = 1;
+    int last_dbfv_ks = -1;        // exacto_ctx_info.dbfv_key_switch          // the most key-switch sums per output limb a dbfv_mul of this context asked for
     // a dBFV pass with shared extensions: d and its products per item (0: plain BFV products), for
     // run_inv_tensor's algorithmic bytes and the tensor kernels' prime-major block order
     int tensor_share_d = 0, tensor_share_npairs = 0;
@@ -363,6 +375,7 @@ struct exacto_ctx {
     // profiling
     bool prof = false;
     std::vector<ProfRec> recs;
+    std::map<int, std::map<const void*, std::pair<u64, double>>> prof_kern;   // kind -> kernel -> (launches, ms)
 };
 
 // EXACTO_DEBUG_ALLOC=1: every device allocation and release of the library is logged
@@ -1054,6 +1067,8 @@ extern "C" int exacto_ctx_get_info(const exacto_ctx* c, exacto_ctx_info* info) {
     info->ks32_primes = c->ks32 ? c->S32 : 0;
     info->psum_max = c->psum_env ? c->psum_max : 0;
     info->ks32_lazy = c->ks32 && c->ks32_lazy_active ? 1 : 0;
+    info->ntt_order = EXACTO_NTT_ORDER;
+    info->dbfv_key_switch = c->last_dbfv_ks;
     return 0;
 }
 
@@ -1132,12 +1147,15 @@ struct ProfScope {
     ProfScope(exacto_ctx* c_, int kind, u64 units, double bytes) : c(c_), on(c_->prof) {
         if (!on) return;
         rec.kind = kind; rec.polys = units; rec.bytes = bytes;
+        g_last_kernel = nullptr;
         if (hipEventCreate(&rec.a) != hipSuccess || hipEventCreate(&rec.b) != hipSuccess ||
             hipEventRecord(rec.a, c->stream) != hipSuccess)
             on = false;
     }
     ~ProfScope() {
-        if (on && hipEventRecord(rec.b, c->stream) == hipSuccess) c->recs.push_back(rec);
+        if (!on) return;
+        rec.kern = g_last_kernel;
+        if (hipEventRecord(rec.b, c->stream) == hipSuccess) c->recs.push_back(rec);
     }
 };
 
@@ -1395,7 +1413,9 @@ static int ks32_select_basis(exacto_ctx* c) {
         if (c->kz.P.cmp(bm) <= 0) break;
         sm = (int)m;
     }
-    if (sm >= 1) {
+    // never a basis that lifts fewer sums than the narrow one where those sums are needed (a dBFV digit
+    // sum the lazy basis cannot hold would otherwise drop to the per-product key switch)
+    if (sm >= 1 && sm >= std::min(c->kn.sum_max, std::max(1, c->ks32_need_m))) {
         c->kz.sum_max = sm;
         use_ks32_basis(c, c->kz);
     }
@@ -2114,6 +2134,11 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     const size_t gu = std::min<size_t>(c->G, c->rlk_keys);
     const int m = c->cached_sum_m;
     // the primary basis (narrow or lazy) and its sum_max depend on the resident key: decide first
+    if (m > c->ks32_need_m) {
+        c->ks32_need_m = m;
+        // a key already on the lazy basis that cannot lift these sums while the narrow one can: re-select
+        if (c->rs_valid && c->ks32_lazy_active && m > c->ks32_sum_max && m <= c->kn.sum_max) c->rs_valid = false;
+    }
     if (c->S32 > 0 && c->ks32 && c->rlk_loaded && gu > 0)
         if (int e = ensure_rs(c)) return e;
     const bool on = c->S32 > 0 && c->ks32 && m > 0 && c->digit16 && c->gbase <= 65536 &&
@@ -2121,6 +2146,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     const bool use_prim = on && m <= c->ks32_sum_max;
     const bool use_wide = on && !use_prim && c->kw.S > 0 && m <= c->kw.sum_max;
     const bool sum_ks = use_prim || use_wide;
+    c->last_dbfv_ks = use_prim ? 1 : use_wide ? 2 : 0;
     const int S = use_wide ? c->kw.S : c->S32;
     const Prime32* p32 = use_wide ? c->kw.d_p32 : c->d_p32;
     const Ks32Tables* kst = use_wide ? c->kw.d_kst : c->d_kst;
@@ -3687,6 +3713,11 @@ extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, dou
         HIP_TRY(hipEventElapsedTime(&t, r.a, r.b));
         ms += t; by += r.bytes; np += r.polys; ++nl;
         if (t > 0) rate.push_back(r.bytes / t);
+        if (r.kern) {
+            auto& k = c->prof_kern[kind][r.kern];
+            k.first += 1;
+            k.second += t;
+        }
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
     }
@@ -3709,6 +3740,47 @@ extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, dou
     return 0;
 }
 
+// The kernels behind one profiled family in the records exacto_prof_read consumed since the last
+// exacto_prof_kernels call for it, as rocprofv3 names them (the demangled kernel symbol without its
+// "void " and parameter list), by descending event time: "name (launches, ms); name (...)".  Returns
+// the length of the full text (like snprintf); buf may be NULL.  The list is cleared by the call.
+static std::string kernel_symbol_name(const void* handle) {
+    Dl_info info{};
+    if (!dladdr(handle, &info) || !info.dli_sname) return "?";
+    int st = 0;
+    char* dm = abi::__cxa_demangle(info.dli_sname, nullptr, nullptr, &st);
+    std::string nm = (st == 0 && dm) ? dm : info.dli_sname;
+    free(dm);
+    if (nm.rfind("void ", 0) == 0) nm = nm.substr(5);
+    int depth = 0;   // cut the parameter list: the first '(' outside template brackets
+    for (size_t i = 0; i < nm.size(); ++i) {
+        if (nm[i] == '<') ++depth;
+        else if (nm[i] == '>') --depth;
+        else if (nm[i] == '(' && depth == 0) { nm.resize(i); break; }
+    }
+    return nm;
+}
+
+extern "C" size_t exacto_prof_kernels(exacto_ctx* c, int kind, char* buf, size_t len) {
+    if (!c) return 0;
+    std::vector<std::pair<double, std::string>> v;
+    for (auto& kv : c->prof_kern[kind]) {
+        char tail[64];
+        snprintf(tail, sizeof tail, " (%llu, %.3f ms)", (unsigned long long)kv.second.first, kv.second.second);
+        v.emplace_back(kv.second.second, kernel_symbol_name(kv.first) + tail);
+    }
+    c->prof_kern.erase(kind);
+    std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    std::string out;
+    for (auto& e : v) out += (out.empty() ? "" : "; ") + e.second;
+    if (buf && len) {
+        const size_t k = std::min(len - 1, out.size());
+        std::memcpy(buf, out.data(), k);
+        buf[k] = 0;
+    }
+    return out.size();
+}
+
 // ============================================================== RCCL collectives
 //
 // Keys are made once and broadcast over xGMI to every GPU (the reference builds them on one host,
@@ -3718,7 +3790,6 @@ extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, dou
 // library has no link-time dependency on it.  Communicators are plain ncclComm_t handles, passed as
 // void*: made here (exacto_rccl_comm_init) or by the caller's own RCCL.
 
-#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 namespace {
@@ -3733,6 +3804,9 @@ struct Rccl {
     ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    // optional (deadline handling): a communicator whose collective missed its deadline is aborted
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*) = nullptr;
 };
 
 const Rccl& rccl() {
@@ -3755,6 +3829,8 @@ const Rccl& rccl() {
         sym(x.all_gather, "ncclAllGather");
         sym(x.error_string, "ncclGetErrorString");
         x.ok = all;
+        x.comm_abort = reinterpret_cast<decltype(x.comm_abort)>(dlsym(h, "ncclCommAbort"));
+        x.async_error = reinterpret_cast<decltype(x.async_error)>(dlsym(h, "ncclCommGetAsyncError"));
         if (!all) x.why = "RCCL library lacks a required symbol";
         return x;
     }();
@@ -3783,6 +3859,50 @@ extern "C" int exacto_rccl_unique_id(uint8_t* id) {
     return 0;
 }
 
+// Deadline of the blocking RCCL steps (communicator init, the agreement all-gather, exacto_rccl_sync):
+// $EXACTO_RCCL_TIMEOUT_S seconds (default 300; 0 = wait forever).  A rank that never joins makes the
+// others fail with EXACTO_ERR_HIP "RCCL error: ... timed out" instead of blocking their process for
+// good (the driver's 8-GPU run has one time limit for everything).
+static double rccl_timeout_s() {
+    const char* e = getenv("EXACTO_RCCL_TIMEOUT_S");
+    return e ? atof(e) : 300.0;
+}
+
+// Communicators aborted after a missed deadline: RCCL has freed them, so destroy must not touch them.
+static std::mutex g_aborted_mu;
+static std::set<void*> g_aborted;
+
+static int rccl_abort_timeout(void* comm, const std::string& what, double secs) {
+    if (rccl().comm_abort) {
+        (void)rccl().comm_abort((ncclComm_t)comm);
+        std::lock_guard<std::mutex> g(g_aborted_mu);
+        g_aborted.insert(comm);
+    }
+    return fail(EXACTO_ERR_HIP, "RCCL error: " + what + " timed out after " + std::to_string((int)secs) +
+                                    " s (a rank did not join); communicator aborted");
+}
+
+// Waits for the context stream (the collectives enqueued on it) with the deadline: polls hipStreamQuery
+// and the communicator's asynchronous error.  On expiry the communicator is aborted (RCCL then stops its
+// kernels) and the call fails; it never returns with a collective still blocking the stream silently.
+static int rccl_stream_wait(exacto_ctx* c, void* comm, const char* what) {
+    const double lim = rccl_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 0;; ++it) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return 0;
+        if (q != hipErrorNotReady) return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(q) + " (" + what + ")");
+        if (rccl().async_error) {
+            ncclResult_t ae = ncclSuccess;
+            if (rccl().async_error((ncclComm_t)comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+                return fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(ae) + " (" + what + ")");
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (lim > 0 && el > lim) return rccl_abort_timeout(comm, what, lim);
+        std::this_thread::sleep_for(std::chrono::microseconds(it < 100 ? 20 : 1000));
+    }
+}
+
 extern "C" int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id, int rank, int device) {
     if (!comm || !id) return invalid_param("null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return invalid_param("rank out of range");
@@ -3790,17 +3910,58 @@ extern "C" int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id,
     HIP_TRY(hipSetDevice(device));
     ncclUniqueId u;
     std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-    ncclComm_t cm = nullptr;
-    RCCL_TRY(rccl().comm_init_rank(&cm, nranks, u, rank));
-    *comm = cm;
+    // ncclCommInitRank blocks until every rank has joined: it runs on a helper thread so that the
+    // caller's wait has a deadline.  On expiry the helper is left behind (it holds only its own copy
+    // of the arguments) and the call fails; the caller is expected to end the process.
+    struct InitState {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false;
+        ncclResult_t r = ncclSuccess;
+        ncclComm_t cm = nullptr;
+    };
+    auto st = std::make_shared<InitState>();
+    std::thread([st, nranks, u, rank, device] {
+        (void)hipSetDevice(device);
+        ncclComm_t cm = nullptr;
+        const ncclResult_t r = rccl().comm_init_rank(&cm, nranks, u, rank);
+        std::lock_guard<std::mutex> g(st->mu);
+        st->r = r;
+        st->cm = cm;
+        st->done = true;
+        st->cv.notify_all();
+    }).detach();
+    const double lim = rccl_timeout_s();
+    std::unique_lock<std::mutex> lk(st->mu);
+    if (lim > 0) {
+        if (!st->cv.wait_for(lk, std::chrono::duration<double>(lim), [&] { return st->done; }))
+            return fail(EXACTO_ERR_HIP, "RCCL error: ncclCommInitRank timed out after " + std::to_string((int)lim) +
+                                            " s (a rank did not join)");
+    } else {
+        st->cv.wait(lk, [&] { return st->done; });
+    }
+    if (st->r != ncclSuccess)
+        return fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(st->r) + " (ncclCommInitRank)");
+    *comm = st->cm;
     return 0;
 }
 
 extern "C" int exacto_rccl_comm_destroy(void* comm) {
     if (!comm) return 0;
     if (int e = rccl_ready()) return e;
+    {
+        std::lock_guard<std::mutex> g(g_aborted_mu);
+        if (g_aborted.erase(comm)) return 0;   // freed by ncclCommAbort
+    }
     RCCL_TRY(rccl().comm_destroy((ncclComm_t)comm));
     return 0;
+}
+
+extern "C" int exacto_rccl_sync(exacto_ctx* c, void* comm) {
+    if (int e = check_ctx(c)) return e;
+    if (!comm) return invalid_param("null communicator");
+    if (int e = rccl_ready()) return e;
+    return rccl_stream_wait(c, comm, "collective on the context stream");
 }
 
 extern "C" int exacto_rccl_comm_count(void* comm, int* nranks) {
@@ -3851,12 +4012,13 @@ static int rccl_agree(exacto_ctx* c, void* comm, u64 mine, u64 ok, bool* agreed,
             rc = fail(EXACTO_ERR_HIP, std::string("RCCL error: ") + rccl().error_string(r) + " (ncclAllGather)");
         else if (hipMemcpyAsync(host.data() + 2, dev + 2, 2 * sizeof(u64) * nr, hipMemcpyDeviceToHost, c->stream) !=
                      hipSuccess ||
-                 hipStreamSynchronize(c->stream) != hipSuccess)
-            rc = fail(EXACTO_ERR_HIP, "HIP error: agreement header read-back");
+                 (rc = rccl_stream_wait(c, comm, "agreement all-gather")) != 0) {
+            if (!rc) rc = fail(EXACTO_ERR_HIP, "HIP error: agreement header read-back");
+        }
     }
+    if (rc) return rc;   // a timed-out all-gather may still own `dev`: leave it (the process is ending)
     (void)hipStreamSynchronize(c->stream);
     (void)hipFree(dev);
-    if (rc) return rc;
     for (int r = 0; r < nr; ++r) {
         if (!host[2 + 2 * r + 1]) {
             *why = "rank " + std::to_string(r) + " rejected the call";

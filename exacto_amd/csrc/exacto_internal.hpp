@@ -267,3 +267,16 @@ void launch_boot_key_map(const u64* s, u64* boot_coef, u64* s_pt, int n, u64 q, 
 void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, int L, const PrimeConst* primes,
                           hipStream_t s);
 }  // namespace exacto
+
+namespace exacto {
+// Every kernel launch of the library goes through EXACTO_LAUNCH, which records the launched kernel's
+// host handle (thread-local) before the launch.  The profiler (ProfScope, exacto_prof_kernels) names
+// what actually ran from it (dladdr + demangling: the rocprofv3 name), so no caller keeps a mirror of
+// the library's kernel choices.
+extern thread_local const void* g_last_kernel;
+}  // namespace exacto
+#define EXACTO_LAUNCH(K_, ...)                                                  \
+    do {                                                                        \
+        ::exacto::g_last_kernel = reinterpret_cast<const void*>(&(K_));         \
+        hipLaunchKernelGGL(K_, __VA_ARGS__);                                    \
+    } while (0)

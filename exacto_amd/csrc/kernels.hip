@@ -371,7 +371,7 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
     const long blocks = rows * blocks_per_row(n);
     if (blocks == 0) return;
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
-#define LIFT30(LT) hipLaunchKernelGGL((exact_lift_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, ct, primes)
+#define LIFT30(LT) EXACTO_LAUNCH((exact_lift_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, ct, primes)
         switch (L) {
             case 1: LIFT30(1); break;
             case 2: LIFT30(2); break;
@@ -384,10 +384,10 @@ void launch_exact_lift(const u64* coefQ, u64* extP, long rows, int n, const CrtT
         return;
     }
 #define LIFT(NR, FS, LT, KT)                                                                                     \
-    hipLaunchKernelGGL((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
+    EXACTO_LAUNCH((exact_lift_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, L, K, ct, \
                        primes)
 #define LIFT_SP(LT)                                                                                              \
-    hipLaunchKernelGGL((exact_lift_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, coefQ,  \
+    EXACTO_LAUNCH((exact_lift_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, coefQ,  \
                        extP, n, L, K, ct, primes)
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6) {
         switch (L) {
@@ -440,7 +440,7 @@ void launch_hps_extend(const u64* coefQ, u64* extP, long rows, int n, const Prim
                        int K, hipStream_t s) {
     const long blocks = rows * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(hps_extend_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, K, primes);
+    EXACTO_LAUNCH(hps_extend_kernel, dim3(blocks), dim3(TPB), 0, s, coefQ, extP, n, K, primes);
 }
 
 // ---------------------------------------------------------------- exact scale-and-round
@@ -693,7 +693,7 @@ bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int
                        hipStream_t s) {
     const long blocks = (long)items_b * d * 2 * blocks_per_row(n);
     if (blocks == 0) return true;
-#define PSUM_(LT) hipLaunchKernelGGL((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d, npairs, \
+#define PSUM_(LT) EXACTO_LAUNCH((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d, npairs, \
                                      term_start, terms, n, ct, primes)
     switch (L) {
         case 1: PSUM_(1); break;
@@ -720,7 +720,7 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
         const int dig = (D16 == nullptr && D == nullptr) || guse <= 0 ? 0
                         : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? (digits8 && gshift <= 8 ? 3 : 1) : 2;
 #define SCALE30_(LT, DG)                                                                                        \
-    hipLaunchKernelGGL((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
+    EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
                        D16, guse, n, ct, primes, c2only ? 1 : 0)
 #define SCALE30(LT)                         \
     do {                                    \
@@ -742,10 +742,10 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
         return;
     }
 #define SCALE(NR, FS, LT, KT)                                                                                    \
-    hipLaunchKernelGGL((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
+    EXACTO_LAUNCH((exact_scale_kernel<NR, FS, LT, KT>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, \
                        D, D16, guse, n, L, K, ct, primes)
 #define SCALE_SP(LT)                                                                                             \
-    hipLaunchKernelGGL((exact_scale_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, T, R,   \
+    EXACTO_LAUNCH((exact_scale_kernel<true, true, LT, LT + 1, true>), dim3(blocks), dim3(TPB), 0, s, T, R,   \
                        r_stride, ncomp_r, D, D16, guse, n, L, K, ct, primes)
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6) {
         switch (L) {
@@ -800,7 +800,7 @@ void launch_phase(const u64* ct, int polys, long ct_stride, const u64* sk, u64* 
                   const PrimeConst* primes, hipStream_t s) {
     const long blocks = (long)items * L * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(phase_kernel, dim3(blocks), dim3(TPB), 0, s, ct, polys, ct_stride, sk, out, n, L, primes);
+    EXACTO_LAUNCH(phase_kernel, dim3(blocks), dim3(TPB), 0, s, ct, polys, ct_stride, sk, out, n, L, primes);
 }
 
 // m = floor((x p + floor(Q/2)) / Q) mod p for x = CRT(phase) in [0, Q) (encrypt.rs:145-171),
@@ -846,7 +846,7 @@ void launch_decrypt_round(const u64* X, u64* out, int items, int n, int L, const
                           const PrimeConst* primes, u64 plain, hipStream_t s) {
     const long blocks = (long)items * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(decrypt_round_kernel, dim3(blocks), dim3(TPB), 0, s, X, out, n, L, ct, primes, plain);
+    EXACTO_LAUNCH(decrypt_round_kernel, dim3(blocks), dim3(TPB), 0, s, X, out, n, L, ct, primes, plain);
 }
 
 // Signed digit recomposition (dbfv/decomposition.rs:45-68, 112-127): sum centred(mu_k) b^k in
@@ -883,7 +883,7 @@ void launch_dbfv_recompose(const u64* digits, u64* out, int items, int n, int d,
                            bool scalar, hipStream_t s) {
     const long total = (long)items * (scalar ? 1 : n);
     if (total == 0) return;
-    hipLaunchKernelGGL(dbfv_recompose_kernel, dim3((unsigned)((total + TPB - 1) / TPB)), dim3(TPB), 0, s, digits,
+    EXACTO_LAUNCH(dbfv_recompose_kernel, dim3((unsigned)((total + TPB - 1) / TPB)), dim3(TPB), 0, s, digits,
                        out, items, n, d, base, plain, t, scalar ? 1 : 0);
 }
 
@@ -1072,7 +1072,7 @@ void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, 
                       hipStream_t s) {
     const long blocks = (long)items * 3 * blocks_per_row(n);
     if (blocks == 0) return;
-#define HPS_(F, DT, KK) hipLaunchKernelGGL((hps_scale_kernel<F, DT, KK>), dim3(blocks), dim3(TPB), 0, s, T, R, \
+#define HPS_(F, DT, KK) EXACTO_LAUNCH((hps_scale_kernel<F, DT, KK>), dim3(blocks), dim3(TPB), 0, s, T, R, \
                                            r_stride, ncomp_r, D, (DT*)D16, guse, n, K, ct, primes)
     if (fast && K == 1) {
         if (d8) HPS_(true, int8_t, 1); else HPS_(true, int16_t, 1);
@@ -1104,7 +1104,7 @@ void launch_decompose(const u64* C2, long c2_stride, u64* D, int guse, int items
                       const CrtTables* ct, const PrimeConst* primes, int L, hipStream_t s, int16_t* D16) {
     const long blocks = (long)items * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(decompose_kernel, dim3(blocks), dim3(TPB), 0, s, C2, c2_stride, D, D16, guse, n, L,
+    EXACTO_LAUNCH(decompose_kernel, dim3(blocks), dim3(TPB), 0, s, C2, c2_stride, D, D16, guse, n, L,
                        ct, primes);
 }
 
@@ -1262,14 +1262,14 @@ __global__ void __launch_bounds__(64) xcd_probe_kernel(const u64* src, u64* dst,
 }
 
 void launch_xcd_probe(const u64* src, u64* dst, long words, uint32_t* xcc, int blocks, hipStream_t s) {
-    hipLaunchKernelGGL(xcd_probe_kernel, dim3(blocks), dim3(64), 0, s, src, dst, words, xcc);
+    EXACTO_LAUNCH(xcd_probe_kernel, dim3(blocks), dim3(64), 0, s, src, dst, words, xcc);
 }
 
 void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, long len, long rows, hipStream_t s) {
     const long total = len * rows;
     if (total <= 0) return;
     const long blocks = std::min<long>((total + TPB - 1) / TPB, 65536);
-    hipLaunchKernelGGL(rows_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, dst, dst_stride, src, src_stride, len,
+    EXACTO_LAUNCH(rows_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, dst, dst_stride, src, src_stride, len,
                        total, g_watch.lo, g_watch.hi, g_watch.hit);
 }
 
@@ -1284,12 +1284,12 @@ void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64
     }();
     if (use_lds && guse <= MAC_GMAX && Ln % MAC_LS == 0) {
         const dim3 grid((unsigned)(Ln / MAC_LS), (unsigned)((items + MAC_IG - 1) / MAC_IG));
-        hipLaunchKernelGGL(relin_mac_lds_kernel, grid, dim3(TPB), (size_t)guse * 4 * MAC_LS * sizeof(u64), s, base,
+        EXACTO_LAUNCH(relin_mac_lds_kernel, grid, dim3(TPB), (size_t)guse * 4 * MAC_LS * sizeof(u64), s, base,
                            base_stride, D, rlk, rlk_s, guse, out, out_stride, items, n, L, primes);
         return;
     }
     const long blocks = (long)items * ((Ln / 2 + TPB - 1) / TPB);
-    hipLaunchKernelGGL(relin_mac_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, base, base_stride, D, rlk, rlk_s,
+    EXACTO_LAUNCH(relin_mac_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, base, base_stride, D, rlk, rlk_s,
                        guse, out, out_stride, items, n, L, primes);
 }
 
@@ -1319,7 +1319,7 @@ void launch_pointwise(PwOp op, const u64* a, const u64* b, u64* out, long polys,
                       const u64* scalar_mod, const PrimeConst* primes, hipStream_t s) {
     const long blocks = polys * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(pointwise_kernel, dim3(blocks), dim3(TPB), 0, s, (int)op, a, b, out, n, L,
+    EXACTO_LAUNCH(pointwise_kernel, dim3(blocks), dim3(TPB), 0, s, (int)op, a, b, out, n, L,
                        scalar_mod, primes);
 }
 
@@ -1352,7 +1352,7 @@ void launch_bfv_addsub(bool sub, const u64* a, int p1, const u64* b, int p2, u64
                        const PrimeConst* primes, hipStream_t s) {
     const long blocks = items * (p1 > p2 ? p1 : p2) * L * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(bfv_addsub_kernel, dim3(blocks), dim3(TPB), 0, s, sub ? 1 : 0, a, p1, b, p2, out, n, L, primes);
+    EXACTO_LAUNCH(bfv_addsub_kernel, dim3(blocks), dim3(TPB), 0, s, sub ? 1 : 0, a, p1, b, p2, out, n, L, primes);
 }
 
 // ---------------------------------------------------------------- dBFV combine
@@ -1385,7 +1385,7 @@ void launch_dbfv_combine(const u64* prod, int npairs, const int* term_start,
                          const PrimeConst* primes, hipStream_t s) {
     const long blocks = (long)items * d * 2 * L * blocks_per_row(n);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(dbfv_combine_kernel, dim3(blocks), dim3(TPB), 0, s, prod, npairs, term_start,
+    EXACTO_LAUNCH(dbfv_combine_kernel, dim3(blocks), dim3(TPB), 0, s, prod, npairs, term_start,
                        terms, out, d, n, L, primes);
 }
 
@@ -1406,7 +1406,7 @@ void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words, g_watch.lo, g_watch.hi,
+    EXACTO_LAUNCH(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words, g_watch.lo, g_watch.hi,
                        g_watch.hit);
 }
 
@@ -1424,7 +1424,7 @@ void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words, g_watch.lo, g_watch.hi,
+    EXACTO_LAUNCH(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words, g_watch.lo, g_watch.hi,
                        g_watch.hit);
 }
 

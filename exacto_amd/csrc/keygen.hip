@@ -115,7 +115,7 @@ void launch_sample(int kind, const ChaChaKey& key, u64 nonce, u64* out, long out
                    int tail, double total, hipStream_t s) {
     const long blocks = polys * ((n + KG_TPB - 1) / KG_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(sample_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, kind, key, nonce, out, out_stride,
+    EXACTO_LAUNCH(sample_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, kind, key, nonce, out, out_stride,
                        poly_base, poly_step, n, L, primes, cdt, cdt_len, tail, total);
 }
 
@@ -138,7 +138,7 @@ void launch_scale_plain(const u64* pt, const u64* delta, u64* dm, long items, in
                         hipStream_t s) {
     const long blocks = items * L * ((n + KG_TPB - 1) / KG_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(scale_plain_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, pt, delta, dm, n, L, primes);
+    EXACTO_LAUNCH(scale_plain_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, pt, delta, dm, n, L, primes);
 }
 
 // NTT-domain combinations, one thread per (item, limb, coefficient); polynomials [L][n] per item.
@@ -188,7 +188,7 @@ void launch_combine(int op, u64* x, long items, long item_stride, long x1_off, c
                     hipStream_t st) {
     const long blocks = items * L * ((n + KG_TPB - 1) / KG_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(combine_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, st, op, x, item_stride, x1_off, s, aux,
+    EXACTO_LAUNCH(combine_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, st, op, x, item_stride, x1_off, s, aux,
                        aux2, pk, gpow, n, L, primes);
 }
 
@@ -246,11 +246,11 @@ void launch_automorph(const u64* in, long in_stride, u64* out, long out_stride, 
         for (int it = 0; it < 7; ++it) kinv = kinv * (2 - k * kinv);
         kinv &= two_n - 1;
         const long blocks = rows * ((n + KG_TPB - 1) / KG_TPB);
-        hipLaunchKernelGGL(automorph_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, in, in_stride, out,
+        EXACTO_LAUNCH(automorph_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, in, in_stride, out,
                            out_stride, polys, n, L, kinv, primes, prime_fixed);
     } else {
         launch_rows(out, out_stride, nullptr, 0, (long)polys * L * n, items, s);
-        hipLaunchKernelGGL(automorph_serial_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, in,
+        EXACTO_LAUNCH(automorph_serial_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, in,
                            in_stride, out, out_stride, polys, n, L, k, rows, primes, prime_fixed);
     }
 }
@@ -270,7 +270,7 @@ lift_q0_kernel(const u64* __restrict__ v, u64* __restrict__ out, int n, int L, c
 void launch_lift_q0(const u64* v, u64* out, long rows, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = rows * ((n + KG_TPB - 1) / KG_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(lift_q0_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, v, out, n, L, primes);
+    EXACTO_LAUNCH(lift_q0_kernel, dim3((unsigned)blocks), dim3(KG_TPB), 0, s, v, out, n, L, primes);
 }
 
 }  // namespace exacto

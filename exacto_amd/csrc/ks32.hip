@@ -286,10 +286,10 @@ static void ks32_launch_digits(const void* D, bool wide, uint32_t* DS, int items
 #define DIG_(F_)                                                                                                \
     do {                                                                                                        \
         if (wide)                                                                                               \
-            hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int32_t, F_>), grid, block, 0, st, (const int32_t*)D, \
+            EXACTO_LAUNCH((ks32_digit_ntt_kernel<LOGN, int32_t, F_>), grid, block, 0, st, (const int32_t*)D, \
                                DS, G, S, primes);                                                               \
         else                                                                                                    \
-            hipLaunchKernelGGL((ks32_digit_ntt_kernel<LOGN, int16_t, F_>), grid, block, 0, st, (const int16_t*)D, \
+            EXACTO_LAUNCH((ks32_digit_ntt_kernel<LOGN, int16_t, F_>), grid, block, 0, st, (const int16_t*)D, \
                                DS, G, S, primes);                                                               \
     } while (0)
     FORM_SWITCH(form, DIG_)
@@ -299,7 +299,7 @@ static void ks32_launch_digits(const void* D, bool wide, uint32_t* DS, int items
 template <int LOGN>
 static void ks32_launch_key(const u64* K, uint32_t* RS, long rows, int L, int S, const Prime32* primes,
                             const PrimeConst* qprimes, int form, hipStream_t st) {
-#define KEY_(F_) hipLaunchKernelGGL((ks32_key_kernel<LOGN, F_>), dim3((unsigned)(rows * S)), dim3((1 << LOGN) / 16), 0, \
+#define KEY_(F_) EXACTO_LAUNCH((ks32_key_kernel<LOGN, F_>), dim3((unsigned)(rows * S)), dim3((1 << LOGN) / 16), 0, \
                                     st, K, RS, L, S, primes, qprimes)
     FORM_SWITCH(form, KEY_)
 #undef KEY_
@@ -310,11 +310,11 @@ static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items,
                             const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
     const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
     if (S == 2)
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 2, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 2, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else if (S == 3)
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 3, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 3, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
     else
-        hipLaunchKernelGGL((ks32_crt_kernel<LOGN, 4, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 4, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
 }
 
 #define KS32_SWITCH(logn, CALL)                  \
@@ -353,7 +353,7 @@ void ks32_key(const u64* K, uint32_t* RS, long rows, int L, int S, int logn, con
 
 void ks32_key_norms(const u64* K, u64* out, long rows, int L, int n, const PrimeConst* qprimes, hipStream_t st) {
     if (rows <= 0) return;
-    hipLaunchKernelGGL(ks32_key_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, K, out, L, n, qprimes);
+    EXACTO_LAUNCH(ks32_key_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, K, out, L, n, qprimes);
 }
 
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
@@ -372,7 +372,7 @@ void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, in
     const int* rs = reinterpret_cast<const int*>(RS);
 // mac_form: 0 primes up to 2^31 (7 products per reduction), 1 below 2^32 / 3 (12), 2 below 2^30
 // (12, lazy output)
-#define MAC_(C_, W_, R_, Z_) hipLaunchKernelGGL((ks32_mac_kernel<C_, W_, R_, Z_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
+#define MAC_(C_, W_, R_, Z_) EXACTO_LAUNCH((ks32_mac_kernel<C_, W_, R_, Z_>), grid, dim3(W_ * 64), lds, st, ds, rs, U, G, CL, S, items, n, primes)
 #define MAC(C_)                                                  \
     do {                                                         \
         if (mac_form == 2) { if (NW == 8) MAC_(C_, 8, 12, true); else MAC_(C_, 4, 12, true); } \
@@ -398,7 +398,7 @@ void ks32_digit_sum(const void* D, bool in8, int npairs, const int* term_start, 
     const int nb = n >= 2048 ? n / 2048 : 1;   // n >= 1024, a power of two; 2048 digits per block
     const dim3 grid((unsigned)(rows * nb)), block(n >= 2048 ? 256 : n / 8);
     const int nsh = __builtin_ctz((unsigned)nb);
-#define DSUM_(OT, IT) hipLaunchKernelGGL((ks32_digit_sum_kernel<OT, IT>), grid, block, 0, st, (const IT*)D, npairs, \
+#define DSUM_(OT, IT) EXACTO_LAUNCH((ks32_digit_sum_kernel<OT, IT>), grid, block, 0, st, (const IT*)D, npairs, \
                                          term_start, terms, (OT*)out, d, gu, n, nsh)
     if (wide) {
         if (in8) DSUM_(int32_t, int8_t); else DSUM_(int32_t, int16_t);

@@ -1139,15 +1139,15 @@ static void launch_mi(const u64* A, const u64* B, u64* out, long rows, int perio
     constexpr int threads = (1 << LOGN) / 16 < 64 ? 64 : (1 << LOGN) / 16;
     if constexpr (LOGN == 12 || LOGN == 13) {
         if (asm_inv) {
-            hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, true, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
+            EXACTO_LAUNCH((ntt_mulinv_kernel<LOGN, true, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
                                primes);
             return;
         }
     }
     if (lazy)
-        hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period, primes);
+        EXACTO_LAUNCH((ntt_mulinv_kernel<LOGN, true>), dim3(rows), dim3(threads), 0, s, A, B, out, period, primes);
     else
-        hipLaunchKernelGGL((ntt_mulinv_kernel<LOGN, false>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
+        EXACTO_LAUNCH((ntt_mulinv_kernel<LOGN, false>), dim3(rows), dim3(threads), 0, s, A, B, out, period,
                            primes);
 }
 
@@ -1211,9 +1211,9 @@ bool launch_polymul(const u64* A, const u64* B, u64* out, long rows, int period,
     // (a pinned-home form at 4 waves per SIMD, a parked in out's rows, measured 866-876 vs 806 us per
     // cfg2 launch and was removed, round 4)
     if (logn == 12)
-        hipLaunchKernelGGL(ntt_polymul_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
+        EXACTO_LAUNCH(ntt_polymul_kernel<12>, dim3(rows), dim3(256), 0, s, A, B, out, period, primes);
     else if (logn == 13)
-        hipLaunchKernelGGL(ntt_polymul_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
+        EXACTO_LAUNCH(ntt_polymul_kernel<13>, dim3(rows), dim3(512), 0, s, A, B, out, period, primes);
     else
         return false;
     return true;
@@ -1235,12 +1235,12 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
                        hipStream_t s) {
     constexpr int threads = (1 << LOGN) / 16;
     if (inverse)
-        hipLaunchKernelGGL((lazy ? ntt_inv_kernel<LOGN, true> : ntt_inv_kernel<LOGN, false>), dim3(count),
+        EXACTO_LAUNCH((lazy ? ntt_inv_kernel<LOGN, true> : ntt_inv_kernel<LOGN, false>), dim3(count),
                            dim3(threads), 0, s, nb, primes);
     else if (lazy)
-        hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
+        EXACTO_LAUNCH((ntt_fwd_kernel<LOGN, true>), dim3(count), dim3(threads), 0, s, nb, primes);
     else
-        hipLaunchKernelGGL((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
+        EXACTO_LAUNCH((ntt_fwd_kernel<LOGN, false>), dim3(count), dim3(threads), 0, s, nb, primes);
 }
 
 // dBFV, psum (dbfv_mul_core): the auxiliary-prime residues of each output limb's c0 and c1 tensors
@@ -1288,7 +1288,7 @@ void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int n
                          const CombineTerm* terms, int L, int K, int n, const PrimeConst* primes, hipStream_t s) {
     const long blocks = (long)items_b * K * d * (n >> 8);
     if (blocks == 0 || n < 256) return;
-    hipLaunchKernelGGL(dbfv_pairsum_kernel, dim3(blocks), dim3(256), 0, s, op, out, d, npairs, L, K, n, term_start,
+    EXACTO_LAUNCH(dbfv_pairsum_kernel, dim3(blocks), dim3(256), 0, s, op, out, d, npairs, L, K, n, term_start,
                        terms, primes);
 }
 
@@ -1330,20 +1330,20 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
         if (asm_inv && tensor_pin_at(LOGN)) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             if (lzo)
-                hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN, true>), dim3(b2), dim3(threads), 0, s, op, extP, T,
+                EXACTO_LAUNCH((ntt_inv_tensor_pin_kernel<LOGN, true>), dim3(b2), dim3(threads), 0, s, op, extP, T,
                                    L, K, primes, remap, p2only, np);
             else
-                hipLaunchKernelGGL((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L,
+                EXACTO_LAUNCH((ntt_inv_tensor_pin_kernel<LOGN>), dim3(b2), dim3(threads), 0, s, op, extP, T, L,
                                    K, primes, remap, p2only, np);
             return;
         }
         if (asm_inv) {
             const long b2 = p2only ? blocks / (3 * (L + K)) * (3 * L + K) : blocks;
             if (lzo)
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true, 0, false, 60, true>), dim3(b2),
+                EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, true, true, 0, false, 60, true>), dim3(b2),
                                    dim3(threads), 0, s, op, extP, T, L, K, primes, remap, p2only, np);
             else
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
+                EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, true, true>), dim3(b2), dim3(threads), 0, s, op, extP,
                                    T, L, K, primes, remap, p2only, np);
             return;
         }
@@ -1351,19 +1351,19 @@ static void launch_it(const Operands& op, const u64* extP, u64* T, long blocks, 
     if constexpr (LOGN == 10 || LOGN == 12 || LOGN == 13) {
         if (lazy && !p2only && ntt_gen_on()) {   // every prime below 2^60: the generated generic-prime rounds
             if (gen_small<LOGN>(qbits))
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true, gen_qb<LOGN>()>), dim3(blocks),
+                EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, true, false, 0, true, gen_qb<LOGN>()>), dim3(blocks),
                                    dim3(threads), 0, s, op, extP, T, L, K, primes, remap, 0, np);
             else
-                hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0,
+                EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, true, false, 0, true>), dim3(blocks), dim3(threads), 0,
                                    s, op, extP, T, L, K, primes, remap, 0, np);
             return;
         }
     }
     if (lazy)
-        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L, K,
+        EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, true>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L, K,
                            primes, remap);
     else
-        hipLaunchKernelGGL((ntt_inv_tensor_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L,
+        EXACTO_LAUNCH((ntt_inv_tensor_kernel<LOGN, false>), dim3(blocks), dim3(threads), 0, s, op, extP, T, L,
                            K, primes, remap);
 }
 
@@ -1401,8 +1401,8 @@ bool launch_ntt_fwd2(const NttBatch& nb1, int count1, const NttBatch& nb2, int c
                      const PrimeConst* primes, hipStream_t s) {
     if (count1 <= 0 || count2 <= 0 || (logn != 12 && logn != 13)) return false;
     const dim3 grid((unsigned)(count1 + count2));
-    if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), grid, dim3(256), 0, s, nb1, primes, nb2, count1);
-    else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), grid, dim3(512), 0, s, nb1, primes, nb2, count1);
+    if (logn == 12) EXACTO_LAUNCH((ntt_fwd_pin_kernel<12>), grid, dim3(256), 0, s, nb1, primes, nb2, count1);
+    else EXACTO_LAUNCH((ntt_fwd_pin_kernel<13>), grid, dim3(512), 0, s, nb1, primes, nb2, count1);
     return true;
 }
 
@@ -1414,22 +1414,22 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
     // DESIGN.md §6)
     if (asm_fwd && !inverse && (logn == 12 || logn == 13)) {
         if (nb.lazy_out) {
-            if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12, 0, true>), dim3(count), dim3(256), 0, s, nb, primes);
-            else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13, 0, true>), dim3(count), dim3(512), 0, s, nb, primes);
+            if (logn == 12) EXACTO_LAUNCH((ntt_fwd_pin_kernel<12, 0, true>), dim3(count), dim3(256), 0, s, nb, primes);
+            else EXACTO_LAUNCH((ntt_fwd_pin_kernel<13, 0, true>), dim3(count), dim3(512), 0, s, nb, primes);
         } else {
-            if (logn == 12) hipLaunchKernelGGL((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-            else hipLaunchKernelGGL((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+            if (logn == 12) EXACTO_LAUNCH((ntt_fwd_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+            else EXACTO_LAUNCH((ntt_fwd_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         }
         return;
     }
     if (asm_inv && inverse && (logn == 12 || logn == 13)) {
-        if (logn == 12) hipLaunchKernelGGL((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
-        else hipLaunchKernelGGL((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
+        if (logn == 12) EXACTO_LAUNCH((ntt_inv_pin_kernel<12>), dim3(count), dim3(256), 0, s, nb, primes);
+        else EXACTO_LAUNCH((ntt_inv_pin_kernel<13>), dim3(count), dim3(512), 0, s, nb, primes);
         return;
     }
     if (lazy && (logn == 10 || logn == 12 || logn == 13) && ntt_gen_on()) {   // every prime below 2^60: generic asm rounds
         const dim3 th(1u << (logn - 4));
-#define GEN_NTT_(K_, LG_, QB_) hipLaunchKernelGGL((K_<LG_, QB_>), dim3(count), th, 0, s, nb, primes)
+#define GEN_NTT_(K_, LG_, QB_) EXACTO_LAUNCH((K_<LG_, QB_>), dim3(count), th, 0, s, nb, primes)
         if (inverse) {
             if (logn == 10) { if (gen_small<10>(qbits)) GEN_NTT_(ntt_inv_gen_kernel, 10, 50); else GEN_NTT_(ntt_inv_gen_kernel, 10, 60); }
             else if (logn == 12) { if (gen_small<12>(qbits)) GEN_NTT_(ntt_inv_gen_kernel, 12, 56); else GEN_NTT_(ntt_inv_gen_kernel, 12, 60); }
@@ -1461,7 +1461,7 @@ void launch_ntt(const NttBatch& nb, int count, int logn, bool inverse, bool lazy
 void launch_shoup_companions(const u64* w, u64* ws, long count, int n, int L, const PrimeConst* primes,
                              hipStream_t s) {
     if (count <= 0) return;
-    hipLaunchKernelGGL(shoup_companion_kernel, dim3((count + 255) / 256), dim3(256), 0, s, w, ws, count, n, L,
+    EXACTO_LAUNCH(shoup_companion_kernel, dim3((count + 255) / 256), dim3(256), 0, s, w, ws, count, n, L,
                        primes);
 }
 

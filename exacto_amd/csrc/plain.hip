@@ -45,7 +45,7 @@ void launch_plain_apply(int op, const u64* x, long x_item_stride, u64* out, long
                         long pt_item_stride, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = items * polys * L * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(plain_apply_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, op, x, x_item_stride, out, polys,
+    EXACTO_LAUNCH(plain_apply_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, op, x, x_item_stride, out, polys,
                        pt, pt_item_stride, n, L, primes);
 }
 
@@ -72,7 +72,7 @@ void launch_inner_product(const u64* cts, const u64* pts, u64* out, int K, int p
                           const PrimeConst* primes, hipStream_t s) {
     const long blocks = (long)polys * L * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0 || K == 0) return;
-    hipLaunchKernelGGL(inner_product_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, cts, pts, out, K, polys, n,
+    EXACTO_LAUNCH(inner_product_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, cts, pts, out, K, polys, n,
                        L, primes);
 }
 
@@ -96,7 +96,7 @@ monomial_kernel(u64* __restrict__ out, u64 j0, int neg, int n, int L, const Prim
 void launch_monomials(u64* out, long J, u64 j0, bool neg, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = J * L * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(monomial_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, j0, (int)neg, n, L, primes);
+    EXACTO_LAUNCH(monomial_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, j0, (int)neg, n, L, primes);
 }
 
 }  // namespace exacto
@@ -120,7 +120,7 @@ axpy_kernel(u64* __restrict__ out, const u64* __restrict__ x, u64 a, int n, int 
 void launch_axpy(u64* out, const u64* x, u64 a, long rows, int n, int L, const PrimeConst* primes, hipStream_t s) {
     const long blocks = rows * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(axpy_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, x, a, n, L, primes);
+    EXACTO_LAUNCH(axpy_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, x, a, n, L, primes);
 }
 
 // trivial encryptions of the constant m (digit_extract.rs:160-176): (Delta m, 0) per item, where the
@@ -142,7 +142,7 @@ void launch_trivial_const(u64* out, long items, u64 m, const u64* delta, int n, 
                           hipStream_t s) {
     const long blocks = items * 2 * L * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(trivial_const_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, m, delta, n, L, primes);
+    EXACTO_LAUNCH(trivial_const_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, out, m, delta, n, L, primes);
 }
 
 }  // namespace exacto
@@ -168,7 +168,7 @@ modswitch_kernel(const u64* __restrict__ coef, u64* __restrict__ out, int* __res
 void launch_modswitch(const u64* coef, u64* out, int* flags, long items, int n, u64 q, u64 qp, u64 tb, hipStream_t s) {
     const long blocks = items * 2 * ((n + PL_TPB - 1) / PL_TPB);
     if (blocks == 0) return;
-    hipLaunchKernelGGL(modswitch_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, coef, out, flags, n, q, qp, tb);
+    EXACTO_LAUNCH(modswitch_kernel, dim3((unsigned)blocks), dim3(PL_TPB), 0, s, coef, out, flags, n, q, qp, tb);
 }
 
 // gen_bootstrap_key's two images of the ternary secret s (coefficients mod q_orig):
@@ -195,7 +195,7 @@ boot_key_map_kernel(const u64* __restrict__ s, u64* __restrict__ boot_coef, u64*
 }
 
 void launch_boot_key_map(const u64* s, u64* boot_coef, u64* s_pt, int n, u64 q, u64 qb, u64 tb, hipStream_t st) {
-    hipLaunchKernelGGL(boot_key_map_kernel, dim3((unsigned)((n + PL_TPB - 1) / PL_TPB)), dim3(PL_TPB), 0, st, s,
+    EXACTO_LAUNCH(boot_key_map_kernel, dim3((unsigned)((n + PL_TPB - 1) / PL_TPB)), dim3(PL_TPB), 0, st, s,
                        boot_coef, s_pt, n, q, qb, tb);
 }
 

@@ -15,8 +15,68 @@ dbfv_mul shard across the GPUs"): output limb k = sum over pairs (i, j) with i +
 
 from __future__ import annotations
 
+import json
+import os
+import sys
+import threading
+import time
+
 import torch
 import torch.distributed as dist
+
+
+def deadline_s() -> float:
+    """Deadline of one phase of the multi-rank path, seconds ($EXACTO_DIST_DEADLINE_S, default 600)."""
+    return float(os.environ.get("EXACTO_DIST_DEADLINE_S", "600"))
+
+
+class Watchdog:
+    """Deadline per phase of a multi-rank run.
+
+    A daemon thread checks the armed phase twice a second.  When a phase outlives its deadline (a
+    rank never joined a collective, a communicator init or an RCCL kernel is stuck) it prints one JSON
+    diagnostic line to stderr and ends the process with ``os._exit(124)``: no exec, no interpreter
+    teardown that could block again in the same collective.  torchrun then sees a failed rank and stops
+    the others, so the whole job exits non-zero within about one deadline.  Native calls release the
+    GIL (ctypes, torch.distributed), so the thread runs while the main thread is blocked in them.
+
+    Test hook (``--dry`` runs only): ``EXACTO_BENCH_WITHHOLD=<rank>:<phase>`` makes that rank stall at the
+    start of that phase, i.e. withhold its part of the phase's collective."""
+
+    def __init__(self, rank: int, enabled: bool = True, withhold_ok: bool = False):
+        self.rank = rank
+        self.phase = None
+        self.deadline = None
+        self.t0 = None
+        self._lock = threading.Lock()
+        w = os.environ.get("EXACTO_BENCH_WITHHOLD", "") if withhold_ok else ""
+        self._withhold = tuple(w.split(":", 1)) if ":" in w else None
+        if enabled:
+            threading.Thread(target=self._run, name="exacto-watchdog", daemon=True).start()
+
+    def arm(self, phase: str, seconds: float | None = None):
+        with self._lock:
+            self.phase, self.t0 = phase, time.monotonic()
+            self.deadline = self.t0 + (deadline_s() if seconds is None else seconds)
+        if self._withhold and self._withhold == (str(self.rank), phase):
+            while True:   # withholding this rank's part: only the watchdog ends this
+                time.sleep(3600)
+
+    def disarm(self):
+        with self._lock:
+            self.phase = self.deadline = None
+
+    def _run(self):
+        while True:
+            time.sleep(0.5)
+            with self._lock:
+                ph, dl, t0 = self.phase, self.deadline, self.t0
+            if dl is not None and time.monotonic() > dl:
+                sys.stderr.write(json.dumps({"watchdog": "deadline exceeded", "rank": self.rank, "phase": ph,
+                                             "waited_s": round(time.monotonic() - t0, 1)}) + "\n")
+                sys.stderr.flush()
+                sys.stdout.flush()
+                os._exit(124)
 
 
 def shard(total: int, rank: int, world: int) -> tuple[int, int]:

@@ -95,6 +95,10 @@ class BfvParamsBuilder {
                                         device_));
         exacto_ctx_info info{};
         detail::check(exacto_ctx_get_info(p->ctx_, &info));
+        // NTT-domain data (keys, ciphertexts) is laid out in the library's storage order: refuse a
+        // library whose order differs from the one this header was written for
+        if (info.ntt_order != EXACTO_NTT_ORDER)
+            throw ExactoError(EXACTO_ERR_INVALID_PARAM, "libexacto_hip NTT-domain order differs from exacto.hpp's");
         p->ring_degree = n_;
         p->plain_modulus = p_;
         p->ct_moduli = ct_;

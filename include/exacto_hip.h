@@ -81,7 +81,16 @@ typedef struct exacto_ctx_info {
     int psum_max;             /* dbfv_mul: products per output limb scaled as one sum (0: per product) */
     int ks32_lazy;            /* 1: the resident relinearisation key runs in the lazy 31-bit basis (primes
                                  below 2^30, chosen from the key's own norms at its first use) */
+    int ntt_order;            /* storage order of every NTT-domain buffer (keys, ciphertexts): 1 = evaluation k
+                                 at position (k mod 16)*n/16 + floor(k/16) (library 0.5 and later); 0 would be
+                                 the plain bit-reversed order of 0.4 and earlier, which this library no longer
+                                 reads or writes.  Bindings check it (INTEGRATION.md "Format versions") */
+    int dbfv_key_switch;      /* the last dbfv_mul's key switch: 1 = the products' digits summed per output
+                                 limb in the primary 31-bit basis, 2 = the same in the wide basis, 0 = one key
+                                 switch per product, -1 = no dbfv_mul yet */
 } exacto_ctx_info;
+
+#define EXACTO_NTT_ORDER 1
 
 /* ---- context: replaces BfvParamsBuilder::build + RnsBasis::new + make_plan ----
  * params/mod.rs:81-124, ring/rns.rs:35-63, ring/ntt.rs:19-29.
@@ -396,7 +405,13 @@ int exacto_bfv_bootstrap_dev(exacto_ctx* orig, exacto_ctx* boot, const uint64_t*
  *                              num_keys, fail with InvalidParam on EVERY rank, keys untouched
  *   exacto_broadcast_galois_key      a device Galois key buffer [num_keys][2][L][n], in place
  *   exacto_rccl_allgather_u64  recv = [nranks][count] u64 (never a reduction: residues are not summable
- *                              by RCCL) */
+ *                              by RCCL)
+ *   exacto_rccl_sync           waits for the context stream (the collectives enqueued on it) with a deadline
+ * Deadlines: communicator init, the agreement all-gather and exacto_rccl_sync wait at most
+ * $EXACTO_RCCL_TIMEOUT_S seconds (default 300, 0 = forever) for the other ranks; on expiry they return
+ * EXACTO_ERR_HIP "RCCL error: ... timed out" (a collective's communicator is aborted with ncclCommAbort,
+ * after which exacto_rccl_comm_destroy on it is a no-op), so a rank that never joins cannot block the
+ * others for good. */
 int exacto_rccl_unique_id(uint8_t* id);
 int exacto_rccl_comm_init(void** comm, int nranks, const uint8_t* id, int rank, int device);
 int exacto_rccl_comm_destroy(void* comm);
@@ -404,6 +419,7 @@ int exacto_rccl_comm_count(void* comm, int* nranks);
 int exacto_ctx_broadcast_relin_key(exacto_ctx* ctx, void* comm, int root, size_t num_keys);
 int exacto_broadcast_galois_key(exacto_ctx* ctx, void* comm, int root, uint64_t* gk_dev, size_t num_keys);
 int exacto_rccl_allgather_u64(exacto_ctx* ctx, void* comm, const uint64_t* send, uint64_t* recv, size_t count);
+int exacto_rccl_sync(exacto_ctx* ctx, void* comm);
 
 size_t exacto_last_error(char* buf, size_t len);
 /* Per-kernel-family timing of the last profiled calls: enable, then read
@@ -412,6 +428,10 @@ size_t exacto_last_error(char* buf, size_t len);
 int exacto_prof_enable(exacto_ctx* ctx, int enable);
 int exacto_prof_read(exacto_ctx* ctx, int kind, uint64_t* launches, double* total_ms,
                      double* total_bytes, uint64_t* polys);
+/* The kernels that ran for one family in the records exacto_prof_read consumed (since the last call for
+ * that kind), named as rocprofv3 names them ("exacto::ntt_fwd_pin_kernel<12, 0, false>"), by descending
+ * event time: "name (launches, ms); ...".  Returns the full length (snprintf-like); buf may be NULL. */
+size_t exacto_prof_kernels(exacto_ctx* ctx, int kind, char* buf, size_t len);
 const char* exacto_version(void);
 
 #ifdef __cplusplus

@@ -270,6 +270,10 @@ def worst_digests(threads):
 #   cfg1    bfv_mul_and_relin on compact_bfv, B = 8192 (chunks of 7168 + 1024; eval.rs:157-332)
 #   u64dbfv dbfv_mul on u64_dbfv, B = 64 items (4096 HPS products, chunks of 1152; dbfv/eval.rs:82-149)
 #   cfg2    INTT(NTT(a) . NTT(b)) of B = 16384 coefficient-domain polys (ntt.rs:181-195)
+#   cfg4    dbfv_mul d = 2 over cfg3's basis, B = 1024 items (3072 products with psum digit sums across
+#           six 512-product chunks; dbfv/eval.rs:82-149)
+#   cfg5    dbfv_mul chain of depth 4 (paper_repro.rs:203-236: acc <- dbfv_mul(acc, y)), B = 8 chains at
+#           n = 8192, every chain digested on its own
 # Inputs are regenerated from the seed by the GPU test (numpy default_rng, tests/bridge.py); the
 # digests of row blocks name the failing rows when one differs.
 BENCH_DIGESTS = {
@@ -277,7 +281,10 @@ BENCH_DIGESTS = {
     "cfg1_bench": {"config": "cfg1", "n": 1024, "batch": 8192, "seed": 1101, "block": 1024},
     "u64dbfv_bench": {"config": "u64dbfv", "n": 4096, "batch": 64, "seed": 6401, "block": 8},
     "cfg2_bench": {"config": "cfg2", "n": 4096, "batch": 16384, "seed": 2201, "block": 2048},
+    "cfg4_bench": {"config": "cfg4", "n": 4096, "batch": 1024, "seed": 4401, "block": 128},
+    "cfg5_bench": {"config": "cfg5", "n": 8192, "batch": 8, "seed": 5501, "block": 1, "depth": 4},
 }
+DBFV_CFGS = ("u64dbfv", "cfg4", "cfg5")
 BENCH_GEN = ("numpy.random.default_rng(seed); bfv: ct1, ct2 = uniform_residues((B, 2)), rlk = "
              "uniform_residues((G, 2)); dbfv: a, b = uniform_residues((B, d, 2)), rlk; cfg2: a, b = "
              "uniform_residues((B,))  (tests/bridge.py)")
@@ -292,17 +299,21 @@ def bench_params(cfg, n):
         return P.u64_dbfv()
     if cfg == "cfg2":
         return P.BfvParamsBuilder().ring_degree(n).plain_modulus(65537).ct_moduli([P.Q3[0]]).build()
+    if cfg == "cfg4":
+        return P.cfg4_params(n)
+    if cfg == "cfg5":
+        return P.cfg5_params(n)
     raise ValueError(cfg)
 
 
 def bench_digest_inputs(spec):
     """(params, x, y, rlk) of a BENCH_DIGESTS entry; x, y are ct1/ct2, a/b or the cfg2 operands."""
     prm = bench_params(spec["config"], spec["n"])
-    bp = prm.bfv_params if spec["config"] == "u64dbfv" else prm
+    dbfv = spec["config"] in DBFV_CFGS
+    bp = prm.bfv_params if dbfv else prm
     rng = np.random.default_rng(spec["seed"])
     q, n, B = bp.ct_basis.moduli, bp.ring_degree, spec["batch"]
-    pre = {"cfg2": (B,), "u64dbfv": (B, prm.num_digits if spec["config"] == "u64dbfv" else 0, 2)}.get(
-        spec["config"], (B, 2))
+    pre = (B,) if spec["config"] == "cfg2" else (B, prm.num_digits, 2) if dbfv else (B, 2)
     x = uniform_residues(rng, pre, q, n)
     y = uniform_residues(rng, pre, q, n)
     rlk = None if spec["config"] == "cfg2" else uniform_residues(rng, (bp.gadget_digits, 2), q, n)
@@ -313,8 +324,11 @@ def bench_output(spec, prm, x, y, rlk, threads):
     from oracle import cref
     if spec["config"] == "cfg2":
         return cref.polymul(spec["n"], prm.ct_basis.moduli[0], x, y, threads=threads)
-    if spec["config"] == "u64dbfv":
-        return cref.dbfv_mul(prm, x, y, rlk, threads=threads)
+    if spec["config"] in DBFV_CFGS:
+        acc = x
+        for _ in range(spec.get("depth", 1)):
+            acc = cref.dbfv_mul(prm, acc, y, rlk, threads=threads)
+        return acc
     return cref.bfv_mul_and_relin(prm, x, y, rlk, threads=threads)
 
 

@@ -235,3 +235,19 @@ def test_gloo_gather_plan(world):
 def test_bench_world_size_mismatch_exits_nonzero():
     rc, line, _ = _bench("--gpus", "2", "--dry", env_extra={"WORLD_SIZE": "1"})
     assert rc != 0 and line is None
+
+
+@pytest.mark.parametrize("phase", ["key_broadcast", "timed"])
+def test_bench_dry_withheld_rank_exits_within_deadline(phase):
+    """Verdict r5 item 6: one rank withholding its part of a collective (the key broadcast, or the
+    barrier that opens the timed region) ends the job non-zero within about one deadline, with the
+    watchdog's diagnostic line, instead of blocking it until the driver's time limit."""
+    import time
+    t0 = time.monotonic()
+    rc, line, r = _bench("--gpus", "2", "--dry", "--config", "cfg3", "--batch", "4", "--steps", "2", "--warmup", "1",
+                         "--min-time", "0.1",
+                         env_extra={"EXACTO_BENCH_WITHHOLD": f"1:{phase}", "EXACTO_DIST_DEADLINE_S": "6"})
+    dt = time.monotonic() - t0
+    assert rc != 0 and line is None
+    assert '"watchdog": "deadline exceeded"' in r.stderr and f'"phase": "{phase}"' in r.stderr, r.stderr[-2000:]
+    assert dt < 150

@@ -14,7 +14,11 @@ n (L + K); a batch that fits one chunk is split in halves over the two lanes):
   cfg3    B = 1024: two 512-product chunks, one per lane;
   cfg1    B = 8192: a 7168-product chunk and a 1024-product chunk, one per lane;
   u64dbfv B = 64 items = 4096 HPS products: four 1152-product chunks (18 items) and a 640-product one;
-  cfg2    B = 16384 polys through ntt_polymul_kernel<12>.
+  cfg2    B = 16384 polys through ntt_polymul_kernel<12>;
+  cfg4    B = 1024 dbfv_mul items (d = 2): 3072 products in six 512-product chunks over two lanes, the
+          psum digit sums of an output limb spanning its item's products;
+  cfg5    B = 8 depth-4 chains at n = 8192 (dbfv_mul_chain_dev, as bench.py calls it); each chain's
+          output has its own digest (block = 1).
 """
 
 import hashlib
@@ -40,6 +44,8 @@ BENCH = {
     "cfg3": (4096, Q3, [], 65537, 1 << 16, None),
     "u64dbfv": (4096, [1152921504606830593], [18014398509998081, 36028797018972161], 1040407, 256,
                 (8, 256, 0)),
+    "cfg4": (4096, Q3, [], 260111, 1 << 16, (2, 256, 65536)),
+    "cfg5": (8192, Q3 + [1152921504606601217], [], 1040407, 256, (8, 256, 0)),
 }
 
 
@@ -56,6 +62,7 @@ def _run(name, chunk=0):
     """The bench's call for BENCH_DIGESTS[name] on cuda:0; returns (spec, output as uint64)."""
     import torch
     spec = _spec(name)
+    assert set(BENCH_DIGESTS[name]) <= set(spec), (name, "digests.json lacks keys of the spec")
     for k, v in BENCH_DIGESTS[name].items():
         assert spec[k] == v, (name, k)
     prm, x, y, rlk = bench_digest_inputs(spec)
@@ -79,9 +86,17 @@ def _run(name, chunk=0):
         ctx.bfv_mul_and_relin_dev(dx, dy, out, B)
     else:
         d, base, dplain = dbfv
-        ctx.dbfv_mul_dev(d, base, dplain, dx, dy, out, B)
+        depth = spec.get("depth", 1)
+        if depth == 1:
+            ctx.dbfv_mul_dev(d, base, dplain, dx, dy, out, B)
+        else:
+            ctx.dbfv_mul_chain_dev(d, base, dplain, dx, dy, out, B, depth)
     ctx.synchronize()
     torch.cuda.synchronize()
+    if dbfv is not None and spec["config"] in ("cfg4", "cfg5"):
+        # the summed-digit key switch stays on: cfg4's two-product limb in the wide basis,
+        # cfg5's up-to-eight-product limbs in the primary one
+        assert ctx.dbfv_key_switch == {"cfg4": 2, "cfg5": 1}[spec["config"]], ctx.dbfv_key_switch
     return spec, out.cpu().numpy().view(np.uint64)
 
 

@@ -9,6 +9,8 @@
   covers the partition and the gather with gloo on CPU).
 """
 
+import os
+
 import numpy as np
 import pytest
 
@@ -80,7 +82,7 @@ def test_rccl_one_rank_broadcast_and_allgather(gpu_available):
         recv = torch.zeros(1000, dtype=torch.int64, device="cuda")
         torch.cuda.synchronize()
         dst.allgather_u64(comm, send, recv, 1000)
-        dst.synchronize()
+        dst.rccl_sync(comm)   # exacto_rccl_sync: the collective's completion under the deadline
         assert torch.equal(gk, g0) and torch.equal(recv, send)
         with pytest.raises(ExactoError):
             dst.broadcast_relin_key(comm, 1, dst.G)   # root out of range
@@ -93,3 +95,32 @@ def test_rccl_one_rank_broadcast_and_allgather(gpu_available):
         assert comm.count() == 1
     finally:
         comm.close()
+
+
+_MISSING_RANK = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["EXACTO_ROOT"])
+from exacto_amd._ffi import ExactoError, RcclComm, rccl_unique_id
+t0 = time.monotonic()
+try:
+    RcclComm(2, rccl_unique_id(), 0, 0)   # rank 1 never joins
+    print("JOINED")
+except ExactoError as e:
+    print("ERR", round(time.monotonic() - t0, 1), str(e))
+sys.stdout.flush()
+os._exit(0)   # the init helper thread is still blocked in RCCL: no interpreter teardown
+"""
+
+
+def test_rccl_comm_init_deadline_when_a_rank_never_joins(gpu_available):
+    """Verdict r5 item 6: a two-rank communicator whose second rank never joins fails with the library's
+    deadline ($EXACTO_RCCL_TIMEOUT_S) instead of blocking forever (in a child process, which ends with
+    os._exit: the abandoned init thread stays blocked in RCCL)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, EXACTO_RCCL_TIMEOUT_S="5", EXACTO_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", _MISSING_RANK], capture_output=True, text=True, timeout=90, env=env)
+    out = r.stdout.strip().splitlines()
+    assert out and out[-1].startswith("ERR"), (r.stdout[-1000:], r.stderr[-1000:])
+    assert "timed out" in out[-1] and float(out[-1].split()[1]) < 30
