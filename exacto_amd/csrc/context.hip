@@ -272,6 +272,8 @@ struct exacto_ctx {
     // product count m with m (p n Q + 2) < P, so that the summed rounding stays liftable from P
     bool psum_env = true;
     int psum_max = 0;
+    int psum_fp_max = 0;         // ... and with |sum| < P / 4, the rounded-float CRT over P (kernels.hip fpc_lift)
+    bool fp_crt = true;          // EXACTO_FP_CRT=0: Garner over P in the SP scale kernels (A/B)
     // HPS: the division-free scale (q > 2^32, p < min(q, 2^32); EXACTO_HPS_LITERAL=1: the literal i128
     // form, kept for the equivalence test) and, in dbfv_mul, the products' c0 / c1 and signed gadget
     // digits summed per output limb before ONE forward NTT + relinearisation MAC per limb
@@ -284,6 +286,7 @@ struct exacto_ctx {
         const int* term_start = nullptr;
         const CombineTerm* terms = nullptr;
         u64* out = nullptr;       // [B][d][2][L][n], coefficient domain
+        bool fpc = false;         // its scale may take the rounded-float CRT over P (m <= psum_fp_max)
     } psum;
     u64* d_hdig = nullptr;       // dBFV over HPS: the summed digits' NTT residues [B][d][G][L][n]
     size_t hdig_cap = 0;
@@ -369,7 +372,12 @@ struct exacto_ctx {
     size_t terms_cap = 0;
     // per-call scratch: the context's own stream-ordered pool (Scratch)
     hipMemPool_t pool = nullptr;
-    bool own_pool = false;   // pool created for this context alone (EXACTO_SCRATCH_POOL=own)
+    // the bootstrap's intermediates (coefficients, flags, the c0'/c1' rows, phase, slots): a persistent
+    // buffer of the boot context, grown like the workspaces, never from the stream-ordered pool
+    u64* boot_buf = nullptr;
+    size_t boot_cap = 0;
+    u64* boot_slots = nullptr;   // ... and the slots of the ring path, grown when an item takes it
+    size_t boot_slots_cap = 0;
     bool debug_scratch = false;
     size_t dbfv_group_bytes = (size_t)16384 << 20;  // dbfv_mul item groups (EXACTO_DBFV_GROUP_MB)
     // profiling
@@ -815,6 +823,27 @@ static int build_tables(exacto_ctx* c) {
             for (int k = 0; k <= L; ++k)
                 set_shoup(C.qpq_w[k][a], C.qpq_ws[k][a], mulmod_h(C.qpref_w[k][L + a], qinv, pa), pa);
         }
+        for (int a = 0; a < K; ++a) {   // the FPC constants (see CrtTables)
+            const u64 pa = pv[a];
+            u64 others = 1;   // (P / p_a) mod p_a
+            for (int b = 0; b < K; ++b)
+                if (b != a) others = mulmod_h(others, pv[b] % pa, pa);
+            const u64 pi = invmod_h(others, pa);
+            C.fpc_pq[a] = mulmod_h(C.pq_w[a], pi, pa);
+            for (int k = 0; k < L; ++k) C.fpc_qpq[k][a] = mulmod_h((pa - C.qpq_w[k][a]) % pa, pi, pa);
+            C.fpc_neg[a] = pi;
+            C.fpc_inv[a] = 1.0 / (double)pa;
+            for (int i = 0; i < L; ++i) {
+                u64 pm = 1 % qv[i];
+                for (int b = 0; b < K; ++b)
+                    if (b != a) pm = mulmod_h(pm, pv[b] % qv[i], qv[i]);
+                C.fpc_pm[a][i] = pm;
+            }
+        }
+        for (int i = 0; i < L; ++i) {
+            const u64 pm = P.mod(qv[i]);
+            C.fpc_negP[i] = pm == 0 ? 0 : qv[i] - pm;
+        }
     }
     {
         const u64 mx = *std::max_element(c->primes.begin(), c->primes.end());
@@ -945,6 +974,13 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
             if (Y.cmp(P) >= 0) break;
             c->psum_max = (int)m;
         }
+        // m (p n Q + 2) <= P / 2, i.e. |R| <= m (p n Q / 2 + 1) <= P / 4: the float CRT is exact
+        for (u64 m = 1; m <= 64; ++m) {
+            Big Y = X;
+            Y.mul(2 * m);
+            if (Y.cmp(P) >= 0) break;
+            c->psum_fp_max = (int)m;
+        }
     }
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) { delete c; return fail(EXACTO_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(e)); }
@@ -956,10 +992,12 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
         // device and shared by every context on it.  Its freed blocks stay mapped for reuse instead of
         // going back to the driver at every synchronisation (release threshold 0 is the default), and
         // the device's default pool keeps its settings for everything else in the process.
-        // One pool per context instead (EXACTO_SCRATCH_POOL=own, rounds 1-4) made the bootstrap's
-        // n = 16 scratch read back zeros written by no kernel of the library in 4 of 20 runs of the
-        // C++ API test, 13 of 20 with destroyed contexts' pools kept alive, and 0 of 20 with one pool
-        // for all contexts (tools/r4_bootab.sh).
+        // One pool per context instead (rounds 1-4; EXACTO_SCRATCH_POOL=own until round 5) made the
+        // bootstrap's n = 16 scratch read back zeros written by no kernel of the library in 4 of 20 runs
+        // of the C++ API test, 13 of 20 with destroyed contexts' pools kept alive, and 0 of 20 with one
+        // pool for all contexts (tools/archive/r4_bootab.sh).  Round 6 removed that mode
+        // ("own" now means the shared pool) and moved the bootstrap's intermediates off the pool.
+        // The release threshold is read back after it is set: a pool that does not keep it is not used.
         // EXACTO_SCRATCH_POOL=default: the device's default pool (threshold raised there), for A/B
         const char* pe = getenv("EXACTO_SCRATCH_POOL");
         const std::string mode = pe ? pe : "shared";
@@ -971,13 +1009,17 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
             props.location.id = device;
             if (hipMemPoolCreate(p, &props) != hipSuccess) return (*p = nullptr, false);
             dbg_alloc_log("hipMemPoolCreate", nullptr, 0, *p, nullptr, false);
-            if (hipMemPoolSetAttribute(*p, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess) return true;
+            uint64_t back = 0;
+            const bool set = hipMemPoolSetAttribute(*p, hipMemPoolAttrReleaseThreshold, &thr) == hipSuccess &&
+                             hipMemPoolGetAttribute(*p, hipMemPoolAttrReleaseThreshold, &back) == hipSuccess;
+            if (dbg_alloc_on())
+                std::fprintf(stderr, "exacto-alloc pool %p device %d release threshold set %s, read back 0x%llx\n",
+                             (void*)*p, device, set ? "ok" : "FAILED", (unsigned long long)back);
+            if (set && back == thr) return true;
             (void)hipMemPoolDestroy(*p);
             return (*p = nullptr, false);
         };
-        if (mode == "own") {
-            c->own_pool = make_pool(&c->pool);
-        } else if (mode != "default") {
+        if (mode != "default") {
             static std::mutex mu;
             static std::map<int, hipMemPool_t> shared;   // never destroyed: lives as long as the process
             std::lock_guard<std::mutex> g(mu);
@@ -1008,6 +1050,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_FP_CRT")) c->fp_crt = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
     c->hps_fast = c->path == EXACTO_PATH_HPS && c->ctq[0] > (1ull << 32) && c->plain < c->ctq[0] &&
@@ -1046,10 +1089,7 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->own_pool && c->pool) {
-        dbg_alloc_log("hipMemPoolDestroy", nullptr, 0, c->pool, nullptr, false);
-        (void)hipMemPoolDestroy(c->pool);
-    }
+    free_dev(c->boot_buf); free_dev(c->boot_slots);
     delete c;
 }
 
@@ -1574,7 +1614,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                                                   : c->ws_D16)
                                    : nullptr,
                                guse, cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
-                               c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8);
+                               c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8, c->fp_crt);
         CHECK_LAUNCH();
         }
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
@@ -1585,7 +1625,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             ProfScope pq(c, PK_PSUM_SCALE, (u64)(cnt / ps.npairs) * ps.d,
                          ib * 2.0 * n * 8.0 * (ps.d * (double)(K + L) + (double)ps.npairs * L));
             if (!launch_psum_scale(c->ws_T, c->ws_extP, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
-                                   ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream))
+                                   ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream, ps.fpc))
                 return fail(EXACTO_ERR_HIP, "internal: psum scale not available for these limbs");
             CHECK_LAUNCH();
         }
@@ -2213,6 +2253,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         c->psum.term_start = c->d_term_start;
         c->psum.terms = c->d_terms;
         c->psum.out = cf;
+        c->psum.fpc = c->fp_crt && m <= c->psum_fp_max;
     }
     bool coef = false;
     if (op.ea) {
@@ -3455,12 +3496,19 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (B == 0) return 0;
     const int n = o->n;
     const long Lbn = (long)b->L * n;
-    StreamRebind one(o, b->stream);   // declared first: destroyed after the scratch blocks are freed
-    // Scratch of the whole call.  A block of o's stream is also read on b's stream (small), so
-    // both streams drain before any block goes back to its pool: `drain` is declared after the
-    // blocks, so its destructor runs first on every return path; the normal path calls finish()
-    // to fold a failed synchronisation (e.g. a kernel fault) into the return code.
-    Scratch coef_s, flags_s, c0pt_s, phase_s, slots_s;
+    StreamRebind one(o, b->stream);
+    // The call's intermediates live in b's persistent buffers (boot_buf: coefficients, flags, the
+    // c0'/c1' rows, phase; boot_slots: the ring path's slots), grown like the workspaces and never
+    // taken from the stream-ordered pool (round 4-5's zeros appeared in pool blocks).
+    // Both streams drain before the call returns (`drain`, on every return path; the normal path calls
+    // finish() to fold a failed synchronisation, e.g. a kernel fault, into the return code).
+    const size_t ctw = 2 * Lbn;
+    const size_t w_coef = 2 * B * 2 * n, w_flags = (B + 1) / 2, w_c0pt = 2 * B * n;
+    {
+        size_t cap = b->boot_cap;
+        if (grow(&b->boot_buf, &cap, (w_coef + w_flags + w_c0pt + ctw) * sizeof(u64))) return EXACTO_ERR_HIP;
+        b->boot_cap = cap;
+    }
     int rc = 0;
     struct Drain {
         exacto_ctx *o, *b;
@@ -3480,11 +3528,8 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     };
     BootDebug dbg(b->stream);
     // 1. to coefficients (o), modulus switch to q' and reduce mod t_boot; c1 == 0 flags
-    ok(coef_s.alloc(2 * B * 2 * n * sizeof(u64), o->stream, o->pool, o->debug_scratch), "alloc");
-    ok(flags_s.alloc(B * sizeof(int), o->stream, o->pool, o->debug_scratch), "alloc");
-    if (rc) return rc;
-    u64* coef = coef_s.as<u64>();
-    int* flags = flags_s.as<int>();
+    u64* coef = b->boot_buf;
+    int* flags = reinterpret_cast<int*>(coef + w_coef);
     u64* small = coef + B * 2 * n;
     dbg.snap("ct", ct, B * 2 * n);
     ok(dev_copy(coef, ct, B * 2 * n * sizeof(u64), o->stream), "copy");
@@ -3503,8 +3548,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     if (rc == 0) ok(hipStreamSynchronize(o->stream), "sync");
     // 2. phase = TrivialEnc(c0') + bsk * c1' (b), written into out
     // [B][n] copies of c0' and c1' rows in the plaintext layout
-    if (rc == 0) ok(c0pt_s.alloc(2 * B * n * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
-    u64* c0pt = c0pt_s.as<u64>();
+    u64* c0pt = coef + w_coef + w_flags;
     u64* c1pt = c0pt + B * n;
     // debug: the library's generic writers (rows / copy / fill kernels) report writes into c0pt and
     // c1pt from here to the end of the call (the rows copies below are the expected ones, kind 0)
@@ -3545,9 +3589,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
     dbg.snap("c0pt", c0pt, B * n);
     dbg.snap("phase_out", out, B * 2 * Lbn);
     // 3. per item: rounding polynomial directly (trivial) or CoeffsToSlots -> g -> SlotsToCoeffs
-    const size_t ctw = 2 * Lbn;
-    if (rc == 0) ok(phase_s.alloc(ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
-    u64* phase = phase_s.as<u64>();
+    u64* phase = c0pt + w_c0pt;
     u64 *slots = nullptr, *rounded = nullptr;
     for (size_t i = 0; i < B && rc == 0; ++i) {
         u64* oi = out + i * ctw;
@@ -3560,9 +3602,12 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
             continue;
         }
         if (!slots) {  // once per call, on the first item that takes the ring path
-            ok(slots_s.alloc(2 * (size_t)n * ctw * sizeof(u64), b->stream, b->pool, b->debug_scratch), "alloc");
+            size_t cap = b->boot_slots_cap;
+            if (b->boot_slots_cap < 2 * (size_t)n * ctw * sizeof(u64)) ok(hipStreamSynchronize(b->stream), "sync");
+            if (rc == 0 && grow(&b->boot_slots, &cap, 2 * (size_t)n * ctw * sizeof(u64))) rc = EXACTO_ERR_HIP;
+            b->boot_slots_cap = cap;
             if (rc) break;
-            slots = slots_s.as<u64>();
+            slots = b->boot_slots;
             rounded = slots + (size_t)n * ctw;
         }
         rc = exacto_extract_coefficients_dev(b, phase, 0, n, elements, E, gks, num_keys, slots);
@@ -3743,7 +3788,8 @@ extern "C" int exacto_prof_read(exacto_ctx* c, int kind, uint64_t* launches, dou
 // The kernels behind one profiled family in the records exacto_prof_read consumed since the last
 // exacto_prof_kernels call for it, as rocprofv3 names them (the demangled kernel symbol without its
 // "void " and parameter list), by descending event time: "name (launches, ms); name (...)".  Returns
-// the length of the full text (like snprintf); buf may be NULL.  The list is cleared by the call.
+// the length of the full text (like snprintf); buf may be NULL (a size query).  A call with a buffer
+// clears the list.
 static std::string kernel_symbol_name(const void* handle) {
     Dl_info info{};
     if (!dladdr(handle, &info) || !info.dli_sname) return "?";
@@ -3769,7 +3815,7 @@ extern "C" size_t exacto_prof_kernels(exacto_ctx* c, int kind, char* buf, size_t
         snprintf(tail, sizeof tail, " (%llu, %.3f ms)", (unsigned long long)kv.second.first, kv.second.second);
         v.emplace_back(kv.second.second, kernel_symbol_name(kv.first) + tail);
     }
-    c->prof_kern.erase(kind);
+    if (buf && len) c->prof_kern.erase(kind);   // a size query (buf NULL) keeps the list
     std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
     std::string out;
     for (auto& e : v) out += (out.empty() ? "" : "; ") + e.second;

@@ -56,6 +56,15 @@ struct CrtTables {
     // folded scale constants: pq[t] = p * Q^-1 mod p_t (aux t), qpq[k][a] = qpref[k][L+a] * Q^-1 mod p_a
     u64 pq_w[EXACTO_MAX_K], pq_ws[EXACTO_MAX_K];
     u64 qpq_w[EXACTO_MAX_L + 1][EXACTO_MAX_K], qpq_ws[EXACTO_MAX_L + 1][EXACTO_MAX_K];
+    // CRT over P by a rounded float sum (the SP scale kernels' FPC form): with Pi_a = (P / p_a)^-1 mod p_a
+    // folded into every constant, each dot product gives y_a = r Pi_a mod p_a directly, and
+    // r = sum_a y_a (P / p_a) - round(sum_a y_a / p_a) P when |r| < P / 4
+    u64 fpc_pq[EXACTO_MAX_K];                    // pq[a] Pi_a
+    u64 fpc_qpq[EXACTO_MAX_L][EXACTO_MAX_K];     // (p_a - qpq[k][a]) Pi_a
+    u64 fpc_neg[EXACTO_MAX_K];                   // Pi_a (the +1 of a negative s)
+    double fpc_inv[EXACTO_MAX_K];                // 1 / p_a
+    u64 fpc_pm[EXACTO_MAX_K][EXACTO_MAX_L];      // (P / p_a) mod q_i
+    u64 fpc_negP[EXACTO_MAX_L];                  // (q_i - P mod q_i) mod q_i
     int near;       // max prime < 2 * min prime: residues move between primes by one conditional subtraction
     int fast;       // near and every prime < 2^60: lazy CRT kernels (unreduced Shoup sums)
     int special;    // fast and every prime is 2^60 - d, d < 2^24: reduce_near60 instead of reduce64
@@ -181,7 +190,7 @@ bool exact_scale_sp_ok(int L, int K, int mode);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false,
-                        bool digits8 = false);
+                        bool digits8 = false, bool fpc = false);
 // D: digits as residues mod q [item][g][n]; D16 (instead): signed int16 (d8: int8) digits [item][g][n].
 // fast: q > 2^32 and p < min(q, 2^32): the division-free form (bit-identical to the literal one)
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, void* D16, bool d8, int guse,
@@ -226,7 +235,7 @@ void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int n
                          const CombineTerm* terms, int L, int K, int n, const PrimeConst* primes, hipStream_t s);
 bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                       hipStream_t s);
+                       hipStream_t s, bool fpc = false);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
 // coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n], int16 or (wide) int32
 // D: int16 digits, or int8 when in8 (base <= 2^8, exact_scale's digits8)

@@ -531,11 +531,44 @@ exact_scale_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride
         gadget_digits<NEAR, LT>(res, L, C, primes, D + item * (long)guse * L * n + j, n, guse);
 }
 
+// FPC: the centred lift of r from P by a rounded float sum instead of Garner over P.  y_a = r Pi_a mod
+// p_a (Pi_a = (P / p_a)^-1 mod p_a, folded into the dot products' constants, so y_a costs what r_a
+// did), X = sum_a y_a (P / p_a) == r (mod P) with X / P = sum_a y_a / p_a, and the centred r is
+// X - round(X / P) P.  Exact whenever |r| < P / 4: X / P is then within 1/4 of an integer, and the
+// fp64 sum of K <= 7 terms y_a * fl(1 / p_a) (each < 1, y_a rounded to 53 bits) is off by < 2^-48.
+// The scale's |r| <= p n Q / 2 + 1 < P / 8 (P > 4 p n Q); a psum of m terms needs m (2 p n Q + 4) <= P
+// (context psum_fp_max).  res_i = sum_a y_a ((P / p_a) mod q_i) + alpha (q_i - P mod q_i), alpha <= K.
+// Replaces K (K - 1) / 2 Shoup products, the digits' comparison with floor(P/2) and their splits.
+template <int LT>
+__device__ __forceinline__ void fpc_lift(const u64 (&y)[LT + 1], u64 (&res)[EXACTO_MAX_L], const CrtTables* __restrict__ C,
+                                         const PrimeConst* __restrict__ primes) {
+    constexpr int L = LT, K = LT + 1;
+    double f = 0.0;
+    uint32_t y0[K], y1[K];
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        f = fma((double)y[a], C->fpc_inv[a], f);
+        y0[a] = (uint32_t)y[a] & M30;
+        y1[a] = (uint32_t)(y[a] >> 30);
+    }
+    const uint32_t alpha = (uint32_t)__double2int_rn(f);   // 0 .. K
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const u64 q = primes[i].q;
+        Dot30 A{0, 0, 0};
+        dot30_mac(A, alpha, 0, C->fpc_negP[i]);
+#pragma unroll
+        for (int a = 0; a < K; ++a) dot30_mac(A, y0[a], y1[a], C->fpc_pm[a][i]);
+        res[i] = dot30_fold(A, q);
+    }
+}
+
 // SP, K = L + 1: exact_scale_kernel with every modular dot product as a 30-bit-limb dot:
 //   r_a = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs        mod p_a   (then Garner over P)
 //   res_i = sum_a w_a (p_0 .. p_{a-1}) + negr (q_i - P mod q_i)    mod q_i
-// and int16 gadget digits by gadget_digits16_sp.
-template <int LT, int DIG>
+// (FPC: y_a = r_a Pi_a by the same dots with folded constants, then fpc_lift), and int16 gadget
+// digits by gadget_digits16_sp.
+template <int LT, int DIG, bool FPC>
 __global__ void __launch_bounds__(TPB)
 exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
                       u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n,
@@ -556,6 +589,20 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
         v0[k] = (uint32_t)v[k] & M30;
         v1[k] = (uint32_t)(v[k] >> 30);
     }
+    u64 res[EXACTO_MAX_L];
+    if constexpr (FPC) {
+        u64 y[K];
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+            const u64 ta = Tin[(long)(L + a) * n];   // [0, 2q): as below
+            Dot30 A{negs ? C->fpc_neg[a] : 0ull, 0, 0};
+            dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->fpc_pq[a]);
+#pragma unroll
+            for (int k = 0; k < L; ++k) dot30_mac(A, v0[k], v1[k], C->fpc_qpq[k][a]);
+            y[a] = dot30_fold(A, primes[L + a].q);
+        }
+        fpc_lift<LT>(y, res, C, primes);
+    } else {
     u64 w[EXACTO_MAX_K];
 #pragma unroll
     for (int a = 0; a < K; ++a) {
@@ -580,7 +627,6 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
         w0[a] = (uint32_t)w[a] & M30;
         w1[a] = (uint32_t)(w[a] >> 30);
     }
-    u64 res[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < L; ++i) {
         const u64 q = primes[i].q;
@@ -588,6 +634,7 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
 #pragma unroll
         for (int a = 0; a < K; ++a) dot30_mac(A, w0[a], w1[a], C->ppref_w[a][i]);
         res[i] = dot30_fold(A, q);
+    }
     }
     if (comp < ncomp_r) {
         u64* out = R + item * r_stride + (long)comp * L * n + j;
@@ -617,7 +664,7 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
 // lifts one r: the context checks m (p n Q + 2) < P (|R| < P / 2, psum_max).  Bit-identical to
 // summing the per-product results mod q_i (dbfv_combine_kernel), which is what it replaces.
 // row = (ib d + k) 2 + c; T as the tensor kernels leave it, Tsum [ib][k][c][a][n] (launch_dbfv_pairsum).
-template <int LT>
+template <int LT, bool FPC>
 __global__ void __launch_bounds__(TPB)
 exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u64* __restrict__ out, int d, int npairs,
                      const int* __restrict__ term_start, const CombineTerm* __restrict__ terms, int n,
@@ -635,7 +682,7 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
         for (int a = 0; a < K; ++a) {
             const u64 ta = Ts[(long)a * n];   // canonical (inverse transform output)
             Dot30 A{0, 0, 0};
-            dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->pq_w[a]);
+            dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), FPC ? C->fpc_pq[a] : C->pq_w[a]);
             carry[a] = dot30_fold(A, primes[L + a].q);
         }
     }
@@ -655,11 +702,20 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
 #pragma unroll
         for (int a = 0; a < K; ++a) {
             const u64 pa = primes[L + a].q;
-            Dot30 A{carry[a] + (negs ? 1ull : 0ull), 0, 0};   // carry < p_a: a0's constant stays < 2^60
+            // carry < p_a: a0's constant stays < 2^60 (FPC: < 2^61, inside dot30_fold's budget)
+            Dot30 A{carry[a] + (negs ? (FPC ? C->fpc_neg[a] : 1ull) : 0ull), 0, 0};
 #pragma unroll
-            for (int kk = 0; kk < L; ++kk) dot30_mac(A, v0[kk], v1[kk], pa - C->qpq_w[kk][a]);
+            for (int kk = 0; kk < L; ++kk) dot30_mac(A, v0[kk], v1[kk], FPC ? C->fpc_qpq[kk][a] : pa - C->qpq_w[kk][a]);
             carry[a] = dot30_fold(A, pa);
         }
+    }
+    u64* o = out + row * L * (long)n + j;
+    if constexpr (FPC) {   // carry[a] = R Pi_a mod p_a
+        u64 res[EXACTO_MAX_L];
+        fpc_lift<LT>(carry, res, C, primes);
+#pragma unroll
+        for (int i = 0; i < L; ++i) o[(long)i * n] = res[i];
+        return;
     }
     u64 w[EXACTO_MAX_K];
 #pragma unroll
@@ -677,7 +733,6 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
         w0[a] = (uint32_t)w[a] & M30;
         w1[a] = (uint32_t)(w[a] >> 30);
     }
-    u64* o = out + row * L * (long)n + j;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
         const u64 q = primes[i].q;
@@ -690,11 +745,16 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
 
 bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                       hipStream_t s) {
+                       hipStream_t s, bool fpc) {
     const long blocks = (long)items_b * d * 2 * blocks_per_row(n);
     if (blocks == 0) return true;
-#define PSUM_(LT) EXACTO_LAUNCH((exact_psum_sp_kernel<LT>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d, npairs, \
-                                     term_start, terms, n, ct, primes)
+#define PSUM_(LT)                                                                                                   \
+    do {                                                                                                            \
+        if (fpc) EXACTO_LAUNCH((exact_psum_sp_kernel<LT, true>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d,    \
+                               npairs, term_start, terms, n, ct, primes);                                          \
+        else EXACTO_LAUNCH((exact_psum_sp_kernel<LT, false>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d,       \
+                           npairs, term_start, terms, n, ct, primes);                                              \
+    } while (0)
     switch (L) {
         case 1: PSUM_(1); break;
         case 2: PSUM_(2); break;
@@ -712,7 +772,7 @@ bool exact_scale_sp_ok(int L, int K, int mode) { return mode == 3 && K == L + 1 
 
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift, bool c2only, bool digits8) {
+                        int K, int mode, hipStream_t s, int gshift, bool c2only, bool digits8, bool fpc) {
     const long blocks = (long)items * (c2only ? 1 : 3) * blocks_per_row(n);
     if (blocks == 0) return;
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
@@ -720,8 +780,12 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
         const int dig = (D16 == nullptr && D == nullptr) || guse <= 0 ? 0
                         : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? (digits8 && gshift <= 8 ? 3 : 1) : 2;
 #define SCALE30_(LT, DG)                                                                                        \
-    EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG>), dim3(blocks), dim3(TPB), 0, s, T, R, r_stride, ncomp_r, D,  \
-                       D16, guse, n, ct, primes, c2only ? 1 : 0)
+    do {                                                                                                        \
+        if (fpc) EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, true>), dim3(blocks), dim3(TPB), 0, s, T, R,      \
+                               r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0);                 \
+        else EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, false>), dim3(blocks), dim3(TPB), 0, s, T, R,         \
+                           r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0);                     \
+    } while (0)
 #define SCALE30(LT)                         \
     do {                                    \
         if (dig == 1) SCALE30_(LT, 1);      \

@@ -561,6 +561,18 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
         }                                                                                        \
     }
 
+// n = 8192: the last exchange (element layout LO = 1 -> LO = 0, a swap of 8 values within each lane
+// pair) by DPP instead of LDS (EXACTO_XCHG_PIN_LP, tools/gen_ntt_asm.py LanePairXchg); the values of
+// the last round then sit in the homes PERM_LP (value 2j in home j, 2j + 1 in home 8 + j).
+#ifndef EXACTO_FWD13_LP
+#define EXACTO_FWD13_LP 1
+#endif
+// position of the value in home h after the last forward round (the stores' order)
+template <int LOGN>
+__device__ constexpr int fwd_pin_value_of_home(int h) {
+    return (LOGN == 13 && EXACTO_FWD13_LP) ? (h < 8 ? 2 * h : 2 * (h - 8) + 1) : h;
+}
+
 // The forward rounds over the pinned homes (canonical inputs, element tid + k T; canonical outputs,
 // element 16 tid + k): fwd_rounds_asm's twiddles and exchanges.
 // SFX_: empty, or _LZ for the last round with outputs in [0, 2q) (NttBatch::lazy_out)
@@ -589,8 +601,13 @@ constexpr int gen_qb() { return LOGN == 10 ? 50 : LOGN == 12 ? 56 : 60; }
         if constexpr (LOGN_ == 13) {                                                             \
             TwPair tw[15];                                                                       \
             load_round_tw<13, 0, 0, 0>(tw, tid_, pin_tab);                                       \
-            PIN_EXCHANGE(lds_, tid_, 1, 0)                                                       \
-            EXACTO_FWD_PIN_13_3##SFX_(tw, pin_K);                                                \
+            if constexpr (EXACTO_FWD13_LP) { /* the exchange within lane pairs, no LDS */        \
+                EXACTO_XCHG_PIN_LP(tid_);                                                        \
+                EXACTO_FWD_PIN_13_3_LP##SFX_(tw, pin_K);                                         \
+            } else {                                                                             \
+                PIN_EXCHANGE(lds_, tid_, 1, 0)                                                   \
+                EXACTO_FWD_PIN_13_3##SFX_(tw, pin_K);                                            \
+            }                                                                                    \
         }                                                                                        \
     }
 
@@ -737,7 +754,10 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
     if constexpr (PROBE == 2) {   // the exchanges of PIN_FWD_ROUNDS without its butterflies
         PIN_EXCHANGE(lds, tid, LOGN - 4, LOGN - 8)
         PIN_EXCHANGE(lds, tid, LOGN - 8, LOGN == 12 ? 0 : 1)
-        if constexpr (LOGN == 13) PIN_EXCHANGE(lds, tid, 1, 0)
+        if constexpr (LOGN == 13) {
+            if constexpr (EXACTO_FWD13_LP) EXACTO_XCHG_PIN_LP(tid);
+            else PIN_EXCHANGE(lds, tid, 1, 0)
+        }
     } else if constexpr (LZO) {
         PIN_FWD_ROUNDS(LOGN, lds, tid, tw_table(P.tw_fwd), make_asmk(q), _LZ)
     } else {
@@ -748,7 +768,7 @@ ntt_fwd_pin_kernel(NttBatch nb1, const PrimeConst* __restrict__ primes, NttBatch
         if (nb.dst_item_stride != -7) return;   // never stored; the compiler cannot drop the work
     }
     const PolyWr rd(dst, N * 8);
-#define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, (k) * T * 8);
+#define PIN_OUT(k) rd.st64(PIN_GET(k), tid * 8, fwd_pin_value_of_home<LOGN>(k) * T * 8);
     PIN_X16(PIN_OUT)
 #undef PIN_OUT
 }

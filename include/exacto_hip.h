@@ -430,7 +430,8 @@ int exacto_prof_read(exacto_ctx* ctx, int kind, uint64_t* launches, double* tota
                      double* total_bytes, uint64_t* polys);
 /* The kernels that ran for one family in the records exacto_prof_read consumed (since the last call for
  * that kind), named as rocprofv3 names them ("exacto::ntt_fwd_pin_kernel<12, 0, false>"), by descending
- * event time: "name (launches, ms); ...".  Returns the full length (snprintf-like); buf may be NULL. */
+ * event time: "name (launches, ms); ...".  Returns the full length (snprintf-like); buf may be NULL (a
+ * size query, which keeps the list; a call with a buffer clears it). */
 size_t exacto_prof_kernels(exacto_ctx* ctx, int kind, char* buf, size_t len);
 const char* exacto_version(void);
 

@@ -35,6 +35,16 @@ def test_rounds_match_exact_arithmetic():
                 asm_sim.check_round_pinned(logn, r, q, rng, approx, lazy_out=True)
 
 
+def test_lane_pair_exchange_and_permuted_last_round():
+    """n = 8192 forward: the last exchange within lane pairs by DPP (EXACTO_XCHG_PIN_LP, two lanes
+    simulated with quad_perm [1, 0, 3, 2]) leaves the LO = 0 layout in the PERM_LP homes, and the last
+    round over those homes (EXACTO_FWD_PIN_13_3_LP[_LZ]) matches exact arithmetic."""
+    rng = random.Random(23)
+    for i in range(40):
+        q = asm_sim.PRIMES[i % len(asm_sim.PRIMES)]
+        asm_sim.check_lane_pair_xchg(rng, q, approx=True, lazy_out=bool(i % 2))
+
+
 def test_generic_rounds_match_exact_arithmetic():
     # FwdRoundGenAsm / InvRoundGenAsm (any q < 2^60) at every size they are emitted for, over the
     # HPS primes of the published configurations and the ends of the range

@@ -10,7 +10,7 @@ test_gpu_psum.py); bit-exact, integer work.
 Not listed (no effect on results): EXACTO_SCRATCH_POOL / EXACTO_DEBUG_SCRATCH / EXACTO_DEBUG_FILL /
 EXACTO_LEAK_CTX (allocation diagnostics, tools/diag.sh), EXACTO_DEBUG_BOOT / EXACTO_DEBUG_WATCH /
 EXACTO_DEBUG_ALLOC (bootstrap snapshots, write watch, allocation log), EXACTO_DBFV_GROUP_MB (tests/test_gpu_psum.py runs it),
-EXACTO_PROF_RAW (profiling arithmetic), EXACTO_RCCL_LIB (library path).
+EXACTO_PROF_RAW (profiling arithmetic), EXACTO_RCCL_LIB (library path), EXACTO_RCCL_TIMEOUT_S (collective deadline).
 """
 
 import json
@@ -44,6 +44,8 @@ VARIANTS = {
     "ks32_lazy_off": ({"EXACTO_KS32_LAZY": "0"}, ["cfg3", "cfg4", "cfg5"]),
     "ks32_wide_primary": ({"EXACTO_KS32_WIDE": "2"}, ["cfg3", "cfg4"]),
     "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
+    # Garner over P instead of the rounded-float CRT in the SP scale and psum kernels
+    "fp_crt_off": ({"EXACTO_FP_CRT": "0"}, ["cfg3", "cfg4", "cfg5"]),
     "dot30_off": ({"EXACTO_DOT30": "0"}, ["cfg3", "cfg5"]),
     "xcd_remap_off": ({"EXACTO_XCD_REMAP": "0"}, ["cfg3", "cfg5"]),
     "mac_lds_off": ({"EXACTO_MAC_LDS": "0"}, ["hps"]),
@@ -83,7 +85,7 @@ def test_every_library_switch_is_covered():
                 found |= set(re.findall(r'(?:getenv|env_switch)\("(EXACTO_[A-Z0-9_]+)"', fh.read()))
     neutral = {"EXACTO_SCRATCH_POOL", "EXACTO_DEBUG_SCRATCH", "EXACTO_DEBUG_FILL", "EXACTO_DBFV_GROUP_MB",
                "EXACTO_PROF_RAW", "EXACTO_RCCL_LIB", "EXACTO_DEBUG_BOOT", "EXACTO_LEAK_CTX",
-               "EXACTO_DEBUG_ALLOC", "EXACTO_DEBUG_WATCH"}
+               "EXACTO_DEBUG_ALLOC", "EXACTO_DEBUG_WATCH", "EXACTO_RCCL_TIMEOUT_S"}
     assert found - neutral == set(SWITCHES), found ^ (set(SWITCHES) | neutral)
 
 

@@ -278,6 +278,77 @@ def check_inv_round_pinned(logn, r, q, rng, approx=True, lazy_out=False):
         assert got[k] < rd.bound_out * q, ("pinned inv bound", logn, r, k, got[k] / q)
 
 
+def check_lane_pair_xchg(rng, q, approx=True, lazy_out=False):
+    """The 8192-point forward's last exchange by DPP (G.LanePairXchg) on a lane pair, then the last
+    round with the permuted homes (G.PERM_LP): the pair's 32 elements end where the LDS exchange
+    (layout LO = 1 -> LO = 0) and the plain last round would leave them, congruent and in bound."""
+    seq = G.LanePairXchg().gen()
+    # element layout LO = 1: lane b (b = 0 even, 1 odd) holds element 2k + b as value k
+    elems = [rng.randrange(16 * q) for _ in range(32)]
+    lanes = []
+    for b in (0, 1):
+        ln = Lane({"tid": [b, 32]})   # %[tid]; only its parity matters
+        for k in range(16):
+            e = elems[2 * k + b]
+            ln.v[G.PIN_BASE + 2 * k] = e & M32
+            ln.v[G.PIN_BASE + 2 * k + 1] = e >> 32
+        lanes.append(ln)
+    for ins in seq:
+        t = ins.text.strip()
+        if t.startswith("s_nop"):
+            continue
+        mnem, _, rest = t.partition(" ")
+        if mnem in ("v_mov_b32_dpp", "v_cndmask_b32_dpp"):
+            # quad_perm [1, 0, 3, 2]: src0 is read from the partner lane, before this instruction writes
+            ops = [o.strip() for o in rest.split(" quad_perm")[0].split(",")]
+            src0 = [ln.rd32(ops[1]) for ln in lanes]
+            for i, ln in enumerate(lanes):
+                part = src0[1 - i]
+                if mnem == "v_mov_b32_dpp":
+                    ln.wr32(ops[0], part)
+                else:   # D = VCC ? src1 : src0(partner)
+                    ln.wr32(ops[0], ln.rd32(ops[2]) if ln.s["vcc"] else part)
+            continue
+        for ln in lanes:
+            if mnem == "v_cmp_eq_u32_e32":
+                ops = [o.strip() for o in rest.split(",")]
+                ln.s["vcc"] = 1 if ln.rd32(ops[1]) == ln.rd32(ops[2]) else 0
+            elif mnem == "v_cndmask_b32_e32":
+                ops = [o.strip() for o in rest.split(",")]
+                ln.wr32(ops[0], ln.rd32(ops[2]) if ln.s["vcc"] else ln.rd32(ops[1]))
+            else:
+                ln.run(t)
+    # layout LO = 0: lane b holds element 16 b + k' as value k', in home PERM_LP[k']
+    for b, ln in enumerate(lanes):
+        for kk in range(16):
+            h = G.PERM_LP[kk]
+            got = ln.v[G.PIN_BASE + 2 * h] | (ln.v[G.PIN_BASE + 2 * h + 1] << 32)
+            assert got == elems[16 * b + kk], ("lane-pair exchange", b, kk)
+    # the permuted last round on each lane
+    rd = G.Round(13, 3, approx, True, pinned=True, lazy_out=lazy_out, perm=G.PERM_LP)
+    rseq = rd.gen()
+    for b, ln in enumerate(lanes):
+        x = [elems[16 * b + kk] for kk in range(16)]
+        tw = [rng.randrange(q) for _ in range(15)]
+        named, _, _ = _named(rd, [0] * 16, tw, q, 13)
+        lane = Lane(named)
+        for kk in range(16):
+            h = G.PERM_LP[kk]
+            lane.v[G.PIN_BASE + 2 * h] = x[kk] & M32
+            lane.v[G.PIN_BASE + 2 * h + 1] = x[kk] >> 32
+        for ins in rseq:
+            lane.run(ins.text)
+        want = [v % q for v in x]
+        for lb, bfs in rd.stages():
+            for k0, k1, slot in bfs:
+                t = want[k1] * tw[slot] % q
+                want[k0], want[k1] = (want[k0] + t) % q, (want[k0] - t) % q
+        for kk in range(16):
+            h = G.PERM_LP[kk]
+            got = lane.v[G.PIN_BASE + 2 * h] | (lane.v[G.PIN_BASE + 2 * h + 1] << 32)
+            assert got % q == want[kk] and got < (2 if lazy_out else 1) * q, ("permuted last round", b, kk)
+
+
 def check_mulpair(w, q, rng, bound=1):
     """MulNear60Asm<w>: r_k == a_k b_k (mod q) and r_k < 2q for a_k, b_k < bound q (extremes
     included; bound 2: the extension transforms' lazy outputs)."""

@@ -301,9 +301,12 @@ class Round(Statement):
     """One forward round (stage bits BHI..LO of a 4-bit window) as one asm statement."""
 
     def __init__(self, logn, r, approx=True, addx=True, pinned=False, generic=False, qbits=60, bound_in=None,
-                 lazy_out=False):
+                 lazy_out=False, perm=None):
         super().__init__()
         self.logn, self.r, self.approx, self.addx, self.pinned = logn, r, approx, addx, pinned
+        # perm (pinned only): value k lives in home perm[k] (the lane-pair exchange leaves the values
+        # of the 8192-point forward's last round there, LanePairXchg)
+        self.perm = perm
         # lazy_out (last round, special primes: the extension transforms that only the asm tensor
         # products read): the final values are left in [0, 2q) after the fold, no canonical step
         self.lazy_out = lazy_out
@@ -356,7 +359,7 @@ class Round(Statement):
 
     def gen(self):
         base = PIN_BASE if self.pinned else VBASE
-        P = [base + 2 * k for k in range(16)]
+        P = [base + 2 * (self.perm[k] if self.perm else k) for k in range(16)]
         TB = base + 32
         # 10 VGPRs per stream: Z (Z.hi stays 0), A (= D = qh), B (then cq - T), E (T), F (cross chain)
         temps = [dict(Z=TB + 10 * j, A=TB + 10 * j + 2, B=TB + 10 * j + 4, E=TB + 10 * j + 6,
@@ -472,9 +475,11 @@ class Round(Statement):
     def emit(self):
         seq = self.gen()
         if self.pinned:
-            return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}{'_LZ' if self.lazy_out else ''}", self, seq,
+            sfx = ("_LP" if self.perm else "") + ("_LZ" if self.lazy_out else "")
+            return emit_pinned(f"EXACTO_FWD_PIN_{self.logn}_{self.r}{sfx}", self, seq,
                                self.vmax,
-                               f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes: "
+                               f"round {self.r} of the {1 << self.logn}-point forward NTT, pinned homes"
+                               f"{' (value k in home PERM_LP[k])' if self.perm else ''}: "
                                f"stage bits {self.bhi}..{self.lo}")
         struct = f"FwdRoundGenAsm<{self.logn}, {self.r}, {self.qbits}>" if self.generic else \
             f"FwdRoundAsm<{self.logn}, {self.r}>"
@@ -484,6 +489,51 @@ class Round(Statement):
                               f"{self.bhi}..{self.lo}, inputs < {self.bound_in}q, "
                               f"{'round-start reduction' if self.reduce_x else 'no round-start reduction'}",
                               "u64 (&x)[16], const TwPair (&tw)[15], const AsmK& K")
+
+
+# The lane-pair exchange (LanePairXchg): value 2j of the last round in home j, value 2j + 1 in home 8 + j
+PERM_LP = [k // 2 + 8 * (k % 2) for k in range(16)]
+
+
+class LanePairXchg(Statement):
+    """The 8192-point forward's last exchange (element layout LO = 1 -> LO = 0) without LDS.  In the
+    LO = 1 layout thread 2s + b holds elements 32 s + 2 k + b (value k); in LO = 0 thread t holds 16 t + k.
+    Both are the 32 elements 32 s .. 32 s + 31 spread over the lane pair (2s, 2s + 1), so the exchange is
+    a swap of 8 values between adjacent lanes: the even lane keeps its values 0..7 (new values 0, 2, ..,
+    14) and takes the odd lane's 0..7 (new 1, 3, .., 15); the odd lane takes the even lane's 8..15
+    (new 0, 2, ..) and keeps its own 8..15 (new 1, 3, ..).  Written in place: new value 2j goes to home j,
+    2j + 1 to home 8 + j (PERM_LP; the last round and the stores read them there).  Per value pair j and
+    32-bit half: T = dpp(home j) (the partner's), home j = even ? home j : dpp(home 8 + j), home 8 + j =
+    even ? T : home 8 + j -- a v_mov_b32_dpp, a v_cndmask_b32_dpp and a v_cndmask_b32 with VCC = the
+    even lanes; quad_perm [1, 0, 3, 2] swaps adjacent lanes.  48 VALU instead of 16 ds_write_b64 + 16
+    ds_read_b64 and two s_barrier."""
+
+    def gen(self):
+        P = [PIN_BASE + 2 * k for k in range(16)]
+        T = PIN_BASE + 32
+        self.vmax = T + 2
+        dpp = "quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        seq = [Ins(f"v_and_b32 {v(T)}, 1, %[tid]"),
+               Ins(f"v_cmp_eq_u32_e32 vcc, 0, {v(T)}"),
+               Ins("s_nop 1", valu=False)]    # VCC and the homes (DPP sources) were written by a VALU
+        for j in range(8):
+            for h in (0, 1):
+                a, b = P[j] + h, P[8 + j] + h
+                seq += [Ins(f"v_mov_b32_dpp {v(T + h)}, {v(a)} {dpp}"),
+                        Ins(f"v_cndmask_b32_dpp {v(a)}, {v(b)}, {v(a)}, vcc {dpp}"),
+                        Ins(f"v_cndmask_b32_e32 {v(b)}, {v(b)}, {v(T + h)}, vcc")]
+        return seq
+
+    def emit(self):
+        seq = self.gen()
+        body = "\\n\\t".join(i.text for i in seq)
+        clob = [f'"v{i}"' for i in range(PIN_BASE + 32, self.vmax)] + ['"vcc"']
+        outs = ", ".join(f'"+v"(xl{k}), "+v"(xh{k})' for k in range(16))
+        valu = sum(1 for i in seq if i.valu)
+        return (f"// the 8192-point forward's last exchange within lane pairs (DPP), {valu} VALU\n"
+                f"#define EXACTO_XCHG_PIN_LP(TID) \\\n"
+                f"    asm volatile(\"{body}\" \\\n        : {outs} \\\n        : [tid] \"v\"(TID) \\\n"
+                f"        : {', '.join(clob)})\n")
 
 
 class InvRound(Statement):
@@ -941,6 +991,12 @@ def main():
         # the extension transforms' last round, outputs in [0, 2q)
         parts.append(Round(logn, (logn + 3) // 4 - 1, approx, True, pinned=True, lazy_out=True).emit())
         parts.append("\n")
+        if logn == 13:   # the last round after the lane-pair exchange (EXACTO_FWD13_LP)
+            parts.append(LanePairXchg().emit())
+            parts.append("\n")
+            for lz in (False, True):
+                parts.append(Round(13, 3, approx, True, pinned=True, lazy_out=lz, perm=PERM_LP).emit())
+                parts.append("\n")
         for rd in inv_rounds_pinned(logn, approx):
             parts.append(InvRoundPinned(logn, rd.r, rd.bound_in, approx).emit())
             parts.append("\n")
