@@ -316,6 +316,13 @@ struct exacto_ctx {
     bool dual = true;
     int lanes = 2;
     hipEvent_t ev_fork = nullptr;
+    // dBFV chains of two or more items run as two halves on two streams (exacto_dbfv_mul_chain_dev):
+    // the second half on a twin context (same parameters, its own stream and workspaces, a copy of
+    // the relinearisation key), so each half's whole chain overlaps the other's
+    exacto_ctx* twin = nullptr;
+    bool chain_split = true;         // EXACTO_CHAIN_SPLIT=0: one stream for the whole batch
+    unsigned rlk_version = 0, twin_rlk_version = ~0u;
+    hipEvent_t ev_twin_in = nullptr, ev_twin_out = nullptr;
     LaneSet xl[EXACTO_MAX_LANES - 1];   // lanes 1 .. lanes-1
     // dBFV: per-ciphertext extensions shared by the products that use the ciphertext
     // (EXACTO_SHARE_EXT=0 recomputes them per product)
@@ -1050,6 +1057,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_DIGIT16")) c->digit16 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_KS32")) c->ks32 = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_CHAIN_SPLIT")) c->chain_split = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_FP_CRT")) c->fp_crt = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
@@ -1087,6 +1095,9 @@ extern "C" void exacto_ctx_destroy(exacto_ctx* c) {
     free_dev(c->kw.d_p32); free_dev(c->kw.d_tw32); free_dev(c->kw.d_kst); free_dev(c->kw.d_rs);
     free_dev(c->ws_DS); free_dev(c->ws_U);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->twin) exacto_ctx_destroy(c->twin);
+    if (c->ev_twin_in) (void)hipEventDestroy(c->ev_twin_in);
+    if (c->ev_twin_out) (void)hipEventDestroy(c->ev_twin_out);
     free_dev(c->io); free_dev(c->prod); free_dev(c->d_off); free_dev(c->d_term_start); free_dev(c->d_terms);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
     free_dev(c->boot_buf); free_dev(c->boot_slots);
@@ -1147,6 +1158,7 @@ extern "C" uint64_t* exacto_ctx_relin_key_buffer(exacto_ctx* c, size_t num_keys)
     c->rlk_loaded = true;
     c->rlk_s_valid = false;  // contents change: companions recomputed before first use
     c->rs_valid = false; c->kw.rs_valid = false;     // and the auxiliary-basis key
+    ++c->rlk_version;
     return c->d_rlk;
 }
 
@@ -2518,10 +2530,56 @@ extern "C" int exacto_dbfv_decrypt_poly(exacto_ctx* c, size_t d, uint64_t base, 
 // chain of bfv_host.rs:258-288 without its bootstrap): acc <- dbfv_mul(acc, y) `depth` times,
 // both mul_depth reset to 0 before every step; intermediates ping-pong between two
 // context-owned device buffers and never leave HBM.
+// The twin of a context (its second chain stream): created on first use with the same parameters
+// and chunking, its own stream, workspaces and scratch; the relinearisation key is copied from the
+// context whenever it changed since (rlk_version), ordered after everything on the context's stream.
+static int ensure_twin(exacto_ctx* c) {
+    if (!c->twin) {
+        exacto_ctx* t = nullptr;
+        if (int e = exacto_ctx_create(&t, c->n, c->ctq.data(), c->L, c->user_aux.empty() ? nullptr : c->user_aux.data(),
+                                      c->user_aux.size(), c->plain, c->gbase, c->device))
+            return e;
+        t->chain_split = false;
+        t->chunk = c->chunk;
+        c->twin = t;
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_twin_in, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_twin_out, hipEventDisableTiming));
+    }
+    exacto_ctx* t = c->twin;
+    t->chunk = c->chunk;
+    HIP_TRY(hipEventRecord(c->ev_twin_in, c->stream));
+    HIP_TRY(hipStreamWaitEvent(t->stream, c->ev_twin_in, 0));
+    if (c->twin_rlk_version != c->rlk_version) {
+        if (int e = exacto_ctx_load_relin_key_dev(t, c->d_rlk, c->rlk_keys)) return e;
+        c->twin_rlk_version = c->rlk_version;
+    }
+    return 0;
+}
+
+static int dbfv_chain_one(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* x,
+                          const uint64_t* y, uint64_t* out, size_t B, size_t depth);
+
 extern "C" int exacto_dbfv_mul_chain_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
                                          const uint64_t* x, const uint64_t* y, uint64_t* out, size_t B,
                                          size_t depth) {
     if (int e = check_ctx(c)) return e;
+    // two halves on two streams: items are independent, so each half's chain is the chain of those
+    // items (bit-identical: tests/test_gpu_chain.py against EXACTO_CHAIN_SPLIT=0)
+    if (c->chain_split && c->dual && !c->prof && B >= 2 && depth >= 1 && c->rlk_loaded && !c->deferred_code) {
+        if (int e = dbfv_params_check(d, base, plain)) return e;
+        if (int e = ensure_twin(c)) return e;
+        const size_t B0 = (B + 1) / 2, w = d * 2 * c->L * (size_t)c->n;
+        const int r1 = dbfv_chain_one(c->twin, d, base, plain, x + B0 * w, y + B0 * w, out + B0 * w, B - B0, depth);
+        const int r0 = dbfv_chain_one(c, d, base, plain, x, y, out, B0, depth);
+        HIP_TRY(hipEventRecord(c->ev_twin_out, c->twin->stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_twin_out, 0));
+        return r0 ? r0 : r1;   // (the last error message is the failing call's)
+    }
+    return dbfv_chain_one(c, d, base, plain, x, y, out, B, depth);
+}
+
+static int dbfv_chain_one(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* x,
+                          const uint64_t* y, uint64_t* out, size_t B, size_t depth) {
     const size_t bytes = B * d * 2 * c->L * poly_bytes(c);
     if (depth == 0) {
         if (B && out != x) HIP_TRY(dev_copy(out, x, bytes, c->stream));
@@ -2702,6 +2760,7 @@ extern "C" int exacto_gen_relin_key_dev(exacto_ctx* c, const uint64_t* sk, doubl
         c->rlk_loaded = true;
         c->rlk_s_valid = false;
         c->rs_valid = false; c->kw.rs_valid = false;
+        ++c->rlk_version;
     }
     return 0;
 }

@@ -1392,7 +1392,8 @@ void launch_inv_tensor(const Operands& op, const u64* extP, u64* T, int items, i
                        bool lazy_out) {
     // prime-major block order needs whole dBFV items in the launch (tensor_block)
     // (measured: cfg5, 36 products per item, tensor 270 -> 261 us; cfg4's 3 products per item and
-    // u64_dbfv within noise: applied from 8 products per item)
+    // u64_dbfv within noise: applied from 8 products per item; round 6 again at cfg4:
+    // tensor 140 -> 143-147 us, 185.6k vs 185.1k/s)
     if (share_np < 8 || items % share_np != 0) share_np = 0;
     const long blocks = (long)items * 3 * (L + K);
     if (blocks == 0) return;

@@ -6,7 +6,8 @@ Case groups:
   cfg3    bfv_mul_and_relin, n = 4096, 3 limbs (forward, inverse, tensor, ks32 key switch), 160
           products in pipeline chunks of 64 (three chunks: both lanes, or three with EXACTO_LANES=3)
   cfg4    dbfv_mul d = 2 (n = 4096, 3 limbs: psum, the wide 31-bit basis for int32 digit sums)
-  cfg5    dbfv_mul and a depth-2 chain (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels)
+  cfg5    dbfv_mul and a depth-2 chain of 3 items (n = 8192, 4 limbs: psum, the n = 8192 tensor kernels,
+          the chain split over two streams)
   hps     compact_bfv products (one aux prime) and a u64_dbfv dbfv_mul (two aux primes, digit sums)
   polymul the fused NTT product at n = 4096 / 8192, out of place and in place on b
 """
@@ -64,8 +65,9 @@ def cfg5(out):
     prm5 = dp.bfv_params
     q5, d = prm5.ct_basis.moduli, dp.num_digits
     rng = np.random.default_rng(7002)
-    a = uniform_residues(rng, (1, d, 2), q5, 8192)
-    b = uniform_residues(rng, (1, d, 2), q5, 8192)
+    # three items: the chain batch splits 2 + 1 over the context and its twin (EXACTO_CHAIN_SPLIT)
+    a = uniform_residues(rng, (3, d, 2), q5, 8192)
+    b = uniform_residues(rng, (3, d, 2), q5, 8192)
     rlk5 = uniform_residues(rng, (prm5.gadget_digits, 2), q5, 8192)
     ctx5 = HipContext.from_params(prm5)
     ctx5.load_relin_key(rlk5)
