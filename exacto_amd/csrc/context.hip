@@ -2394,6 +2394,8 @@ static int dbfv_mul_core(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain,
     return 0;
 }
 
+static int ensure_twin(exacto_ctx* c);
+
 extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain, const uint64_t* a,
                                    const uint64_t* b, uint64_t* out, size_t B, const uint32_t* depth_a,
                                    const uint32_t* depth_b, uint32_t* depth_out) {
@@ -2407,7 +2409,18 @@ extern "C" int exacto_dbfv_mul_dev(exacto_ctx* c, size_t d, uint64_t base, uint6
                                                     "ciphertext-level lattice reduction (paper §4.6.2)");
     }
     if (B == 0) return 0;
-    if (int e = dbfv_mul_core(c, d, base, plain, a, b, out, B, false)) return e;
+    if (c->chain_split && c->dual && !c->prof && B >= 2 && c->rlk_loaded && !c->deferred_code) {
+        // two halves on two streams, as the chain (exacto_dbfv_mul_chain_dev)
+        if (int e = ensure_twin(c)) return e;
+        const size_t B0 = (B + 1) / 2, w = d * 2 * c->L * (size_t)c->n;
+        const int r1 = dbfv_mul_core(c->twin, d, base, plain, a + B0 * w, b + B0 * w, out + B0 * w, B - B0, false);
+        const int r0 = dbfv_mul_core(c, d, base, plain, a, b, out, B0, false);
+        HIP_TRY(hipEventRecord(c->ev_twin_out, c->twin->stream));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_twin_out, 0));
+        if (int e = r0 ? r0 : r1) return e;
+    } else if (int e = dbfv_mul_core(c, d, base, plain, a, b, out, B, false)) {
+        return e;
+    }
     if (depth_out)
         for (size_t i = 0; i < B; ++i) depth_out[i] = 1;
     return 0;

@@ -10,7 +10,7 @@ mkdir -p $O
 cd $R
 if [ "$PYTEST_K" != "skip" ]; then
   K=(); [ -n "$PYTEST_K" ] && K=(-k "$PYTEST_K")
-  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread "${K[@]}" > $O/pytest.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread "${K[@]}" > $O/pytest.log 2>&1
   rc=$?; echo "gpu suite rc=$rc"; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 fi
 for c in "$@"; do
