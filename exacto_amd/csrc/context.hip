@@ -3635,7 +3635,7 @@ extern "C" int exacto_bfv_bootstrap_dev(exacto_ctx* o, exacto_ctx* b, const uint
         return (uint32_t*)nullptr;
     }();
     uint32_t* whit = dbg.on ? dbg.whit : watch_hit;
-    if (whit && rc == 0) debug_watch_set(c0pt, c0pt + 2 * B * n, whit);
+    if (whit && rc == 0) debug_watch_set(c0pt, c0pt + 2 * B * n, whit, b->stream);
     dbg.snap("small_again", small, B * 2 * n);
     dbg.xsnap("small", small);
     dbg.xsnap("c0pt_before", c0pt);

@@ -205,8 +205,9 @@ void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s);
 void launch_xcd_probe(const u64* src, u64* dst, long words, uint32_t* xcc, int blocks, hipStream_t s);
 void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s);
 // EXACTO_DEBUG_BOOT: watch a byte range for writes by rows / copy / fill (kernels.hip DbgWatch); hit: a
-// device buffer of 8 words, kind k set to 1 on a write inside [lo, hi)
-void debug_watch_set(const void* lo, const void* hi, uint32_t* hit);
+// device buffer of 8 words, kind k set to 1 on a write inside [lo, hi); only launches on stream s from
+// the calling host thread get it
+void debug_watch_set(const void* lo, const void* hi, uint32_t* hit, hipStream_t s = nullptr);
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
                       int guse, u64* out, long out_stride, int items, int n, int L, const PrimeConst* primes,
                       hipStream_t s);

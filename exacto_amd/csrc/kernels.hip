@@ -1292,17 +1292,22 @@ relin_mac_lds_kernel(const u64* __restrict__ base, long base_stride, const u64* 
 struct DbgWatch {
     u64 lo = 0, hi = 0;
     uint32_t* hit = nullptr;
+    hipStream_t stream = nullptr;   // only launches on this stream get the watch
 };
-static DbgWatch g_watch;   // host side, read by the launchers below
+// host side, read by the launchers below: per host thread, and applied only to launches on the stream
+// the bootstrap call registered (another context, thread or device never receives its hit pointer)
+static thread_local DbgWatch g_watch;
+static DbgWatch watch_for(hipStream_t s) { return (g_watch.hit && s == g_watch.stream) ? g_watch : DbgWatch{}; }
 __device__ __forceinline__ void dbg_watch(const void* a, int kind, u64 lo, u64 hi, uint32_t* hit) {
     const u64 x = (u64)a;
     if (x >= lo && x < hi) hit[kind] = 1;
 }
 
-void debug_watch_set(const void* lo, const void* hi, uint32_t* hit) {
+void debug_watch_set(const void* lo, const void* hi, uint32_t* hit, hipStream_t s) {
     g_watch.lo = (u64)lo;
     g_watch.hi = (u64)hi;
     g_watch.hit = hit;
+    g_watch.stream = s;
 }
 
 __global__ void __launch_bounds__(TPB)
@@ -1333,8 +1338,9 @@ void launch_rows(u64* dst, long dst_stride, const u64* src, long src_stride, lon
     const long total = len * rows;
     if (total <= 0) return;
     const long blocks = std::min<long>((total + TPB - 1) / TPB, 65536);
+    const DbgWatch w = watch_for(s);
     EXACTO_LAUNCH(rows_kernel, dim3((unsigned)blocks), dim3(TPB), 0, s, dst, dst_stride, src, src_stride, len,
-                       total, g_watch.lo, g_watch.hi, g_watch.hit);
+                       total, w.lo, w.hi, w.hit);
 }
 
 void launch_relin_mac(const u64* base, long base_stride, const u64* D, const u64* rlk, const u64* rlk_s,
@@ -1470,8 +1476,8 @@ void launch_copy_u64(u64* dst, const u64* src, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    EXACTO_LAUNCH(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words, g_watch.lo, g_watch.hi,
-                       g_watch.hit);
+    const DbgWatch w = watch_for(s);
+    EXACTO_LAUNCH(copy_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, words, w.lo, w.hi, w.hit);
 }
 
 
@@ -1488,8 +1494,8 @@ void launch_fill_u32(uint32_t* dst, uint32_t v, long words, hipStream_t s) {
     if (words <= 0) return;
     long blocks = (words + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    EXACTO_LAUNCH(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words, g_watch.lo, g_watch.hi,
-                       g_watch.hit);
+    const DbgWatch w = watch_for(s);
+    EXACTO_LAUNCH(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, v, words, w.lo, w.hi, w.hit);
 }
 
 }  // namespace exacto
