@@ -1428,6 +1428,9 @@ static int ks32_convert_key(exacto_ctx* c, const u64* key, size_t keys, uint32_t
     return 0;
 }
 
+#ifndef EXACTO_KN_NORM
+#define EXACTO_KN_NORM 1   // the narrow basis' digit-sum limit from the key's norms too (A/B build switch)
+#endif
 // The primary basis for the resident key: the lazy one (kz) when the key's own norms bound the key
 // switch, |u_{c,l}| <= (B/2) sum_g ||r_{g,c,l}||_1 with ||r||_1 <= (sum floor(|r_j|/2^20) + n) 2^20
 // (ks32_key_norm_kernel), for every (c, l): prod p > 2 m bound for m = 1 (and sum_max = the largest
@@ -1460,7 +1463,7 @@ static int ks32_select_basis(exacto_ctx* c) {
         if (acc.cmp(worst) > 0) worst = acc;
     }
     worst.mul(c->gbase / 2);
-    int sm = 0;
+    int sm = 0, snm = 0;   // sums the lazy / the narrow basis lift for this key (its norms, not the analytic bound)
     for (u64 m = 1; m <= 64; ++m) {
         Big bm = worst;
         bm.mul(2 * m);
@@ -1468,9 +1471,20 @@ static int ks32_select_basis(exacto_ctx* c) {
         if (c->kz.P.cmp(bm) <= 0) break;
         sm = (int)m;
     }
+    for (u64 m = 1; m <= 64 && EXACTO_KN_NORM; ++m) {
+        Big bm = worst;
+        bm.mul(2 * m);
+        bm.add(1);
+        if (c->kn.P.cmp(bm) <= 0) break;
+        snm = (int)m;
+    }
+    // the narrow basis with the key's own bound: cfg4's two-product digit sums (2^90.6) fit its 2^91.2,
+    // which the analytic bound (2^91.6) refused -- they then take the narrow form instead of the wide one
+    c->ks32_sum_max = std::max(c->kn.sum_max, snm);
+    const int kn_sum = c->ks32_sum_max;
     // never a basis that lifts fewer sums than the narrow one where those sums are needed (a dBFV digit
     // sum the lazy basis cannot hold would otherwise drop to the per-product key switch)
-    if (sm >= 1 && sm >= std::min(c->kn.sum_max, std::max(1, c->ks32_need_m))) {
+    if (sm >= 1 && sm >= std::min(kn_sum, std::max(1, c->ks32_need_m))) {
         c->kz.sum_max = sm;
         use_ks32_basis(c, c->kz);
     }
@@ -2192,7 +2206,7 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
     if (m > c->ks32_need_m) {
         c->ks32_need_m = m;
         // a key already on the lazy basis that cannot lift these sums while the narrow one can: re-select
-        if (c->rs_valid && c->ks32_lazy_active && m > c->ks32_sum_max && m <= c->kn.sum_max) c->rs_valid = false;
+        if (c->rs_valid && c->ks32_lazy_active && m > c->ks32_sum_max) c->rs_valid = false;
     }
     if (c->S32 > 0 && c->ks32 && c->rlk_loaded && gu > 0)
         if (int e = ensure_rs(c)) return e;

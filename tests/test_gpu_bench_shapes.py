@@ -94,9 +94,10 @@ def _run(name, chunk=0):
     ctx.synchronize()
     torch.cuda.synchronize()
     if dbfv is not None and spec["config"] in ("cfg4", "cfg5"):
-        # the summed-digit key switch stays on: cfg4's two-product limb in the wide basis,
-        # cfg5's up-to-eight-product limbs in the primary one
-        assert ctx.dbfv_key_switch == {"cfg4": 2, "cfg5": 1}[spec["config"]], ctx.dbfv_key_switch
+        # the summed-digit key switch stays on, in the primary basis: cfg4's two-product
+        # limbs in the narrow basis (bounded by the key's norms), cfg5's up-to-eight-product limbs in
+        # the lazy one
+        assert ctx.dbfv_key_switch == 1, ctx.dbfv_key_switch
     return spec, out.cpu().numpy().view(np.uint64)
 
 
