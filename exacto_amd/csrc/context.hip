@@ -193,6 +193,7 @@ struct ProfRec {
 struct Ks32Basis {
     int S = 0;
     int sum_max = 0;              // dBFV key-switch sums the basis lifts exactly
+    int fpc_max = 0;              // ... and by the float-CRT lift (ks32_fpc_one's margin; S <= 3 or p < 2^32 / 3)
     int mac_form = 0;             // ks32_mac: 0 primes up to 2^31 (7 products per reduction),
                                   // 1 below 2^32 / 3 (12), 2 below 2^30 (12, lazy transforms)
     Big P;                        // product of the primes
@@ -245,6 +246,8 @@ struct exacto_ctx {
     bool ks32 = true;
     int S32 = 0;                 // 0: not eligible for these parameters
     int ks32_sum_max = 0;        // key-switch sums that may be added before one lift (prod p bound)
+    int ks32_fpc_max = 0;        // ... that the active basis' float-CRT lift takes (Ks32Basis::fpc_max)
+    bool ks_fpc = true;          // EXACTO_KS_FPC=0: the Garner lift in ks32_crt always (A/B)
     int ks32_mac_form = 0;       // ks32_mac's reduction form for the active basis (Ks32Basis::mac_form)
     Ks32Basis kw;                // wide basis (primes up to 2^31) for dBFV digit sums the primary cannot hold
     // The primary basis is one of two, chosen per relinearisation key (ensure_rs):
@@ -255,8 +258,8 @@ struct exacto_ctx {
     // S32 / d_p32 / d_tw32 / d_kst / ks32_sum_max / ks32_mac_form describe the active one.
     Ks32Basis kn, kz;
     bool ks32_lazy_active = false;
-    int ks32_need_m = 1;
-    int last_dbfv_ks = -1;        // exacto_ctx_info.dbfv_key_switch          // the most key-switch sums per output limb a dbfv_mul of this context asked for
+    int ks32_need_m = 1;          // the most key-switch sums per output limb a dbfv_mul of this context asked for
+    int last_dbfv_ks = -1;        // exacto_ctx_info.dbfv_key_switch
     // a dBFV pass with shared extensions: d and its products per item (0: plain BFV products), for
     // run_inv_tensor's algorithmic bytes and the tensor kernels' prime-major block order
     int tensor_share_d = 0, tensor_share_npairs = 0;
@@ -546,6 +549,24 @@ static void set_shoup(u64& w, u64& ws, u64 v, u64 q) {
     ws = shoup_h(v, q);
 }
 
+// The largest m <= 64 with prod p > 2 m `one` + 1: the centred lift of a sum of m terms, each at most
+// `one` in magnitude, is exact.  fpc: with the float-CRT lift's margin, prod p 2^20 > (2 m one + 1)
+// (2^20 + 1), so |u| / P < 1/2 - 2^-21 against the float sum's error below 2^-48 (ks32_fpc_one).
+static int sums_lifted(const Big& P, const Big& one, bool fpc) {
+    Big pf = P;
+    if (fpc) pf.mul(1ull << 20);
+    int r = 0;
+    for (u64 m = 1; m <= 64; ++m) {
+        Big bm = one;
+        bm.mul(2 * m);
+        bm.add(1);
+        if (fpc) bm.mul((1ull << 20) + 1);
+        if (pf.cmp(bm) <= 0) break;
+        r = (int)m;
+    }
+    return r;
+}
+
 // ks32.hip's auxiliary basis: the fewest primes p == 1 mod 2n in (2^30, 2^31), largest first, with
 // prod p > 2 G n floor(B/2) floor(q_max/2) (the magnitude bound of sum_g d_g * r_g, digits balanced
 // in [-B/2, B/2), key coefficients balanced).  Eligible: exact path, gadget base <= 2^16 (int16
@@ -579,16 +600,14 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
     }
     b->mac_form = lazy ? 2 : narrow ? 1 : 0;
     b->P = P;
-    b->sum_max = fixedS ? 0 : 1;
-    for (u64 m = 2; m <= 64 && !fixedS; ++m) {
-        Big bm((u64)c->G);
-        bm.mul((u64)c->n);
-        bm.mul(c->gbase / 2);
-        bm.mul(qmax / 2);
-        bm.mul(2 * m);
-        bm.add(1);
-        if (P.cmp(bm) <= 0) break;
-        b->sum_max = (int)m;
+    b->sum_max = b->fpc_max = 0;
+    if (!fixedS) {   // the lazy basis' limits come from the resident key (ks32_select_basis)
+        Big one((u64)c->G);
+        one.mul((u64)c->n);
+        one.mul(c->gbase / 2);
+        one.mul(qmax / 2);
+        b->sum_max = std::max(1, sums_lifted(P, one, false));   // P > bound was checked above
+        b->fpc_max = ps.size() <= 3 || narrow ? sums_lifted(P, one, true) : 0;   // ks32_crt's condition
     }
     const int S = (int)ps.size(), n = c->n;
     std::vector<uint2> tw((size_t)S * 2 * n);
@@ -616,6 +635,17 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
         Q.c32s = sh32(c32, p);
         const u64 m63 = (1ull << 63) % p;
         Q.k63 = (uint32_t)(m63 == 0 ? 0 : p - m63);
+        // the float-CRT lift's factor pi = (P / p)^-1 mod p folded into the last inverse stage
+        u64 pi = 1;
+        for (int k = 0; k < (int)ps.size(); ++k)
+            if (k != s) pi = mulmod_h(pi, ps[k] % p, p);
+        pi = invmod_h(pi, p);
+        const u64 fni = mulmod_h(ninv, pi, p), flw = mulmod_h(lw, pi, p);
+        Q.fn_inv = (uint32_t)fni;
+        Q.fn_inv_s = sh32(fni, p);
+        Q.flast_w = (uint32_t)flw;
+        Q.flast_ws = sh32(flw, p);
+        Q.inv_p = 1.0 / (double)p;
     }
     HIP_TRY(dev_alloc((void**)&b->d_tw32, tw.size() * sizeof(uint2)));
     if (int e_ = upload(c, b->d_tw32, tw.data(), tw.size() * sizeof(uint2))) return e_;
@@ -651,6 +681,16 @@ static int build_ks32_basis_impl(exacto_ctx* c, u64 pmax, u64 qmax, const Big& b
         }
         const u64 pm = P.mod(q);
         T.negP[l] = pm == 0 ? 0 : q - pm;
+        constexpr u64 M30 = (1ull << 30) - 1;
+        for (int s = 0; s < S; ++s) {
+            u64 cs = 1;   // (P / p_s) mod q
+            for (int k = 0; k < S; ++k)
+                if (k != s) cs = mulmod_h(cs, ps[k] % q, q);
+            T.fpc_c[l][s][0] = (uint32_t)(cs & M30);
+            T.fpc_c[l][s][1] = (uint32_t)(cs >> 30);
+        }
+        T.fpc_n[l][0] = (uint32_t)(T.negP[l] & M30);
+        T.fpc_n[l][1] = (uint32_t)(T.negP[l] >> 30);
     }
     HIP_TRY(dev_alloc((void**)&b->d_kst, sizeof(Ks32Tables)));
     if (int e_ = upload(c, b->d_kst, &T, sizeof(Ks32Tables))) return e_;
@@ -665,6 +705,7 @@ static void use_ks32_basis(exacto_ctx* c, const Ks32Basis& b) {
     c->d_tw32 = b.d_tw32;
     c->d_kst = b.d_kst;
     c->ks32_sum_max = b.sum_max;
+    c->ks32_fpc_max = b.fpc_max;
     c->ks32_mac_form = b.mac_form;
     c->ks32_lazy_active = &b == &c->kz;
 }
@@ -1060,6 +1101,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_CHAIN_SPLIT")) c->batch_split = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_FP_CRT")) c->fp_crt = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_KS_FPC")) c->ks_fpc = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
     c->hps_fast = c->path == EXACTO_PATH_HPS && c->ctq[0] > (1ull << 32) && c->plain < c->ctq[0] &&
@@ -1463,29 +1505,22 @@ static int ks32_select_basis(exacto_ctx* c) {
         if (acc.cmp(worst) > 0) worst = acc;
     }
     worst.mul(c->gbase / 2);
-    int sm = 0, snm = 0;   // sums the lazy / the narrow basis lift for this key (its norms, not the analytic bound)
-    for (u64 m = 1; m <= 64; ++m) {
-        Big bm = worst;
-        bm.mul(2 * m);
-        bm.add(1);
-        if (c->kz.P.cmp(bm) <= 0) break;
-        sm = (int)m;
-    }
-    for (u64 m = 1; m <= 64 && EXACTO_KN_NORM; ++m) {
-        Big bm = worst;
-        bm.mul(2 * m);
-        bm.add(1);
-        if (c->kn.P.cmp(bm) <= 0) break;
-        snm = (int)m;
-    }
+    // sums the lazy / the narrow basis lift for this key (its norms, not the analytic bound), by the
+    // Garner and by the float-CRT lift
+    const int sm = sums_lifted(c->kz.P, worst, false);
+    const int snm = EXACTO_KN_NORM ? sums_lifted(c->kn.P, worst, false) : 0;
+    const int fsm = sums_lifted(c->kz.P, worst, true);   // lazy and narrow primes: any S (ks32_crt)
+    const int fsnm = EXACTO_KN_NORM && (c->kn.S <= 3 || c->kn.mac_form != 0) ? sums_lifted(c->kn.P, worst, true) : 0;
     // the narrow basis with the key's own bound: cfg4's two-product digit sums (2^90.6) fit its 2^91.2,
     // which the analytic bound (2^91.6) refused -- they then take the narrow form instead of the wide one
     c->ks32_sum_max = std::max(c->kn.sum_max, snm);
+    c->ks32_fpc_max = std::max(c->kn.fpc_max, fsnm);
     const int kn_sum = c->ks32_sum_max;
     // never a basis that lifts fewer sums than the narrow one where those sums are needed (a dBFV digit
     // sum the lazy basis cannot hold would otherwise drop to the per-product key switch)
     if (sm >= 1 && sm >= std::min(kn_sum, std::max(1, c->ks32_need_m))) {
         c->kz.sum_max = sm;
+        c->kz.fpc_max = fsm;
         use_ks32_basis(c, c->kz);
     }
     return 0;
@@ -1679,7 +1714,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                 {   // per (item, component, limb): S 31-bit sums in, R in and out
                     ProfScope pc(c, PK_KS_CRT, (u64)cnt * 2 * L, (double)n * cnt * 2 * L * (4.0 * c->S32 + 16.0));
                     ks32_crt(c->ws_U, R, out_stride, cnt, L, c->S32, c->logn, c->d_kst, c->d_p32, c->d_primes, c->ks32_mac_form,
-                             c->stream);
+                             c->stream, c->ks_fpc && c->ks32_fpc_max >= 1);
                 }
                 CHECK_LAUNCH();
             }
@@ -2322,7 +2357,9 @@ static int dbfv_mul_group(exacto_ctx* c, size_t d, uint64_t base, uint64_t plain
         }
         {
             ProfScope pc(c, PK_KS_CRT, (u64)Bd * 2 * c->L, nn * Bd * 2 * c->L * (4.0 * S + 16.0));
-            ks32_crt(c->d_uk, cf, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, mac_form, c->stream);
+            const bool fpc = c->ks_fpc && m <= (use_wide ? c->kw.fpc_max : c->ks32_fpc_max);
+            ks32_crt(c->d_uk, cf, 2L * c->L * c->n, (int)Bd, c->L, S, c->logn, kst, p32, c->d_primes, mac_form, c->stream,
+                     fpc);
         }
         CHECK_LAUNCH();
     }
@@ -3007,7 +3044,8 @@ extern "C" int exacto_bfv_apply_automorphism_dev(exacto_ctx* c, const uint64_t* 
             CHECK_LAUNCH();
             ks32_digits(c->ws_D16, c->ws_DS, cnt, guse, kb.S, c->logn, kb.d_p32, kb.mac_form, c->stream);
             ks32_mac(c->ws_DS, c->d_gk_rs, c->ws_U, cnt, guse, L, kb.S, n, kb.d_p32, kb.mac_form, c->stream);
-            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, kb.S, c->logn, kb.d_kst, kb.d_p32, c->d_primes, kb.mac_form, c->stream);
+            ks32_crt(c->ws_U, c->ws_T, 2 * Ln, cnt, L, kb.S, c->logn, kb.d_kst, kb.d_p32, c->d_primes, kb.mac_form, c->stream,
+                     c->ks_fpc && kb.fpc_max >= 1);
             CHECK_LAUNCH();
             NttBatch rb{};
             rb.src = c->ws_T; rb.src_item_stride = 2 * Ln;

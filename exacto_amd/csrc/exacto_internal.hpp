@@ -106,6 +106,9 @@ struct Prime32 {
     uint32_t last_w, last_ws;   // psi_inv_rev[1] n^-1 (fused last inverse stage)
     uint32_t c32, c32s;         // 2^32 mod p
     uint32_t k63;               // (-2^63) mod p
+    uint32_t fn_inv, fn_inv_s;  // n^-1 pi and last_w pi, pi = (P / p)^-1 mod p: the float-CRT lift's
+    uint32_t flast_w, flast_ws; // inverse transforms fold its CRT factor into the last stage
+    double inv_p;               // fl(1 / p)
     const uint2* tw_fwd;        // [n] {psi^brv(i), Shoup}
     const uint2* tw_inv;        // [n] {psi^-brv(i), Shoup}
 };
@@ -116,6 +119,8 @@ struct Ks32Tables {
     u64 pref_w[EXACTO_MAX_L][EXACTO_KS32_MAXS];           // (p_0 ... p_{s-1}) mod q_l
     u64 pref_ws[EXACTO_MAX_L][EXACTO_KS32_MAXS];
     u64 negP[EXACTO_MAX_L];                               // (q_l - P mod q_l) mod q_l
+    uint32_t fpc_c[EXACTO_MAX_L][EXACTO_KS32_MAXS][2];     // (P / p_s) mod q_l in two 30-bit halves
+    uint32_t fpc_n[EXACTO_MAX_L][2];                       // negP[l] in two 30-bit halves
 };
 // int16 digits [items][G][n] -> DS [items][G][S][n], NTT mod p_s
 // form: the basis' butterfly form, 0 primes up to 2^31, 1 below 2^32 / 3, 2 below 2^30 (lazy)
@@ -133,8 +138,10 @@ void ks32_key_norms(const u64* K, u64* out, long rows, int L, int n, const Prime
 void ks32_mac(const uint32_t* DS, const uint32_t* RS, uint32_t* U, int items, int G, int L, int S, int n,
               const Prime32* primes, int mac_form, hipStream_t st);
 // R[item][c][l] += centred lift of INTT(U[item][c][l][.]) mod q_l (every q_l = 2^60 - d, d < 2^24)
+// fpc: the lift by a rounded float sum (ks32_dev.hpp ks32_fpc_one; taken when S <= 3 or the primes are
+// below 2^32 / 3, and the caller checked the basis' fpc_max)
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
-              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st);
+              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st, bool fpc = false);
 
 // ---- kernels.hip launchers (all asynchronous on `s`) ----
 struct Operands {            // two degree-1 ciphertext sources, [2][L][n] per item

@@ -18,7 +18,7 @@
 //                            forward NTT -> RS [g][c][l][s][n] (once per key)
 //   ks32_mac_kernel        : U [item][c][l][s] = sum_g DS [item][g][s] (.) RS [g][c][l][s] mod p_s,
 //                            key slice staged in LDS, 64-bit lazy accumulation
-//   ks32_crt_kernel        : per (item, c, l): S inverse NTTs, centred Garner lift, + R[item][c][l]
+//   ks32_crt_kernel        : per (item, c, l): S inverse NTTs, centred Garner or float-CRT lift, + R[item][c][l]
 //                            mod q_l, written back into R (coefficient domain)
 #include "exacto_internal.hpp"
 #include "ks32_dev.hpp"
@@ -203,7 +203,7 @@ ks32_mac_kernel(const int* __restrict__ DS, const int* __restrict__ RS, uint32_t
     }
 }
 
-template <int LOGN, int S, bool LAZY>
+template <int LOGN, int S, bool LAZY, bool FPC>
 __global__ void __launch_bounds__((1 << LOGN) / 16)
 ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stride, int L,
                 const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
@@ -213,7 +213,7 @@ ks32_crt_kernel(const uint32_t* __restrict__ U, u64* __restrict__ R, long r_stri
     const int tid = threadIdx.x;
     const uint32_t b = blockIdx.x;             // (item, cl)
     u64 x[16];
-    ks32_crt_values<LOGN, S, LAZY>(x, U, R, r_stride, L, b, lds, tid, KT, primes, qprimes);
+    ks32_crt_values<LOGN, S, LAZY, FPC>(x, U, R, r_stride, L, b, lds, tid, KT, primes, qprimes);
     const uint32_t CL = 2 * L;
     const long item = b / CL;
     const __amdgpu_buffer_rsrc_t rd = poly_rsrc(R + item * r_stride + (long)(b - (uint32_t)item * CL) * N, N * 8);
@@ -307,14 +307,18 @@ static void ks32_launch_key(const u64* K, uint32_t* RS, long rows, int L, int S,
 
 template <int LOGN, bool LAZY>
 static void ks32_launch_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, const Ks32Tables* KT,
-                            const Prime32* primes, const PrimeConst* qprimes, hipStream_t st) {
+                            const Prime32* primes, const PrimeConst* qprimes, hipStream_t st, bool fpc) {
     const dim3 grid((unsigned)((long)items * 2 * L)), block((1 << LOGN) / 16);
-    if (S == 2)
-        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 2, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
-    else if (S == 3)
-        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 3, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
-    else
-        EXACTO_LAUNCH((ks32_crt_kernel<LOGN, 4, LAZY>), grid, block, 0, st, U, R, r_stride, L, KT, primes, qprimes);
+#define CRT_(S_, F_) EXACTO_LAUNCH((ks32_crt_kernel<LOGN, S_, LAZY, F_>), grid, block, 0, st, U, R, r_stride, L, KT, \
+                                   primes, qprimes)
+    if (S == 2) {
+        if (fpc) CRT_(2, true); else CRT_(2, false);
+    } else if (S == 3) {
+        if (fpc) CRT_(3, true); else CRT_(3, false);
+    } else {
+        if (fpc) CRT_(4, true); else CRT_(4, false);
+    }
+#undef CRT_
 }
 
 #define KS32_SWITCH(logn, CALL)                  \
@@ -409,12 +413,13 @@ void ks32_digit_sum(const void* D, bool in8, int npairs, const int* term_start, 
 }
 
 void ks32_crt(const uint32_t* U, u64* R, long r_stride, int items, int L, int S, int logn, const Ks32Tables* KT,
-              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st) {
+              const Prime32* primes, const PrimeConst* qprimes, int form, hipStream_t st, bool fpc) {
     if (items <= 0) return;
-#define CALL(L_)                                                                                           \
-    do {                                                                                                   \
-        if (form == F32_LAZY) ks32_launch_crt<L_, true>(U, R, r_stride, items, L, S, KT, primes, qprimes, st); \
-        else ks32_launch_crt<L_, false>(U, R, r_stride, items, L, S, KT, primes, qprimes, st);                \
+    fpc = fpc && (S <= 3 || form != F32_WIDE);   // ks32_fpc_one's 64-bit sums
+#define CALL(L_)                                                                                                \
+    do {                                                                                                        \
+        if (form == F32_LAZY) ks32_launch_crt<L_, true>(U, R, r_stride, items, L, S, KT, primes, qprimes, st, fpc); \
+        else ks32_launch_crt<L_, false>(U, R, r_stride, items, L, S, KT, primes, qprimes, st, fpc);                \
     } while (0)
     KS32_SWITCH(logn, CALL)
 #undef CALL

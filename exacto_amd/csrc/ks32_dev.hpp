@@ -196,12 +196,15 @@ __device__ __forceinline__ void fwd32_store(uint32_t (&x)[16], uint32_t* lds, in
 // min-subtraction and U + 2p - V < 4p goes to the Shoup product as is (9 VALU per butterfly);
 // otherwise both inputs are first reduced to [0, p) (11 VALU).  Outputs below 2p, the last stage's
 // canonical.
-// OUT2P (lazy only): the last stage's outputs stay in [0, 2p) (the Garner terms of ks32_lift_one
-// for s >= 1 take them unreduced)
-template <int LOGN, int LO, int BLO, int BHI, bool LAZY, bool OUT2P = false>
+// OUT2P: the last stage's outputs stay in [0, 2p) (the Garner terms of ks32_lift_one for s >= 1 take
+// them unreduced, the float-CRT lift all of them).  FOLD: the last stage multiplies by n^-1 pi
+// instead of n^-1 (Prime32::fn_inv, the float-CRT lift's CRT factor).
+template <int LOGN, int LO, int BLO, int BHI, bool LAZY, bool OUT2P = false, bool FOLD = false>
 __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Prime32& P) {
     constexpr int N = 1 << LOGN;
     const uint32_t p = P.p, p2 = 2 * p;
+    const uint32_t ni = FOLD ? P.fn_inv : P.n_inv, nis = FOLD ? P.fn_inv_s : P.n_inv_s;
+    const uint32_t lw = FOLD ? P.flast_w : P.last_w, lws = FOLD ? P.flast_ws : P.last_ws;
     const Tw32 twi = tw32(P.tw_inv);
     const int thigh = (LO + 4 >= LOGN) ? 0 : (tid >> LO);
 #pragma unroll
@@ -218,8 +221,8 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
                 if constexpr (LAZY) {
                     const uint32_t U = x[k0], V = x[k1];
                     if (b == LOGN - 1) {  // n^-1 folded in, canonical (OUT2P: below 2p)
-                        x[k0] = shoup32(U + V, P.n_inv, P.n_inv_s, p);
-                        x[k1] = shoup32(U + p2 - V, P.last_w, P.last_ws, p);
+                        x[k0] = shoup32(U + V, ni, nis, p);
+                        x[k1] = shoup32(U + p2 - V, lw, lws, p);
                         if constexpr (!OUT2P) {
                             x[k0] = red32(x[k0], p);
                             x[k1] = red32(x[k1], p);
@@ -231,9 +234,13 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
                     }
                 } else {
                     const uint32_t U = red32(x[k0], p), V = red32(x[k1], p);
-                    if (b == LOGN - 1) {  // n^-1 folded in, canonical
-                        x[k0] = red32(shoup32(U + V, P.n_inv, P.n_inv_s, p), p);
-                        x[k1] = red32(shoup32(U + p - V, P.last_w, P.last_ws, p), p);
+                    if (b == LOGN - 1) {  // n^-1 folded in, canonical (OUT2P: below 2p)
+                        x[k0] = shoup32(U + V, ni, nis, p);
+                        x[k1] = shoup32(U + p - V, lw, lws, p);
+                        if constexpr (!OUT2P) {
+                            x[k0] = red32(x[k0], p);
+                            x[k1] = red32(x[k1], p);
+                        }
                     } else {
                         x[k0] = U + V;
                         x[k1] = shoup32(U + p - V, t.x, t.y, p);
@@ -244,7 +251,7 @@ __device__ __forceinline__ void inv32_round(uint32_t (&x)[16], int tid, const Pr
     }
 }
 
-template <int LOGN, int R, bool LAZY, bool OUT2P = false>
+template <int LOGN, int R, bool LAZY, bool OUT2P = false, bool FOLD = false>
 __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, int tid, const Prime32& P) {
     constexpr int LO = (4 * R) < (LOGN - 4) ? 4 * R : LOGN - 4;
     constexpr int BLO = 4 * R;
@@ -256,8 +263,8 @@ __device__ __forceinline__ void inv32_rounds(uint32_t (&x)[16], uint32_t* lds, i
         lds_sync();
         lds32_load<LO>(lds, x, tid);
     }
-    inv32_round<LOGN, LO, BLO, BHI, LAZY, OUT2P>(x, tid, P);
-    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY, OUT2P>(x, lds, tid, P);
+    inv32_round<LOGN, LO, BLO, BHI, LAZY, OUT2P, FOLD>(x, tid, P);
+    if constexpr (BHI < LOGN - 1) inv32_rounds<LOGN, R + 1, LAZY, OUT2P, FOLD>(x, lds, tid, P);
 }
 
 // One coefficient's centred Garner lift of its S residues v[s] (canonical mod p_s) evaluated mod
@@ -303,12 +310,45 @@ __device__ __forceinline__ u64 ks32_lift_one(const uint32_t (&v)[S], u64 r, cons
     return reduce_near60(t + r, q);                                        // t + r < 2^62
 }
 
+// The same lift by a rounded float sum (S <= 3, or S = 4 below 2^32 / 3).  y_s = u pi_s mod p_s, below 2 p_s (the inverse
+// transforms' FOLD + OUT2P form, pi_s = (P / p_s)^-1 mod p_s), so sum_s y_s (P / p_s) = u_c + alpha P
+// with u_c the centred residue and alpha = round(sum_s y_s / p_s) in [0, 2S]: the float sum of the
+// y_s fl(1 / p_s) is within 2^-48 of the exact one and |u_c| / P < 1/2 - 2^-21 (the host's margin:
+// the basis' fpc_max), so the rounding is exact.  Mod q = 2^60 - d:
+//   sum_s y_s C_s + alpha negP, C_s = (P / p_s) mod q, negP = q - P mod q,
+// with C_s and negP in 30-bit halves: A0 = sum y_s C_s,lo + alpha negP_lo < S 2 p_max 2^30 + 2^33
+// (< 3 2^62 at S = 3, p < 2^31; < 2^63.42 at S = 4, p < 2^32 / 3), A1 likewise, value = A0 + A1 2^30,
+// A1 2^30 = (A1 mod 2^30) 2^30 + (A1 >> 30) 2^60 and 2^60 == d.
+// 8 multiply-adds for the products against the Garner form's 3 Shoup products, mixed-radix compare
+// and 2 Horner folds.
+template <int S>
+__device__ __forceinline__ u64 ks32_fpc_one(const uint32_t (&y)[S], u64 r, const double (&ip)[S],
+                                            const uint32_t (&c0)[S], const uint32_t (&c1)[S], uint32_t n0,
+                                            uint32_t n1, u64 q, uint32_t dq) {
+    static_assert(S <= 4, "A0, A1 < 2^64: S <= 3, or S = 4 with p < 2^32 / 3 (ks32_crt)");
+    double f = (double)y[0] * ip[0];
+#pragma unroll
+    for (int s = 1; s < S; ++s) f = __builtin_fma((double)y[s], ip[s], f);
+    const uint32_t al = (uint32_t)__builtin_rint(f);
+    u64 a0 = (u64)al * n0, a1 = (u64)al * n1;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        a0 += (u64)y[s] * c0[s];
+        a1 += (u64)y[s] * c1[s];
+    }
+    const u64 h = a1 >> 30;                                               // < 2^34
+    const u64 l30 = (a1 & ((1ull << 30) - 1)) << 30;                      // < 2^60
+    const u64 t = a0 + l30 + (u64)(uint32_t)h * dq + ((u64)((uint32_t)(h >> 32) * dq) << 32);  // < 2^63.72
+    return reduce_near60(t + r, q);                                       // t + r < 2^63.83 (S = 4: 2^63.55)
+}
+
 // Per (item, c, l) = block b: the S accumulated rows -> inverse NTT mod p_s -> centred Garner lift ->
 // R[item][c][l] + lift mod q_l, returned in x (element k T + tid in x[k], canonical; R canonical,
 // coefficient domain).  The lift mod q = 2^60 - d is a Horner evaluation x = a_0 + p_0 (a_1 + p_1
 // (a_2 + ...)) whose every step folds the 92-bit product through 2^60 == d (5 instructions); the
 // centring (x > floor(P/2)) is decided on the mixed-radix digits and adds q - (P mod q).
-template <int LOGN, int S, bool LAZY>
+// FPC: ks32_fpc_one instead.
+template <int LOGN, int S, bool LAZY, bool FPC = false>
 __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __restrict__ U, const u64* __restrict__ R,
                                                 long r_stride, int L, uint32_t b, uint32_t* lds, int tid,
                                                 const Ks32Tables* __restrict__ KT, const Prime32* __restrict__ primes,
@@ -325,9 +365,40 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
         const __amdgpu_buffer_rsrc_t rs = poly_rsrc(U + ((long)b * S + s) * N, N * 4);
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[s][k] = buf_ld32(rs, tid * 4, k * T * 4);
-        // s >= 1 (lazy): residues in [0, 2p), which the Garner terms take as they are
-        if (s == 0) inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
+        // s >= 1 (lazy): residues in [0, 2p), which the Garner terms take as they are; the float-CRT
+        // lift takes every residue below 2p, its CRT factor folded into the last stage
+        if constexpr (FPC) inv32_rounds<LOGN, 0, LAZY, true, true>(v[s], lds, tid, primes[s]);
+        else if (s == 0) inv32_rounds<LOGN, 0, LAZY>(v[s], lds, tid, primes[s]);
         else inv32_rounds<LOGN, 0, LAZY, LAZY>(v[s], lds, tid, primes[s]);
+    }
+    // element k*T + tid of every row is in v[s][k]
+    const u64 q = qprimes[l].q;
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+    const __amdgpu_buffer_rsrc_t rr = poly_rsrc(R + item * r_stride + (long)cl * N, N * 8);
+    if constexpr (FPC) {
+        // the residues pass through an empty asm here, so the float sum's conversions are not hoisted
+        // into the later primes' transforms (16 doubles live per prime: 151 VGPRs, 3 waves per SIMD)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[s][k]));
+        double ip[S];
+        uint32_t c0[S], c1[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            ip[s] = primes[s].inv_p;
+            c0[s] = KT->fpc_c[l][s][0];
+            c1[s] = KT->fpc_c[l][s][1];
+        }
+        const uint32_t n0 = KT->fpc_n[l][0], n1 = KT->fpc_n[l][1];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint32_t vk[S];
+#pragma unroll
+            for (int s = 0; s < S; ++s) vk[s] = v[s][k];
+            x[k] = ks32_fpc_one<S>(vk, buf_ld64(rr, tid * 8, k * T * 8), ip, c0, c1, n0, n1, q, dq);
+        }
+        return;
     }
     uint32_t pr[S], hp[S];
 #pragma unroll
@@ -335,11 +406,7 @@ __device__ __forceinline__ void ks32_crt_values(u64 (&x)[16], const uint32_t* __
         pr[s] = primes[s].p;
         hp[s] = KT->halfP[s];
     }
-    // element k*T + tid of every row is in v[s][k]
-    const u64 q = qprimes[l].q;
-    const uint32_t dq = (uint32_t)((1ull << 60) - q);
     const u64 negP = KT->negP[l];
-    const __amdgpu_buffer_rsrc_t rr = poly_rsrc(R + item * r_stride + (long)cl * N, N * 8);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         uint32_t vk[S];
