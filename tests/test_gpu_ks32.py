@@ -41,6 +41,8 @@ def _params(which, n):
         return P.cfg3_params(n)
     if which == "q2":
         return P.BfvParamsBuilder().ring_degree(n).plain_modulus(65537).ct_moduli(P.Q3[1:]).build()
+    if which == "q4b16":   # four limbs at base 2^16: a four-prime 31-bit basis (ks32_crt's S = 4 kernels)
+        return P.BfvParamsBuilder().ring_degree(n).plain_modulus(65537).ct_moduli(P.Q4).build()
     return P.cfg5_params(n).bfv_params
 
 
@@ -51,6 +53,7 @@ def _params(which, n):
     (8192, "cfg5", 2, None, 0),
     (2048, "cfg3", 3, None, 0),        # the remaining transform lengths of the 31-bit basis
     (16384, "q2", 1, None, 0),         # n = 16384: cfg3's last two primes (== 1 mod 2^15)
+    (8192, "q4b16", 2, None, 0),
 ])
 def test_ks32_matches_limbwise_mac(gpu_available, n, which, B, keys, chunk):
     prm = _params(which, n)
@@ -64,6 +67,8 @@ def test_ks32_matches_limbwise_mac(gpu_available, n, which, B, keys, chunk):
     for ks in (True, False):
         ctx = _ctx(prm, ks, chunk)
         assert (ctx.ks32_primes > 0) == ks       # the 31-bit basis is in use exactly when asked
+        if ks and which == "q4b16":
+            assert ctx.ks32_primes == 4
         ctx.load_relin_key(rlk)
         outs.append(ctx.bfv_mul_and_relin(ct1, ct2))
     assert np.array_equal(outs[0], outs[1])
@@ -93,6 +98,7 @@ def test_ks32_key_reload(gpu_available):
     (4096, "cfg3", 5, None, 2),        # 3 chunks
     (4096, "cfg3", 2, 5, 0),           # fewer Galois key digits than G (eval.rs:540-548)
     (8192, "cfg5", 2, None, 0),
+    (8192, "q4b16", 2, None, 0),
 ])
 def test_ks32_automorphism_matches_limbwise(gpu_available, n, which, B, keys, chunk):
     """bfv_apply_automorphism (eval.rs:512-561) with the ks32 key switch against the limb-wise

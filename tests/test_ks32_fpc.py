@@ -5,7 +5,7 @@ gives u = sum_s y_s (P / p_s) - alpha P exactly for every |u| <= m `one` that th
 (P 2^20 > (2 m one + 1)(2^20 + 1)) admits, and the kernel's 30-bit-split evaluation mod q = 2^60 - d
 stays below 2^64 and equals u + r mod q.  At the three 31-bit bases the context builds (narrow primes
 below 2^32 / 3, wide below 2^31, lazy below 2^30) for the cfg3 / cfg4 / cfg5 parameters, with `one`
-pushed to the margin's limit (cfg5's narrow and lazy bases have four primes).
+pushed to the margin's limit; and four narrow / lazy primes (cfg5's ring at base 2^16).
 
 A Python restatement of the device arithmetic (each fp64 operation correctly rounded, as gfx950's
 v_cvt_f64_u32 / v_mul_f64 / v_fma_f64 are), not the kernel."""
@@ -18,8 +18,9 @@ import pytest
 from test_fpc_crt import Q3, Q4, is_prime
 
 M64 = (1 << 64) - 1
-# (n, G, gadget base, ciphertext primes): cfg3 / cfg4 (the same ring) and cfg5
-CONFIGS = {"cfg3": (4096, 12, 1 << 16, Q3), "cfg5": (8192, 15, 1 << 16, Q4)}
+# (n, G, gadget base, ciphertext primes): cfg3 / cfg4 (the same ring), cfg5 (base 256, oracle/params.py
+# cfg5_params), and a four-prime case (cfg5's ring at base 2^16: the S = 4 kernels)
+CONFIGS = {"cfg3": (4096, 12, 1 << 16, Q3), "cfg5": (8192, 30, 256, Q4), "s4": (8192, 15, 1 << 16, Q4)}
 
 
 def basis(n, pmax, bound, fixed_s=0):
