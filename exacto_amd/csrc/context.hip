@@ -277,6 +277,10 @@ struct exacto_ctx {
     int psum_max = 0;
     int psum_fp_max = 0;         // ... and with |sum| < P / 4, the rounded-float CRT over P (kernels.hip fpc_lift)
     bool fp_crt = true;          // EXACTO_FP_CRT=0: Garner over P in the SP scale kernels (A/B)
+    // the scale kernels' s = [p T]_Q by a rounded float sum (with fp_crt; kernels.hip fpq_y) wherever
+    // |f - round(f)| <= fpq_lim.  EXACTO_FPQ=0: Garner over Q always; =2: a 1/4 band (half the
+    // coefficients take Garner: the fallback's bit-exact variant)
+    double fpq_lim = 0.5 - 0x1p-40;
     // HPS: the division-free scale (q > 2^32, p < min(q, 2^32); EXACTO_HPS_LITERAL=1: the literal i128
     // form, kept for the equivalence test) and, in dbfv_mul, the products' c0 / c1 and signed gadget
     // digits summed per output limb before ONE forward NTT + relinearisation MAC per limb
@@ -893,6 +897,19 @@ static int build_tables(exacto_ctx* c) {
             const u64 pm = P.mod(qv[i]);
             C.fpc_negP[i] = pm == 0 ? 0 : qv[i] - pm;
         }
+        for (int i = 0; i < L; ++i) {   // the FPQ constants (see CrtTables)
+            const u64 q = qv[i];
+            u64 qo = 1 % q;   // (Q / q_i) mod q_i
+            for (int k = 0; k < L; ++k)
+                if (k != i) qo = mulmod_h(qo, qv[k] % q, q);
+            set_shoup(C.fpq_pz_w[i], C.fpq_pz_ws[i], mulmod_h(c->plain % q, invmod_h(qo, q), q), q);
+            C.fpq_inv0[i] = 1.0 / (double)q;
+            C.fpq_inv1[i] = (double)(1ull << 30) / (double)q;
+            for (int a = 0; a < K; ++a) {
+                const u64 pa = pv[a], qi = invmod_h(q % pa, pa);
+                C.fpq_c[i][a] = mulmod_h((pa - qi) % pa, C.fpc_neg[a], pa);
+            }
+        }
     }
     {
         const u64 mx = *std::max_element(c->primes.begin(), c->primes.end());
@@ -1101,6 +1118,7 @@ extern "C" int exacto_ctx_create(exacto_ctx** out, size_t n, const uint64_t* ct_
     if (const char* e = getenv("EXACTO_PSUM")) c->psum_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_CHAIN_SPLIT")) c->batch_split = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_FP_CRT")) c->fp_crt = atoi(e) != 0;
+    if (const char* e = getenv("EXACTO_FPQ")) c->fpq_lim = atoi(e) == 0 ? 0.0 : atoi(e) == 2 ? 0.25 : c->fpq_lim;
     if (const char* e = getenv("EXACTO_KS_FPC")) c->ks_fpc = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_DIGIT8")) c->digit8_env = atoi(e) != 0;
     if (const char* e = getenv("EXACTO_HPS_SUM")) c->hps_sum_env = atoi(e) != 0;
@@ -1678,7 +1696,7 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
                                                   : c->ws_D16)
                                    : nullptr,
                                guse, cnt, n, c->d_crt, c->d_primes, L, K, crt_mode(c),
-                               c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8, c->fp_crt);
+                               c->stream, c->h_crt.gshift, ps.on, c->ks_defer && c->ks_defer8, c->fp_crt, c->fpq_lim);
         CHECK_LAUNCH();
         }
         if (ps.on) {   // ... and their scale: the output limbs' c0 / c1, coefficient domain
@@ -1689,7 +1707,8 @@ static int run_mul(exacto_ctx* c, const Operands& op, long P, u64* out, long out
             ProfScope pq(c, PK_PSUM_SCALE, (u64)(cnt / ps.npairs) * ps.d,
                          ib * 2.0 * n * 8.0 * (ps.d * (double)(K + L) + (double)ps.npairs * L));
             if (!launch_psum_scale(c->ws_T, c->ws_extP, ps.out + item0 * ps.d * 2 * Ln, cnt / ps.npairs, ps.d, ps.npairs,
-                                   ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream, ps.fpc))
+                                   ps.term_start, ps.terms, n, c->d_crt, c->d_primes, L, c->stream, ps.fpc,
+                                   c->fpq_lim))
                 return fail(EXACTO_ERR_HIP, "internal: psum scale not available for these limbs");
             CHECK_LAUNCH();
         }

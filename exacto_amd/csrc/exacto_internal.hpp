@@ -65,6 +65,12 @@ struct CrtTables {
     double fpc_inv[EXACTO_MAX_K];                // 1 / p_a
     u64 fpc_pm[EXACTO_MAX_K][EXACTO_MAX_L];      // (P / p_a) mod q_i
     u64 fpc_negP[EXACTO_MAX_L];                  // (q_i - P mod q_i) mod q_i
+    // FPQ: the centred s = [p T]_Q by a rounded float sum too (kernels.hip fpq_y): with
+    // z_i = T_i p (Q / q_i)^-1 mod q_i, s = sum_i z_i (Q / q_i) - round(sum_i z_i / q_i) Q, and in p_a
+    // y_a = T_a fpc_pq[a] + sum_i z_i fpq_c[i][a] + beta fpc_neg[a]
+    u64 fpq_pz_w[EXACTO_MAX_L], fpq_pz_ws[EXACTO_MAX_L];  // p (Q / q_i)^-1 mod q_i (Shoup)
+    double fpq_inv0[EXACTO_MAX_L], fpq_inv1[EXACTO_MAX_L]; // fl(1 / q_i), fl(2^30 / q_i)
+    u64 fpq_c[EXACTO_MAX_L][EXACTO_MAX_K];                 // (p_a - q_i^-1 mod p_a) Pi_a
     int near;       // max prime < 2 * min prime: residues move between primes by one conditional subtraction
     int fast;       // near and every prime < 2^60: lazy CRT kernels (unreduced Shoup sums)
     int special;    // fast and every prime is 2^60 - d, d < 2^24: reduce_near60 instead of reduce64
@@ -197,7 +203,9 @@ bool exact_scale_sp_ok(int L, int K, int mode);
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
                         int K, int mode, hipStream_t s, int gshift = -1, bool c2only = false,
-                        bool digits8 = false, bool fpc = false);
+                        bool digits8 = false, bool fpc = false, double fpq_lim = 0.0);
+// fpq_lim > 0 (with fpc): s = [p T]_Q centred by the float sum (fpq_y) wherever |f - round(f)| <= fpq_lim,
+// Garner over Q elsewhere (0.5 - 2^-40: exact; smaller values only send more coefficients to Garner)
 // D: digits as residues mod q [item][g][n]; D16 (instead): signed int16 (d8: int8) digits [item][g][n].
 // fast: q > 2^32 and p < min(q, 2^32): the division-free form (bit-identical to the literal one)
 void launch_hps_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, void* D16, bool d8, int guse,
@@ -243,7 +251,7 @@ void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int n
                          const CombineTerm* terms, int L, int K, int n, const PrimeConst* primes, hipStream_t s);
 bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                       hipStream_t s, bool fpc = false);
+                       hipStream_t s, bool fpc = false, double fpq_lim = 0.0);
 // dBFV: int16 gadget digits of the products of one output limb summed (combine terms with
 // coefficient 1): D [item][pair][gu][n] -> out [item][k][gu][n], int16 or (wide) int32
 // D: int16 digits, or int8 when in8 (base <= 2^8, exact_scale's digits8)

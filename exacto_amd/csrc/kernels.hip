@@ -563,21 +563,14 @@ __device__ __forceinline__ void fpc_lift(const u64 (&y)[LT + 1], u64 (&res)[EXAC
     }
 }
 
-// SP, K = L + 1: exact_scale_kernel with every modular dot product as a 30-bit-limb dot:
-//   r_a = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs        mod p_a   (then Garner over P)
-//   res_i = sum_a w_a (p_0 .. p_{a-1}) + negr (q_i - P mod q_i)    mod q_i
-// (FPC: y_a = r_a Pi_a by the same dots with folded constants, then fpc_lift), and int16 gadget
-// digits by gadget_digits16_sp.
-template <int LT, int DIG, bool FPC>
-__global__ void __launch_bounds__(TPB)
-exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
-                      u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n,
-                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes, int c2only) {
-    ROW_SETUP(n)
-    constexpr int L = LT, K = LT + 1, NP = L + K;
-    const long item = c2only ? row : row / 3;
-    const int comp = c2only ? 2 : (int)(row - item * 3);
-    const u64* Tin = T + (item * 3 + comp) * NP * n + j;
+// FPC's y_a from the ciphertext-prime residues T_i (i < L) and T_a: s = [p T]_Q centred by Garner over Q
+// (mixed-radix digits v, their comparison with floor(Q/2)), then
+//   y_a = T_a fpc_pq[a] + sum_k v_k fpc_qpq[k][a] + negs Pi_a   (mod p_a, in [0, p_a)).
+// `carry` (psum: the products' running sum, < p_a) is added to each y_a; T_a's term only when ta is set.
+template <int LT, bool TA>
+__device__ __forceinline__ void fpc_y_garner(const u64* __restrict__ Tin, int n, u64 (&y)[LT + 1],
+                                             const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+    constexpr int L = LT, K = LT + 1;
     u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
     for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
@@ -589,7 +582,96 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
         v0[k] = (uint32_t)v[k] & M30;
         v1[k] = (uint32_t)(v[k] >> 30);
     }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        // y[a] (TA: unused on entry; else the carry < p_a): a0's constant < 2^61, inside dot30_fold's budget
+        Dot30 A{(TA ? 0ull : y[a]) + (negs ? C->fpc_neg[a] : 0ull), 0, 0};
+        if constexpr (TA) {
+            const u64 ta = Tin[(long)(L + a) * n];   // [0, 2q) (the tensor's lazy last stage)
+            dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->fpc_pq[a]);
+        }
+#pragma unroll
+        for (int k = 0; k < L; ++k) dot30_mac(A, v0[k], v1[k], C->fpc_qpq[k][a]);
+        y[a] = dot30_fold(A, primes[L + a].q);
+    }
+}
+
+// FPQ: the same y_a with s centred by a rounded float sum.  z_i = T_i p (Q / q_i)^-1 mod q_i (one Shoup
+// product, as u_i was), f = sum_i z_i fl(1 / q_i) (z_i in 30-bit halves: exact doubles), beta = round(f):
+// sum_i z_i (Q / q_i) = s + beta Q with s the centred residue, |s| / Q = |f - beta| up to the float
+// error (< 2^-47 for L <= 6).  So beta is exact wherever |f - beta| <= 1/2 - 2^-40 (`lim`), and then
+//   y_a = T_a fpc_pq[a] + sum_i z_i fpq_c[i][a] + beta Pi_a,   fpq_c[i][a] = (-q_i^-1 mod p_a) Pi_a
+// (s Q^-1 = sum_i z_i q_i^-1 - beta).  Elsewhere (s within 2^-40 Q of +-Q/2; about 2^-39 of uniform
+// coefficients) the lane takes fpc_y_garner.  Replaces Garner over Q's L (L - 1) / 2 Shoup products and
+// the mixed-radix comparison with 2 L conversions and fused multiply-adds.
+template <int LT, bool TA>
+__device__ __forceinline__ void fpq_y(const u64* __restrict__ Tin, int n, u64 (&y)[LT + 1], const CrtTables* __restrict__ C,
+                                      const PrimeConst* __restrict__ primes, double lim) {
+    constexpr int L = LT, K = LT + 1;
+    uint32_t z0[L], z1[L];
+    double f = 0.0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const u64 z = shoup_mul_red(Tin[(long)i * n], C->fpq_pz_w[i], C->fpq_pz_ws[i], primes[i].q);
+        z0[i] = (uint32_t)z & M30;
+        z1[i] = (uint32_t)(z >> 30);
+        f = fma((double)z0[i], C->fpq_inv0[i], f);
+        f = fma((double)z1[i], C->fpq_inv1[i], f);
+    }
+    const double b = __builtin_rint(f);
+    if (__builtin_fabs(f - b) <= lim) {
+        const uint32_t beta = (uint32_t)b;   // 0 .. L
+#pragma unroll
+        for (int a = 0; a < K; ++a) {
+            Dot30 A{TA ? 0ull : y[a], 0, 0};
+            dot30_mac(A, beta, 0, C->fpc_neg[a]);     // < 2^33 in a0 and a1: not a full term
+            if constexpr (TA) {
+                const u64 ta = Tin[(long)(L + a) * n];
+                dot30_mac(A, (uint32_t)ta & M30, (uint32_t)(ta >> 30), C->fpc_pq[a]);
+            }
+#pragma unroll
+            for (int i = 0; i < L; ++i) dot30_mac(A, z0[i], z1[i], C->fpq_c[i][a]);
+            y[a] = dot30_fold(A, primes[L + a].q);
+        }
+    } else {
+        fpc_y_garner<LT, TA>(Tin, n, y, C, primes);
+    }
+}
+
+// SP, K = L + 1: exact_scale_kernel with every modular dot product as a 30-bit-limb dot:
+//   r_a = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs        mod p_a   (then Garner over P)
+//   res_i = sum_a w_a (p_0 .. p_{a-1}) + negr (q_i - P mod q_i)    mod q_i
+// (FPC: y_a = r_a Pi_a by the same dots with folded constants, then fpc_lift), and int16 gadget
+// digits by gadget_digits16_sp.
+template <int LT, int DIG, bool FPC, bool FPQ = false>
+__global__ void __launch_bounds__(TPB)
+exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_stride, int ncomp_r,
+                      u64* __restrict__ D, int16_t* __restrict__ D16, int guse, int n,
+                      const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes, int c2only,
+                      double fpq_lim = 0.0) {
+    ROW_SETUP(n)
+    constexpr int L = LT, K = LT + 1, NP = L + K;
+    const long item = c2only ? row : row / 3;
+    const int comp = c2only ? 2 : (int)(row - item * 3);
+    const u64* Tin = T + (item * 3 + comp) * NP * n + j;
     u64 res[EXACTO_MAX_L];
+    if constexpr (FPQ) {
+        static_assert(FPC, "FPQ feeds the float lift from P");
+        u64 y[K];
+        fpq_y<LT, true>(Tin, n, y, C, primes, fpq_lim);
+        fpc_lift<LT>(y, res, C, primes);
+    } else {
+    u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
+    garner_q_fast<LT>(v, u, L, C, primes);
+    const bool negs = mr_greater<EXACTO_MAX_L>(v, C->halfQ_mr, L);
+    uint32_t v0[L], v1[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) {
+        v0[k] = (uint32_t)v[k] & M30;
+        v1[k] = (uint32_t)(v[k] >> 30);
+    }
     if constexpr (FPC) {
         u64 y[K];
 #pragma unroll
@@ -636,6 +718,7 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
         res[i] = dot30_fold(A, q);
     }
     }
+    }   // FPQ
     if (comp < ncomp_r) {
         u64* out = R + item * r_stride + (long)comp * L * n + j;
 #pragma unroll
@@ -664,11 +747,11 @@ exact_scale_sp_kernel(const u64* __restrict__ T, u64* __restrict__ R, long r_str
 // lifts one r: the context checks m (p n Q + 2) < P (|R| < P / 2, psum_max).  Bit-identical to
 // summing the per-product results mod q_i (dbfv_combine_kernel), which is what it replaces.
 // row = (ib d + k) 2 + c; T as the tensor kernels leave it, Tsum [ib][k][c][a][n] (launch_dbfv_pairsum).
-template <int LT, bool FPC>
+template <int LT, bool FPC, bool FPQ = false>
 __global__ void __launch_bounds__(TPB)
 exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u64* __restrict__ out, int d, int npairs,
                      const int* __restrict__ term_start, const CombineTerm* __restrict__ terms, int n,
-                     const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes) {
+                     const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes, double fpq_lim = 0.0) {
     ROW_SETUP(n)
     constexpr int L = LT, K = LT + 1, NP = L + K;
     const int c = (int)(row & 1);
@@ -688,6 +771,11 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
     }
     for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
         const u64* Tin = T + ((ib * npairs + terms[t].pair) * 3 + c) * (long)NP * n + j;
+        if constexpr (FPQ) {   // carry[a] += this product's s part, by the float sum (Garner near +-Q/2)
+            static_assert(FPC, "FPQ feeds the float lift from P");
+            fpq_y<LT, false>(Tin, n, carry, C, primes, fpq_lim);
+            continue;
+        }
         u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
         for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);
@@ -745,15 +833,18 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
 
 bool launch_psum_scale(const u64* T, const u64* Tsum, u64* out, int items_b, int d, int npairs, const int* term_start,
                        const CombineTerm* terms, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                       hipStream_t s, bool fpc) {
+                       hipStream_t s, bool fpc, double fpq_lim) {
     const long blocks = (long)items_b * d * 2 * blocks_per_row(n);
     if (blocks == 0) return true;
 #define PSUM_(LT)                                                                                                   \
     do {                                                                                                            \
-        if (fpc) EXACTO_LAUNCH((exact_psum_sp_kernel<LT, true>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d,    \
-                               npairs, term_start, terms, n, ct, primes);                                          \
+        if (fpc && fpq_lim > 0.0)                                                                                   \
+            EXACTO_LAUNCH((exact_psum_sp_kernel<LT, true, true>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d,   \
+                          npairs, term_start, terms, n, ct, primes, fpq_lim);                                      \
+        else if (fpc) EXACTO_LAUNCH((exact_psum_sp_kernel<LT, true>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out,  \
+                                    d, npairs, term_start, terms, n, ct, primes, 0.0);                             \
         else EXACTO_LAUNCH((exact_psum_sp_kernel<LT, false>), dim3(blocks), dim3(TPB), 0, s, T, Tsum, out, d,       \
-                           npairs, term_start, terms, n, ct, primes);                                              \
+                           npairs, term_start, terms, n, ct, primes, 0.0);                                         \
     } while (0)
     switch (L) {
         case 1: PSUM_(1); break;
@@ -772,7 +863,8 @@ bool exact_scale_sp_ok(int L, int K, int mode) { return mode == 3 && K == L + 1 
 
 void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D, int16_t* D16, int guse,
                         int items, int n, const CrtTables* ct, const PrimeConst* primes, int L,
-                        int K, int mode, hipStream_t s, int gshift, bool c2only, bool digits8, bool fpc) {
+                        int K, int mode, hipStream_t s, int gshift, bool c2only, bool digits8, bool fpc,
+                        double fpq_lim) {
     const long blocks = (long)items * (c2only ? 1 : 3) * blocks_per_row(n);
     if (blocks == 0) return;
     if (mode == 3 && K == L + 1 && L >= 1 && L <= 6 && use_dot30()) {
@@ -781,10 +873,13 @@ void launch_exact_scale(const u64* T, u64* R, long r_stride, int ncomp_r, u64* D
                         : (D16 != nullptr && gshift > 0 && 32 % gshift == 0) ? (digits8 && gshift <= 8 ? 3 : 1) : 2;
 #define SCALE30_(LT, DG)                                                                                        \
     do {                                                                                                        \
-        if (fpc) EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, true>), dim3(blocks), dim3(TPB), 0, s, T, R,      \
-                               r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0);                 \
+        if (fpc && fpq_lim > 0.0)                                                                               \
+            EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, true, true>), dim3(blocks), dim3(TPB), 0, s, T, R,     \
+                          r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0, fpq_lim);             \
+        else if (fpc) EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, true>), dim3(blocks), dim3(TPB), 0, s, T, R, \
+                               r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0, 0.0);            \
         else EXACTO_LAUNCH((exact_scale_sp_kernel<LT, DG, false>), dim3(blocks), dim3(TPB), 0, s, T, R,         \
-                           r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0);                     \
+                           r_stride, ncomp_r, D, D16, guse, n, ct, primes, c2only ? 1 : 0, 0.0);                \
     } while (0)
 #define SCALE30(LT)                         \
     do {                                    \

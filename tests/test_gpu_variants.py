@@ -46,6 +46,10 @@ VARIANTS = {
     "psum_off": ({"EXACTO_PSUM": "0"}, ["cfg4", "cfg5"]),
     # Garner over P instead of the rounded-float CRT in the SP scale and psum kernels
     "fp_crt_off": ({"EXACTO_FP_CRT": "0"}, ["cfg3", "cfg4", "cfg5"]),
+    # Garner over Q for s = [p T]_Q in those kernels, and the float sum with a 1/4 band (about half the
+    # coefficients then take the Garner fallback inside the same launch)
+    "fpq_off": ({"EXACTO_FPQ": "0"}, ["cfg3", "cfg4", "cfg5"]),
+    "fpq_band": ({"EXACTO_FPQ": "2"}, ["cfg3", "cfg4", "cfg5"]),
     # ... and in the 31-bit key switch's lift (ks32_crt)
     "ks_fpc_off": ({"EXACTO_KS_FPC": "0"}, ["cfg3", "cfg4", "cfg5"]),
     # a dBFV batch (dbfv_mul, chain) on one stream instead of two halves (the twin context)
