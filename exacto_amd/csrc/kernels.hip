@@ -638,6 +638,68 @@ __device__ __forceinline__ void fpq_y(const u64* __restrict__ Tin, int n, u64 (&
     }
 }
 
+// psum (FPQ): one product's z_i (< q_i) added to the row's integer sums Z_i and its beta to bs; the dot over
+// the z_i is linear, so fpq_flush runs it once for every product summed.  A lane in the band adds its
+// product by Garner to carry instead.
+template <int LT>
+__device__ __forceinline__ void fpq_acc(const u64* __restrict__ Tin, int n, u64 (&Z)[LT], uint32_t& bs, u64 (&carry)[LT + 1],
+                                        const CrtTables* __restrict__ C, const PrimeConst* __restrict__ primes,
+                                        double lim) {
+    constexpr int L = LT;
+    u64 z[L];
+    double f = 0.0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        z[i] = shoup_mul_red(Tin[(long)i * n], C->fpq_pz_w[i], C->fpq_pz_ws[i], primes[i].q);
+        f = fma((double)((uint32_t)z[i] & M30), C->fpq_inv0[i], f);
+        f = fma((double)(uint32_t)(z[i] >> 30), C->fpq_inv1[i], f);
+    }
+    const double b = __builtin_rint(f);
+    if (__builtin_fabs(f - b) <= lim) {
+#pragma unroll
+        for (int i = 0; i < L; ++i) Z[i] += z[i];
+        bs += (uint32_t)b;
+    } else {
+        fpc_y_garner<LT, false>(Tin, n, carry, C, primes);
+    }
+}
+
+// carry[a] += sum_i Z_i fpq_c[i][a] + bs Pi_a (mod p_a), then Z = 0, bs = 0.  Z_i (at most 15 products:
+// < 15 q_i < 2^64) = r_i + k_i q_i with r_i < q_i, and q_i fpq_c[i][a] == -Pi_a, so the dot takes the
+// r_i and the k_i join beta with the opposite sign.
+template <int LT>
+__device__ __forceinline__ void fpq_flush(u64 (&Z)[LT], uint32_t& bs, u64 (&carry)[LT + 1], const CrtTables* __restrict__ C,
+                                          const PrimeConst* __restrict__ primes) {
+    constexpr int L = LT, K = LT + 1;
+    constexpr u64 M60 = (1ull << 60) - 1;
+    uint32_t z0[L], z1[L], ks = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        const u64 q = primes[i].q;
+        uint32_t kq = (uint32_t)(Z[i] >> 60);
+        u64 r = (Z[i] & M60) + (u64)kq * (uint32_t)((1ull << 60) - q);   // Z - kq q < 2^60 + 2^28 < 2q
+        if (r >= q) {
+            r -= q;
+            ++kq;
+        }
+        ks += kq;
+        z0[i] = (uint32_t)r & M30;
+        z1[i] = (uint32_t)(r >> 30);
+        Z[i] = 0;
+    }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+        const u64 pa = primes[L + a].q;
+        Dot30 A{carry[a], 0, 0};
+        dot30_mac(A, bs, 0, C->fpc_neg[a]);          // bs, ks < 2^7: not full terms
+        dot30_mac(A, ks, 0, pa - C->fpc_neg[a]);
+#pragma unroll
+        for (int i = 0; i < L; ++i) dot30_mac(A, z0[i], z1[i], C->fpq_c[i][a]);
+        carry[a] = dot30_fold(A, pa);
+    }
+    bs = 0;
+}
+
 // SP, K = L + 1: exact_scale_kernel with every modular dot product as a 30-bit-limb dot:
 //   r_a = T_a (p Q^-1) + sum_k v_k (p_a - qpq_k,a) + negs        mod p_a   (then Garner over P)
 //   res_i = sum_a w_a (p_0 .. p_{a-1}) + negr (q_i - P mod q_i)    mod q_i
@@ -769,13 +831,31 @@ exact_psum_sp_kernel(const u64* __restrict__ T, const u64* __restrict__ Tsum, u6
             carry[a] = dot30_fold(A, primes[L + a].q);
         }
     }
+    if constexpr (FPQ) {   // the products' s parts by the float sum (Garner near +-Q/2), one dot per row
+        static_assert(FPC, "FPQ feeds the float lift from P");
+        u64 Z[L];
+#pragma unroll
+        for (int i = 0; i < L; ++i) Z[i] = 0;
+        uint32_t bs = 0;
+        int cnt = 0;
+        for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+            fpq_acc<LT>(T + ((ib * npairs + terms[t].pair) * 3 + c) * (long)NP * n + j, n, Z, bs, carry, C, primes,
+                        fpq_lim);
+            if (++cnt == 15) {   // Z_i < 15 q_i < 2^64
+                fpq_flush<LT>(Z, bs, carry, C, primes);
+                cnt = 0;
+            }
+        }
+        fpq_flush<LT>(Z, bs, carry, C, primes);
+        u64 res[EXACTO_MAX_L];
+        fpc_lift<LT>(carry, res, C, primes);
+        u64* o = out + row * L * (long)n + j;
+#pragma unroll
+        for (int i = 0; i < L; ++i) o[(long)i * n] = res[i];
+        return;
+    }
     for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
         const u64* Tin = T + ((ib * npairs + terms[t].pair) * 3 + c) * (long)NP * n + j;
-        if constexpr (FPQ) {   // carry[a] += this product's s part, by the float sum (Garner near +-Q/2)
-            static_assert(FPC, "FPQ feeds the float lift from P");
-            fpq_y<LT, false>(Tin, n, carry, C, primes, fpq_lim);
-            continue;
-        }
         u64 u[EXACTO_MAX_L], v[EXACTO_MAX_L];
 #pragma unroll
         for (int i = 0; i < L; ++i) u[i] = shoup_mul(Tin[(long)i * n], C->pmod_w[i], C->pmod_ws[i], primes[i].q);

@@ -113,3 +113,50 @@ def test_fpq_boundary_goes_to_garner():
         x = s * pinv % Q
         _, f, b = fpq([x % q for q in qs], qs, c[3])
         assert abs(f - b) > LIM
+
+
+@pytest.mark.parametrize("cfg", ["cfg4", "cfg5"])
+def test_fpq_psum_deferred_dot(cfg):
+    """exact_psum_sp_kernel's FPQ form: the products' z_i summed as integers (up to 15, then flushed) and
+    their betas summed; fpq_flush reduces Z_i = r_i + k_i q_i and takes -k_i Pi_a with the betas.  Equal mod
+    every p_a to adding each product's own y_a contribution (the per-product dot it replaces)."""
+    n, p, qs = CONFIGS[cfg]
+    c = consts(n, p, qs)
+    ps, Q, pi, pz, fq = c[:5]
+    rng = random.Random(5)
+    for nprod in (0, 1, 2, 8, 15, 16, 31):
+        carry = [rng.randrange(pa) for pa in ps]
+        want = list(carry)
+        Z, bs, cnt = [0] * len(qs), 0, 0
+
+        def flush():
+            nonlocal Z, bs, carry
+            ks = 0
+            rr = []
+            for i, q in enumerate(qs):
+                kq = Z[i] >> 60
+                r = (Z[i] & ((1 << 60) - 1)) + kq * ((1 << 60) - q)
+                assert r < 2 * q
+                if r >= q:
+                    r, kq = r - q, kq + 1
+                assert Z[i] == r + kq * q
+                ks += kq
+                rr.append(r)
+            carry = [(carry[a] + bs * pi[a] + ks * (pa - pi[a]) + sum(r * fq[i][a] for i, r in enumerate(rr))) % pa
+                     for a, pa in enumerate(ps)]
+            Z, bs = [0] * len(qs), 0
+
+        for _ in range(nprod):
+            z, f, b = fpq([rng.randrange(q) for q in qs], qs, pz)
+            assert abs(f - b) <= LIM
+            for a, pa in enumerate(ps):
+                want[a] = (want[a] + sum(zi * fq[i][a] for i, zi in enumerate(z)) + int(b) * pi[a]) % pa
+            Z = [Zi + zi for Zi, zi in zip(Z, z)]
+            assert max(Z) < 1 << 64
+            bs += int(b)
+            cnt += 1
+            if cnt == 15:
+                flush()
+                cnt = 0
+        flush()
+        assert carry == want, (cfg, nprod)
