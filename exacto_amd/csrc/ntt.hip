@@ -14,6 +14,7 @@
 #include "exacto_internal.hpp"
 #include "ks32_dev.hpp"
 #include "bufmem.hpp"
+#include "crt_dev.hpp"
 
 namespace exacto {
 
@@ -1271,6 +1272,9 @@ static void launch_one(const NttBatch& nb, int count, bool inverse, bool lazy, c
 // p_a), so exact_psum_sp_kernel adds the per-product corrections to these sums.  Block = (ib, a, k)
 // x 256 coefficients (consecutive k of one (item, prime) back to back: they re-read the same
 // operands, from L2).
+#ifndef EXACTO_PAIRSUM_DOT
+#define EXACTO_PAIRSUM_DOT 1   // the pair sums as 30-bit-limb dots (A/B build switch; 0: a fold per product)
+#endif
 __global__ void __launch_bounds__(256)
 dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L, int K, int n,
                     const int* __restrict__ term_start, const CombineTerm* __restrict__ terms,
@@ -1282,9 +1286,40 @@ dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L
     const long r1 = row / d;
     const int a = (int)(r1 % K);
     const long ib = r1 / K;
-    const u64 q = primes[L + a].q, q2 = 2 * q;
-    const uint32_t dq = (uint32_t)((1ull << 60) - q);
+    const u64 q = primes[L + a].q;
     const long off_a = (long)a * n + j, off_k = (long)K * n;
+#if EXACTO_PAIRSUM_DOT
+    // the products as 30-bit-limb dots (crt_dev.hpp): operands canonical, so every limb product is below
+    // 2^60; c1 takes two products per pair, so the columns fold every 3 pairs (dot30_fold: at most 7
+    // products plus a canonical constant) instead of a 120-bit fold per product
+    Dot30 S0{0, 0, 0}, S1{0, 0, 0};
+    int cnt = 0;
+    for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
+        const long pr = ib * npairs + terms[t].pair;
+        const u64* EA = op.ea + (long)op.ea_off[pr] + off_a;
+        const u64* EB = op.eb + (long)op.eb_off[pr] + off_a;
+        u64 a0 = EA[0], a1 = EA[off_k], b0 = EB[0], b1 = EB[off_k];   // < 2q
+        a0 = a0 >= q ? a0 - q : a0;
+        a1 = a1 >= q ? a1 - q : a1;
+        b0 = b0 >= q ? b0 - q : b0;
+        b1 = b1 >= q ? b1 - q : b1;
+        const uint32_t a00 = (uint32_t)a0 & M30, a01 = (uint32_t)(a0 >> 30);
+        const uint32_t a10 = (uint32_t)a1 & M30, a11 = (uint32_t)(a1 >> 30);
+        dot30_mac(S0, a00, a01, b0);
+        dot30_mac(S1, a00, a01, b1);
+        dot30_mac(S1, a10, a11, b0);
+        if (++cnt == 3) {
+            S0 = Dot30{dot30_fold(S0, q), 0, 0};
+            S1 = Dot30{dot30_fold(S1, q), 0, 0};
+            cnt = 0;
+        }
+    }
+    u64* o = out + (((ib * d + k) * 2) * K + a) * (long)n + j;
+    o[0] = dot30_fold(S0, q);
+    o[(long)K * n] = dot30_fold(S1, q);
+#else
+    const u64 q2 = 2 * q;
+    const uint32_t dq = (uint32_t)((1ull << 60) - q);
     u64 s0 = 0, s1 = 0;                                // < 2q between terms (products < 2q)
     for (int t = term_start[k]; t < term_start[k + 1]; ++t) {
         const long pr = ib * npairs + terms[t].pair;
@@ -1302,6 +1337,7 @@ dbfv_pairsum_kernel(Operands op, u64* __restrict__ out, int d, int npairs, int L
     u64* o = out + (((ib * d + k) * 2) * K + a) * (long)n + j;
     o[0] = s0 >= q ? s0 - q : s0;
     o[(long)K * n] = s1 >= q ? s1 - q : s1;
+#endif
 }
 
 void launch_dbfv_pairsum(const Operands& op, u64* out, int items_b, int d, int npairs, const int* term_start,
